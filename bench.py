@@ -1,0 +1,214 @@
+"""bench.py -- sealed+checksummed throughput of the MI355X block-transform engine.
+
+Workload (BASELINE.json configs[1]): a device-resident batch of 4 MiB blocks,
+AES-256-GCM Seal fused with CRC32C "full" segment checksums, per-block keys
+and nonces, bit-exact to the reference's Go path (pkg/object/encrypt.go:192 +
+pkg/chunk/disk_cache.go:1218-1231).  One "step" = one jfsx_seal_batch over
+the whole batch (keysetup + transform + finalize + result copy-back).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--blocks B] [--mode seal|open|crc]
+
+For N > 1 it is launched by torch.distributed.run, one rank per GPU; blocks
+shard across ranks with no collective on the data path (the only collectives
+are the timing barrier and the max-over-ranks reduction).  Rank 0 prints ONE
+JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+SEED = 0x4A465321
+BLOCK = 4 << 20
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--blocks", type=int, default=16384, help="4 MiB blocks per GPU (16384 = 64 GiB)")
+    ap.add_argument("--block-bytes", type=int, default=BLOCK)
+    ap.add_argument("--mode", choices=["seal", "open", "crc"], default="seal")
+    ap.add_argument("--algo", choices=["aes256gcm", "chacha20poly1305"], default="aes256gcm")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--verify", type=int, default=4, help="blocks re-checked against the oracle after timing")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        dist = tdist
+    return world, rank, local, dist
+
+
+def barrier(dist):
+    if dist is not None:
+        dist.barrier()
+
+
+def max_over_ranks(dist, x, local):
+    if dist is None:
+        return x
+    import torch
+    dev = "cuda:%d" % local if torch.cuda.is_available() else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_baseline(args):
+    """The oracle's AES-NI/PCLMUL + SSE4.2 port of the Go path, timed on this
+    host's cores over a bounded sample of the same workload."""
+    from oracle import oracle as orc
+    threads = min(16, len(os.sched_getaffinity(0)))
+    algo = orc.AES256GCM if args.algo == "aes256gcm" else orc.CHACHA20P1305
+    nblk = 256  # 1 GiB: BASELINE.json configs[0]
+    secs, _ = orc.bench_seal_crc(algo, threads, nblk, BLOCK, SEED)
+    reps = max(1, min(64, int(args.cpu_seconds / max(secs, 1e-3))))
+    total_s, total_b = 0.0, 0
+    for r in range(reps):
+        s, _ = orc.bench_seal_crc(algo, threads, nblk, BLOCK, SEED + r)
+        total_s += s
+        total_b += nblk * BLOCK
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(total_b / total_s / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": "%d x 1 GiB (256 x 4 MiB blocks) %s seal + CRC32C full, %d threads, %s" %
+                      (reps, args.algo, threads, model)}
+
+
+def main():
+    args = parse()
+    world, rank, local, dist = dist_setup(args)
+    from juicefs_amd import engine as E
+
+    eng = E.Engine(local)
+    nb, L = args.blocks, args.block_bytes
+    algo = E.AES256GCM if args.algo == "aes256gcm" else E.CHACHA20P1305
+    nseg = -(-L // E.SEG)
+    src = eng.alloc(nb * L)
+    dst = eng.alloc(nb * L) if args.mode != "crc" else None
+    crc = eng.alloc(nb * 4 * nseg)
+    base = rank * nb  # global block index: blocks shard across ranks
+    for b in range(nb):
+        eng.gen_synthetic(src, L, SEED, base + b, offset=b * L)
+    eng.sync()
+
+    if args.mode == "crc":
+        ranges = (E.jfsx_range * nb)()
+        for b in range(nb):
+            ranges[b].data, ranges[b].len, ranges[b].crc = src.ptr + b * L, L, crc.ptr + 4 * nseg * b
+        eng.crc32c_segments(ranges, nb, E.CRC_GEN, E.MEM_DEVICE)
+
+        def step():
+            eng.crc32c_segments(ranges, nb, E.CRC_VERIFY, E.MEM_DEVICE)
+        algo_bytes = nb * (L + 4 * nseg)
+    else:
+        specs = []
+        for b in range(nb):
+            key, nonce = E.gen_key(SEED, base + b)
+            specs.append({"key": key, "nonce": nonce, "src": src.ptr + b * L, "dst": dst.ptr + b * L, "len": L,
+                          "crc": crc.ptr + 4 * nseg * b})
+        blks, n = eng.make_blocks(specs)
+        if args.mode == "seal":
+            def step():
+                eng.seal_batch(algo, blks, n, E.CRC_GEN, E.MEM_DEVICE)
+        else:
+            # Open + CRC verify (BASELINE configs[3]): make a sealed image first
+            eng.seal_batch(algo, blks, n, E.CRC_GEN, E.MEM_DEVICE)
+            oblks, _ = eng.make_blocks([dict(s, src=s["dst"], dst=s["src"], tag=bytes(blks[i].tag))
+                                        for i, s in enumerate(specs)])
+
+            def step():
+                eng.open_batch(algo, oblks, n, E.CRC_VERIFY, E.MEM_DEVICE)
+        algo_bytes = nb * (2 * L + 16 + 4 * nseg + 44)
+
+    for _ in range(args.warmup):
+        step()
+    eng.sync()
+    eng.kernel_time(reset=True)
+    eng.set_timing(True)
+    barrier(dist)
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    eng.sync()
+    barrier(dist)
+    t1 = time.perf_counter()
+    eng.set_timing(False)
+    el = max_over_ranks(dist, t1 - t0, local)
+    k_ms, k_n = eng.kernel_time(reset=True)
+    k_avg_ms = k_ms / max(k_n, 1)
+
+    # post-timing spot check of a few blocks against the oracle (checker only)
+    verified = 0
+    if args.verify and args.mode == "seal":
+        from oracle import oracle as orc
+        cs = None
+        for b in range(0, nb, max(1, nb // args.verify))[:args.verify]:
+            p = orc.gen_block(SEED, base + b, L)
+            key, nonce = orc.gen_key(SEED, base + b)
+            c, tag = orc.seal(orc.AES256GCM if algo == E.AES256GCM else orc.CHACHA20P1305, key, nonce, p,
+                              fast=algo == E.AES256GCM)
+            ok = bytes(blks[b].tag) == tag and dst.download(L, offset=b * L).tobytes() == c
+            ok = ok and crc.download(4 * nseg, offset=4 * nseg * b).tobytes() == orc.checksum(p, hw=True)
+            if not ok:
+                raise SystemExit("bench: block %d differs from the oracle" % b)
+            verified += 1
+
+    total_plain = world * nb * L * args.steps
+    value = total_plain / el / 1e9
+    achieved = algo_bytes / (k_avg_ms / 1e3) / 1e9 if k_n else None
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu and args.mode == "seal":
+        cpu = cpu_baseline(args)
+    if rank == 0:
+        line = {
+            "metric": "sealed+checksummed GB/s, 4 MiB blocks" if args.mode == "seal" else
+                      ("opened+verified GB/s, 4 MiB blocks" if args.mode == "open" else "CRC32C-verified GB/s"),
+            "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic (SplitMix64 blocks, "
+            "per-block SplitMix64 keys/nonces), device-resident",
+            "config": {"workload": "%s GiB device-resident batch of 4 MiB blocks per GPU, %s %s + CRC32C %s" % (
+                nb * L / 2**30, args.algo, args.mode, "full" if args.mode == "seal" else "verify"),
+                "blocks_per_gpu": nb, "block_bytes": L, "algo": args.algo, "mode": args.mode,
+                "parallelism": "block-sharded x%d, no collective" % world},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": None,
+                         "kernel": "gcm_main_k" if args.mode != "crc" else "crc_segments_k",
+                         "kernel_avg_ms": round(k_avg_ms, 3), "algorithmic_bytes_per_launch": algo_bytes},
+            "cpu_baseline": cpu,
+            "verified_blocks": verified,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

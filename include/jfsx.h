@@ -1,0 +1,184 @@
+/*
+ * jfsx.h -- C-ABI of libjfsx.so, the MI355X block-transform engine for the
+ * JuiceFS per-block data path (AEAD Seal/Open fused with CRC32C segment
+ * checksums).  Plain C types only: this is the surface a cgo shim binds
+ * (see INTEGRATION.md for the Go side).
+ *
+ * Reference interfaces each entry point replaces (JuiceFS 1.2.0,
+ * /root/reference):
+ *
+ *   jfsx_seal_batch      dataEncryptor.Encrypt's aead.Seal          pkg/object/encrypt.go:164-194 (Seal at :192)
+ *                        + checksum() on the same plaintext         pkg/chunk/disk_cache.go:1218-1231 (called :469)
+ *   jfsx_open_batch      dataEncryptor.Decrypt's aead.Open          pkg/object/encrypt.go:196-216 (Open at :215)
+ *                        + checksum()/verify of the plaintext       pkg/chunk/disk_cache.go:1219, :1315-1327
+ *   jfsx_data_encrypt    dataEncryptor.Encrypt (object format)      pkg/object/encrypt.go:164-194
+ *   jfsx_data_decrypt    dataEncryptor.Decrypt (object format)      pkg/object/encrypt.go:196-216
+ *   jfsx_checksum        checksum(data) []byte                      pkg/chunk/disk_cache.go:1218-1231
+ *   jfsx_crc32c_segments the CRC loop of cacheFile.ReadAt           pkg/chunk/disk_cache.go:1315-1327
+ *   jfsx_cache_verify    cacheFile.ReadAt level logic + verify      pkg/chunk/disk_cache.go:1255-1329
+ *   JFSX_AES256GCM /     NewDataEncryptor algo "aes256gcm-rsa" /    pkg/object/encrypt.go:142-162
+ *   JFSX_CHACHA20P1305   "chacha20-rsa"
+ *
+ * RSA-OAEP key wrapping (encrypt.go:124-134) stays with the caller: the
+ * engine takes the 32-byte data key and 12-byte nonce per block as inputs
+ * (the reference draws both from crypto/rand, encrypt.go:165-180).
+ *
+ * Threading: a context may be used from several host threads; calls on one
+ * context are serialised internally (one HIP stream per context).  Use one
+ * context per GPU (per device ordinal) and per submitting thread for
+ * concurrency.
+ *
+ * Return codes: 0 on success, negative errno-style values on batch-level
+ * failure (JFSX_EINVAL, JFSX_ENODEV, JFSX_EIO, JFSX_ENOMEM).  Per-block
+ * results are in jfsx_blk.status.
+ */
+#ifndef JFSX_H
+#define JFSX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define JFSX_ABI_VERSION 1
+
+/* algorithms (encrypt.go:142-145) */
+#define JFSX_AES256GCM 0     /* "aes256gcm-rsa" (also the "" default)   */
+#define JFSX_CHACHA20P1305 1 /* "chacha20-rsa"                          */
+
+/* CRC32C segment checksum mode, per 32 KiB segment of the PLAINTEXT
+ * (csBlock = 32 KiB, disk_cache.go:1207).  CRC arrays are big-endian uint32
+ * per segment, exactly the bytes checksum() returns (buffer.go:42-44,98-101);
+ * a zero-length block has one zero CRC (4 bytes), as checksum() does. */
+#define JFSX_CRC_NONE 0   /* no checksum                                  */
+#define JFSX_CRC_GEN 1    /* write crc[] (level != none on cache write)   */
+#define JFSX_CRC_VERIFY 2 /* compare against crc[] (cache read verify)    */
+
+/* where src/dst/crc pointers of a batch live */
+#define JFSX_MEM_DEVICE 0 /* device memory (jfsx_alloc_device / hipMalloc) */
+#define JFSX_MEM_HOST 1   /* host memory; staged through the engine          */
+
+/* per-block status */
+#define JFSX_OK 0
+#define JFSX_ETAG 1 /* AEAD authentication failed (Go: cipher's errOpen)      */
+#define JFSX_ECRC 2 /* "data checksum %d != expect %d" (disk_cache.go:1324)   */
+
+/* batch-level errors */
+#define JFSX_EINVAL (-22)
+#define JFSX_ENODEV (-19)
+#define JFSX_EIO (-5)
+#define JFSX_ENOMEM (-12)
+#define JFSX_EMISFORMED (-74) /* "misformed ciphertext: %d %d" (encrypt.go:199-201) */
+
+typedef struct jfsx_ctx jfsx_ctx;
+
+/* One 4 MiB-class block.  For JFSX_MEM_DEVICE batches src/dst must be
+ * 16-byte aligned; dst may equal src (in place, as aead.Seal(p[:0]...) and
+ * aead.Open(ciphertext[:0]...) are).  Any length 0 .. 2^32-1 is accepted. */
+typedef struct jfsx_blk {
+    uint8_t key[32];      /* data key (encrypt.go:165)                        */
+    uint8_t nonce[12];    /* nonce (encrypt.go:177)                           */
+    uint32_t reserved;    /* must be 0                                        */
+    const void *src;      /* seal: plaintext  / open: ciphertext (no tag)     */
+    void *dst;            /* seal: ciphertext / open: plaintext               */
+    uint64_t len;         /* bytes of src/dst                                 */
+    uint8_t tag[16];      /* seal: out / open: in                             */
+    uint8_t *crc;         /* GEN: out, VERIFY: in; 4*max(1,ceil(len/32K)) B   */
+    int32_t status;       /* out: JFSX_OK / JFSX_ETAG / JFSX_ECRC             */
+    int32_t crc_bad_seg;  /* out: first failing segment (VERIFY), else -1     */
+    uint32_t crc_got;     /* out: CRC computed for crc_bad_seg                */
+    uint32_t crc_expect;  /* out: CRC expected for crc_bad_seg                */
+} jfsx_blk;
+
+/* One checksum range: [data, data+len) is a segment-aligned window of a
+ * cache block; crc[k] is the BE32 CRC of its k-th 32 KiB segment. */
+typedef struct jfsx_range {
+    const void *data;
+    uint64_t len;
+    uint8_t *crc;         /* GEN: out, VERIFY: in                             */
+    int32_t status;       /* out: JFSX_OK / JFSX_ECRC                         */
+    int32_t bad_seg;      /* out: first failing segment, -1 none              */
+    uint32_t got, expect; /* out                                              */
+} jfsx_range;
+
+int jfsx_abi_version(void);
+int jfsx_device_count(int *n);
+
+/* context = one GPU + one HIP stream + device workspace + pinned staging */
+int jfsx_ctx_open(int device, uint32_t flags, jfsx_ctx **out);
+int jfsx_ctx_close(jfsx_ctx *ctx);
+int jfsx_ctx_sync(jfsx_ctx *ctx);
+/* returns the context's hipStream_t (as void*) for callers that order their
+ * own copies against the engine's work */
+void *jfsx_ctx_stream(jfsx_ctx *ctx);
+/* kernel timing: when enabled, HIP events bracket the main transform kernel of
+ * every batch on the context's stream; query returns the summed milliseconds
+ * and the number of launches since the last reset */
+int jfsx_ctx_set_timing(jfsx_ctx *ctx, int enable);
+int jfsx_ctx_kernel_time(jfsx_ctx *ctx, double *ms_total, uint64_t *launches, int reset);
+
+/* memory helpers (engine-owned pinned staging, device buffers) */
+int jfsx_alloc_pinned(jfsx_ctx *ctx, size_t bytes, void **p);
+int jfsx_free_pinned(jfsx_ctx *ctx, void *p);
+int jfsx_alloc_device(jfsx_ctx *ctx, size_t bytes, void **p);
+int jfsx_free_device(jfsx_ctx *ctx, void *p);
+int jfsx_memcpy_h2d(jfsx_ctx *ctx, void *dst, const void *src, size_t bytes);
+int jfsx_memcpy_d2h(jfsx_ctx *ctx, void *dst, const void *src, size_t bytes);
+
+/* Batched AEAD over blocks, fused with CRC32C segment checksums of the
+ * plaintext.  mem = JFSX_MEM_DEVICE or JFSX_MEM_HOST.  Synchronous: returns
+ * when tags, CRCs and statuses are written back into blks. */
+int jfsx_seal_batch(jfsx_ctx *ctx, int algo, int n, jfsx_blk *blks, int crc_mode, int mem);
+int jfsx_open_batch(jfsx_ctx *ctx, int algo, int n, jfsx_blk *blks, int crc_mode, int mem);
+
+/* CRC32C per 32 KiB segment over n ranges (cache-hit verify, none-cipher
+ * volumes, staging re-read).  mode = JFSX_CRC_GEN or JFSX_CRC_VERIFY. */
+int jfsx_crc32c_segments(jfsx_ctx *ctx, int n, jfsx_range *ranges, int mode, int mem);
+
+/* checksum(data) on the GPU: out receives 4*max(1,ceil(len/32K)) bytes.
+ * data and out are host memory. */
+int jfsx_checksum(jfsx_ctx *ctx, const void *data, uint64_t len, uint8_t *out);
+
+/* cacheFile.ReadAt verify (disk_cache.go:1255-1329) over an in-memory cache
+ * file image: file = data(length) ‖ BE32 CRCs, level 0 none / 1 full /
+ * 2 shrink / 3 extend (the level openCacheFile resolved).  Copies
+ * [off, off+size) into out.  Returns 0 ok, JFSX_ECRC on mismatch (got,
+ * expect, bad_seg filled), 2 on short read, <0 on argument errors. */
+int jfsx_cache_verify(jfsx_ctx *ctx, const void *file, uint64_t file_size, uint64_t length, int level,
+                      uint64_t off, uint64_t size, void *out, uint64_t *n_out, uint32_t *got,
+                      uint32_t *expect, int64_t *bad_seg);
+
+/* dataEncryptor.Encrypt with an already-wrapped key: writes
+ * BE16(wlen) | 12 | wrapped | nonce | C | tag into out (host memory).
+ * out_cap must be >= 3+wlen+12+len+16. */
+int jfsx_data_encrypt(jfsx_ctx *ctx, int algo, const uint8_t key[32], const uint8_t nonce[12],
+                      const uint8_t *wrapped, int wlen, const void *plaintext, uint64_t len, void *out,
+                      uint64_t out_cap, uint64_t *out_len);
+/* dataEncryptor.Decrypt after the key is unwrapped: parses the header
+ * (JFSX_EMISFORMED if 3+klen+nlen >= olen), opens, and writes the plaintext
+ * to out only when the tag verifies (returns JFSX_ETAG otherwise). */
+int jfsx_data_decrypt(jfsx_ctx *ctx, int algo, const uint8_t key[32], const void *obj, uint64_t olen,
+                      void *out, uint64_t out_cap, uint64_t *out_len);
+/* header helper: returns wrapped-key length and offset/size of the nonce so a
+ * caller can unwrap the key first (encrypt.go:197-205) */
+int jfsx_parse_header(const void *obj, uint64_t olen, int *klen, int *nlen);
+
+/* synthetic input generator used by bench/tests: fills len bytes of device
+ * memory with the SplitMix64 stream of (seed, block) (documented in
+ * DESIGN.md; identical to oracle/jfs_oracle.c:orc_gen_block) */
+int jfsx_gen_synthetic(jfsx_ctx *ctx, void *dst, uint64_t len, uint64_t seed, uint64_t block);
+/* fills n keys (32 B) and nonces (12 B) with the same per-block stream as
+ * orc_gen_key, host side */
+void jfsx_gen_key(uint64_t seed, uint64_t block, uint8_t key[32], uint8_t nonce[12]);
+
+/* diagnostics: the lookup tables the kernels stage into LDS, built on the host
+ * without a device (AES T0|T2 x32 replicated: 16384 dwords; CRC32C slice-by-16
+ * and 1008-byte shift tables: 5120 dwords; CRC lane/power constants: 128) */
+int jfsx_debug_tables(uint32_t *aes, uint32_t *crc, uint32_t *crcx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JFSX_H */

@@ -1,0 +1,813 @@
+// jfsx_api.cpp -- C-ABI of libjfsx.so (include/jfsx.h): contexts, tables,
+// batch planning, staging, launches.  Host code, compiled by hipcc.
+//
+// A batch runs as: H2D of descriptors (one pinned copy) -> keysetup kernel ->
+// main transform kernel (one workgroup per task) -> finalize kernel -> D2H of
+// per-block results (tags, status, first failing CRC) -> stream sync.
+#include <errno.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include "jfsx_internal.h"
+
+using namespace jfsx;
+
+#define HIP_OK(x)                                      \
+    do {                                               \
+        if ((x) != hipSuccess) return JFSX_EIO;        \
+    } while (0)
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// table construction (host)
+// ---------------------------------------------------------------------------
+uint8_t gf8_mul(uint8_t a, uint8_t b) {
+    uint8_t p = 0;
+    while (b) {
+        if (b & 1) p ^= a;
+        a = (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1B : 0));
+        b >>= 1;
+    }
+    return p;
+}
+
+void make_aes_table(std::vector<uint32_t> &t) {
+    // S-box = affine(inverse) over GF(2^8) (FIPS-197 5.1.1)
+    uint8_t sbox[256];
+    for (int x = 0; x < 256; x++) {
+        uint8_t inv = 0;
+        if (x) {
+            uint8_t r = 1, base = (uint8_t)x;
+            for (int e = 254; e; e >>= 1) {
+                if (e & 1) r = gf8_mul(r, base);
+                base = gf8_mul(base, base);
+            }
+            inv = r;
+        }
+        uint8_t s = inv, v = inv;
+        for (int k = 1; k <= 4; k++) v ^= (uint8_t)((s << k) | (s >> (8 - k)));
+        sbox[x] = v ^ 0x63;
+    }
+    t.assign(256 * 64, 0);
+    for (int x = 0; x < 256; x++) {
+        uint32_t s = sbox[x];
+        uint32_t t0 = gf8_mul((uint8_t)s, 2) | (s << 8) | (s << 16) | ((uint32_t)gf8_mul((uint8_t)s, 3) << 24);
+        uint32_t t2 = (t0 << 16) | (t0 >> 16);
+        for (int r = 0; r < 32; r++) {
+            t[x * 64 + r] = t0;
+            t[x * 64 + 32 + r] = t2;
+        }
+    }
+}
+
+uint32_t crc_mulmod_h(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+    for (int i = 0; i < 32; i++) {
+        if (a & 0x80000000u) p ^= b;
+        a <<= 1;
+        b = (b & 1) ? (b >> 1) ^ kCrcPoly : b >> 1;
+    }
+    return p;
+}
+
+void make_crc_tables(std::vector<uint32_t> &crc, std::vector<uint32_t> &crcx) {
+    uint32_t T[256];
+    for (uint32_t i = 0; i < 256; i++) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ kCrcPoly : c >> 1;
+        T[i] = c;
+    }
+    uint32_t x8[32];
+    x8[0] = 0x00800000u;  // x^8
+    for (int k = 1; k < 32; k++) x8[k] = crc_mulmod_h(x8[k - 1], x8[k - 1]);
+    auto xpow8 = [&](uint64_t n) {
+        uint32_t r = 0x80000000u;
+        for (int k = 0; n; k++, n >>= 1)
+            if (n & 1) r = crc_mulmod_h(x8[k], r);
+        return r;
+    };
+    crc.assign(20 * 256, 0);
+    for (int j = 0; j < 16; j++) {
+        const uint32_t xp = xpow8(15 - j);
+        for (int b = 0; b < 256; b++) crc[j * 256 + b] = crc_mulmod_h(xp, T[b]);
+    }
+    const uint32_t x1008 = xpow8(1008);
+    for (int k = 0; k < 4; k++)
+        for (uint32_t v = 0; v < 256; v++) crc[(16 + k) * 256 + v] = crc_mulmod_h(x1008, v << (8 * k));
+    crcx.assign(128, 0);
+    for (int l = 0; l < 64; l++) crcx[l] = xpow8(16 * (63 - l));
+    for (int k = 0; k < 32; k++) crcx[64 + k] = x8[k];
+    crcx[96] = crc_mulmod_h(xpow8(kSeg), 0xffffffffu);
+}
+
+inline uint64_t nseg_of(uint64_t len) { return len ? (len + kSeg - 1) / kSeg : 1; }
+
+struct Plan {
+    std::vector<Task> tasks;
+    uint64_t nslots = 0;
+};
+
+}  // namespace
+
+struct jfsx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    uint32_t *d_tab = nullptr;  // aes | crc | crcx
+    DevTables tabs{};
+    char *d_ws = nullptr;
+    size_t ws_cap = 0;
+    char *h_ws = nullptr;  // pinned
+    size_t hws_cap = 0;
+    char *d_stage = nullptr;
+    size_t stage_cap = 0;
+    bool timing = false;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double ms_total = 0;
+    uint64_t launches = 0;
+};
+
+namespace {
+
+int ensure_dev(jfsx_ctx *c, char **buf, size_t *cap, size_t need) {
+    if (need <= *cap) return 0;
+    if (*buf) {
+        HIP_OK(hipStreamSynchronize(c->stream));
+        HIP_OK(hipFree(*buf));
+        *buf = nullptr;
+        *cap = 0;
+    }
+    size_t n = std::max(need, (size_t)1 << 20);
+    n = (n + 0xFFFFF) & ~(size_t)0xFFFFF;
+    if (hipMalloc((void **)buf, n) != hipSuccess) return JFSX_ENOMEM;
+    *cap = n;
+    return 0;
+}
+
+int ensure_host(jfsx_ctx *c, size_t need) {
+    if (need <= c->hws_cap) return 0;
+    if (c->h_ws) {
+        HIP_OK(hipStreamSynchronize(c->stream));
+        HIP_OK(hipHostFree(c->h_ws));
+        c->h_ws = nullptr;
+        c->hws_cap = 0;
+    }
+    size_t n = std::max(need, (size_t)1 << 20);
+    n = (n + 0xFFFFF) & ~(size_t)0xFFFFF;
+    if (hipHostMalloc((void **)&c->h_ws, n, hipHostMallocDefault) != hipSuccess) return JFSX_ENOMEM;
+    c->hws_cap = n;
+    return 0;
+}
+
+inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Split each block into <= CH-byte tasks (CH a multiple of 16 segments), one
+// workgroup each; 16 partial slots per task.
+Plan plan_tasks(const std::vector<uint64_t> &lens, uint64_t seg_per_task_max) {
+    Plan p;
+    uint64_t total = 0;
+    for (uint64_t l : lens) total += l;
+    const uint64_t unit = (uint64_t)kWaves * kSeg;  // 512 KiB
+    uint64_t ch = seg_per_task_max * kSeg;
+    // enough workgroups to fill 256 CUs twice when the batch is small
+    const uint64_t want = 512;
+    if (total / ch < want) {
+        uint64_t c = (total / want + unit - 1) / unit * unit;
+        ch = std::max(unit, std::min(ch, c));
+    }
+    for (size_t b = 0; b < lens.size(); b++) {
+        for (uint64_t c0 = 0; c0 < lens[b]; c0 += ch) {
+            Task t;
+            t.blk = (uint32_t)b;
+            t.slot0 = (uint32_t)p.nslots;
+            t.c0 = c0;
+            t.c1 = std::min(c0 + ch, lens[b]);
+            p.tasks.push_back(t);
+            p.nslots += kWaves;
+        }
+    }
+    return p;
+}
+
+bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+// Core of seal/open for device-resident buffers.
+int run_aead(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mode) {
+    if (algo != JFSX_AES256GCM && algo != JFSX_CHACHA20P1305) return JFSX_EINVAL;
+    if (crc_mode < 0 || crc_mode > 2 || n < 0) return JFSX_EINVAL;
+    if (n == 0) return 0;
+    if (algo == JFSX_CHACHA20P1305) return JFSX_EINVAL;  // TODO(round 1): ChaCha20-Poly1305 kernels
+    std::vector<uint64_t> lens(n);
+    uint64_t crc_calc_words = 0;
+    for (int i = 0; i < n; i++) {
+        const jfsx_blk &b = blks[i];
+        if (b.len && (!b.src || !b.dst || !aligned16(b.src) || !aligned16(b.dst))) return JFSX_EINVAL;
+        if (b.len >= ((uint64_t)1 << 32) * 16) return JFSX_EINVAL;
+        if (crc_mode && !b.crc) return JFSX_EINVAL;
+        lens[i] = b.len;
+        if (crc_mode == JFSX_CRC_VERIFY) crc_calc_words += nseg_of(b.len);
+    }
+    Plan plan = plan_tasks(lens, kMaxTaskBytes / kSeg);
+    const size_t nt = plan.tasks.size();
+    // device workspace layout
+    size_t off = 0;
+    const size_t o_keys = off; off = align256(off + sizeof(KeyIn) * n);
+    const size_t o_blk = off; off = align256(off + sizeof(BlkDev) * n);
+    const size_t o_task = off; off = align256(off + sizeof(Task) * std::max<size_t>(nt, 1));
+    const size_t o_tagin = off; off = align256(off + 16 * (size_t)n);
+    const size_t h_bytes = off;  // everything above is uploaded from the pinned mirror
+    const size_t o_out = off; off = align256(off + sizeof(BlkOut) * n);
+    const size_t o_sched = off; off = align256(off + sizeof(GcmSched) * n);
+    const size_t o_part = off; off = align256(off + 32 * std::max<uint64_t>(plan.nslots, 1));
+    const size_t o_pexp = off; off = align256(off + 4 * std::max<uint64_t>(plan.nslots, 1));
+    const size_t o_calc = off; off = align256(off + 4 * std::max<uint64_t>(crc_calc_words, 1));
+    int rc;
+    if ((rc = ensure_dev(c, &c->d_ws, &c->ws_cap, off))) return rc;
+    if ((rc = ensure_host(c, std::max(h_bytes, sizeof(BlkOut) * n)))) return rc;
+    char *h = c->h_ws, *d = c->d_ws;
+    KeyIn *hk = (KeyIn *)(h + o_keys);
+    BlkDev *hb = (BlkDev *)(h + o_blk);
+    uint64_t calc = 0;
+    for (int i = 0; i < n; i++) {
+        const jfsx_blk &b = blks[i];
+        memcpy(hk[i].key, b.key, 32);
+        memcpy(hk[i].nonce, b.nonce, 12);
+        hk[i].pad = 0;
+        hb[i].src = (const uint8_t *)b.src;
+        hb[i].dst = (uint8_t *)b.dst;
+        hb[i].len = b.len;
+        hb[i].crc = b.crc;
+        hb[i].crc_calc = nullptr;
+        if (crc_mode == JFSX_CRC_VERIFY) {
+            hb[i].crc_calc = (uint32_t *)(d + o_calc) + calc;
+            calc += nseg_of(b.len);
+        }
+        hb[i].slot0 = 0;
+        hb[i].nslots = 0;
+        hb[i].tag_in = open ? (const uint8_t *)(d + o_tagin + 16 * (size_t)i) : nullptr;
+        memcpy(h + o_tagin + 16 * (size_t)i, b.tag, 16);
+    }
+    for (size_t t = 0; t < nt; t++) {
+        BlkDev &bd = hb[plan.tasks[t].blk];
+        if (bd.nslots == 0) bd.slot0 = plan.tasks[t].slot0;
+        bd.nslots += kWaves;
+    }
+    if (nt) memcpy(h + o_task, plan.tasks.data(), sizeof(Task) * nt);
+    hipStream_t s = c->stream;
+    HIP_OK(hipMemcpyAsync(d, h, h_bytes, hipMemcpyHostToDevice, s));
+    if (crc_mode == JFSX_CRC_GEN)
+        for (int i = 0; i < n; i++)
+            if (blks[i].len == 0) HIP_OK(hipMemsetAsync(blks[i].crc, 0, 4, s));
+    const KeyIn *dk = (const KeyIn *)(d + o_keys);
+    const BlkDev *db = (const BlkDev *)(d + o_blk);
+    const Task *dt = (const Task *)(d + o_task);
+    GcmSched *dsch = (GcmSched *)(d + o_sched);
+    uint32_t *dpart = (uint32_t *)(d + o_part);
+    uint32_t *dpexp = (uint32_t *)(d + o_pexp);
+    BlkOut *dout = (BlkOut *)(d + o_out);
+    launch_gcm_keysetup(s, n, dk, db, dsch, c->tabs);
+    if (c->timing) HIP_OK(hipEventRecord(c->ev0, s));
+    launch_gcm_main(s, (int)nt, open, crc_mode, dt, db, dsch, dpart, dpexp, c->tabs);
+    if (c->timing) HIP_OK(hipEventRecord(c->ev1, s));
+    launch_gcm_finalize(s, n, open, crc_mode, db, dsch, dpart, dpexp, dout);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(h, dout, sizeof(BlkOut) * n, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    if (c->timing && nt) {
+        float ms = 0;
+        HIP_OK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        c->ms_total += ms;
+        c->launches += 1;
+    }
+    const BlkOut *ho = (const BlkOut *)h;
+    for (int i = 0; i < n; i++) {
+        jfsx_blk &b = blks[i];
+        if (!open) memcpy(b.tag, ho[i].tag, 16);
+        b.status = ho[i].status;
+        b.crc_bad_seg = ho[i].bad_seg;
+        b.crc_got = ho[i].got;
+        b.crc_expect = ho[i].expect;
+    }
+    return 0;
+}
+
+// Host-memory batches: stage through device buffers (synchronous).
+int run_aead_host(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mode) {
+    size_t need = 0;
+    for (int i = 0; i < n; i++) {
+        need += align256(blks[i].len) * 1;
+        if (crc_mode) need += align256(4 * nseg_of(blks[i].len));
+    }
+    int rc;
+    if ((rc = ensure_dev(c, &c->d_stage, &c->stage_cap, std::max<size_t>(need, 256)))) return rc;
+    std::vector<jfsx_blk> dv(blks, blks + n);
+    size_t off = 0;
+    hipStream_t s = c->stream;
+    for (int i = 0; i < n; i++) {
+        char *buf = c->d_stage + off;
+        off += align256(blks[i].len);
+        if (blks[i].len) HIP_OK(hipMemcpyAsync(buf, blks[i].src, blks[i].len, hipMemcpyHostToDevice, s));
+        dv[i].src = buf;
+        dv[i].dst = buf;
+        if (crc_mode) {
+            char *cb = c->d_stage + off;
+            off += align256(4 * nseg_of(blks[i].len));
+            if (crc_mode == JFSX_CRC_VERIFY)
+                HIP_OK(hipMemcpyAsync(cb, blks[i].crc, 4 * nseg_of(blks[i].len), hipMemcpyHostToDevice, s));
+            dv[i].crc = (uint8_t *)cb;
+        }
+    }
+    if ((rc = run_aead(c, algo, open, n, dv.data(), crc_mode))) return rc;
+    for (int i = 0; i < n; i++) {
+        blks[i].status = dv[i].status;
+        blks[i].crc_bad_seg = dv[i].crc_bad_seg;
+        blks[i].crc_got = dv[i].crc_got;
+        blks[i].crc_expect = dv[i].crc_expect;
+        if (!open) memcpy(blks[i].tag, dv[i].tag, 16);
+        // Open: plaintext is released only when the tag verified
+        if (blks[i].len && (!open || dv[i].status != JFSX_ETAG))
+            HIP_OK(hipMemcpyAsync(blks[i].dst, dv[i].dst, blks[i].len, hipMemcpyDeviceToHost, s));
+        if (crc_mode == JFSX_CRC_GEN)
+            HIP_OK(hipMemcpyAsync(blks[i].crc, dv[i].crc, 4 * nseg_of(blks[i].len), hipMemcpyDeviceToHost, s));
+    }
+    HIP_OK(hipStreamSynchronize(s));
+    return 0;
+}
+
+int run_crc(jfsx_ctx *c, int n, jfsx_range *r, int mode) {
+    if (n < 0 || (mode != JFSX_CRC_GEN && mode != JFSX_CRC_VERIFY)) return JFSX_EINVAL;
+    if (n == 0) return 0;
+    uint64_t calc_words = 0;
+    std::vector<Task> tasks;
+    const uint64_t per = 4 * (uint64_t)kSeg;
+    for (int i = 0; i < n; i++) {
+        if (r[i].len && (!r[i].data || !aligned16(r[i].data))) return JFSX_EINVAL;
+        if (!r[i].crc) return JFSX_EINVAL;
+        for (uint64_t c0 = 0; c0 < r[i].len; c0 += per) tasks.push_back(Task{(uint32_t)i, 0, c0, std::min(c0 + per, r[i].len)});
+        if (mode == JFSX_CRC_VERIFY) calc_words += nseg_of(r[i].len);
+    }
+    const size_t nt = tasks.size();
+    size_t off = 0;
+    const size_t o_blk = off; off = align256(off + sizeof(BlkDev) * n);
+    const size_t o_task = off; off = align256(off + sizeof(Task) * std::max<size_t>(nt, 1));
+    const size_t h_bytes = off;
+    const size_t o_out = off; off = align256(off + sizeof(BlkOut) * n);
+    const size_t o_calc = off; off = align256(off + 4 * std::max<uint64_t>(calc_words, 1));
+    int rc;
+    if ((rc = ensure_dev(c, &c->d_ws, &c->ws_cap, off))) return rc;
+    if ((rc = ensure_host(c, std::max(h_bytes, sizeof(BlkOut) * n)))) return rc;
+    char *h = c->h_ws, *d = c->d_ws;
+    BlkDev *hb = (BlkDev *)(h + o_blk);
+    uint64_t calc = 0;
+    for (int i = 0; i < n; i++) {
+        memset(&hb[i], 0, sizeof(BlkDev));
+        hb[i].src = (const uint8_t *)r[i].data;
+        hb[i].len = r[i].len;
+        hb[i].crc = r[i].crc;
+        if (mode == JFSX_CRC_VERIFY) {
+            hb[i].crc_calc = (uint32_t *)(d + o_calc) + calc;
+            calc += nseg_of(r[i].len);
+        }
+    }
+    if (nt) memcpy(h + o_task, tasks.data(), sizeof(Task) * nt);
+    hipStream_t s = c->stream;
+    HIP_OK(hipMemcpyAsync(d, h, h_bytes, hipMemcpyHostToDevice, s));
+    if (c->timing) HIP_OK(hipEventRecord(c->ev0, s));
+    launch_crc_segments(s, (int)nt, (const Task *)(d + o_task), (const BlkDev *)(d + o_blk), c->tabs);
+    if (c->timing) HIP_OK(hipEventRecord(c->ev1, s));
+    launch_crc_finalize(s, n, mode, (const BlkDev *)(d + o_blk), (BlkOut *)(d + o_out));
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(h, d + o_out, sizeof(BlkOut) * n, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    if (c->timing && nt) {
+        float ms = 0;
+        HIP_OK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        c->ms_total += ms;
+        c->launches += 1;
+    }
+    const BlkOut *ho = (const BlkOut *)h;
+    for (int i = 0; i < n; i++) {
+        r[i].status = ho[i].status;
+        r[i].bad_seg = ho[i].bad_seg;
+        r[i].got = ho[i].got;
+        r[i].expect = ho[i].expect;
+    }
+    return 0;
+}
+
+int run_crc_host(jfsx_ctx *c, int n, jfsx_range *r, int mode) {
+    size_t need = 0;
+    for (int i = 0; i < n; i++) need += align256(r[i].len) + align256(4 * nseg_of(r[i].len));
+    int rc;
+    if ((rc = ensure_dev(c, &c->d_stage, &c->stage_cap, std::max<size_t>(need, 256)))) return rc;
+    std::vector<jfsx_range> dv(r, r + n);
+    size_t off = 0;
+    hipStream_t s = c->stream;
+    for (int i = 0; i < n; i++) {
+        char *buf = c->d_stage + off;
+        off += align256(r[i].len);
+        char *cb = c->d_stage + off;
+        off += align256(4 * nseg_of(r[i].len));
+        if (r[i].len) HIP_OK(hipMemcpyAsync(buf, r[i].data, r[i].len, hipMemcpyHostToDevice, s));
+        if (mode == JFSX_CRC_VERIFY) HIP_OK(hipMemcpyAsync(cb, r[i].crc, 4 * nseg_of(r[i].len), hipMemcpyHostToDevice, s));
+        dv[i].data = buf;
+        dv[i].crc = (uint8_t *)cb;
+    }
+    if ((rc = run_crc(c, n, dv.data(), mode))) return rc;
+    for (int i = 0; i < n; i++) {
+        r[i].status = dv[i].status;
+        r[i].bad_seg = dv[i].bad_seg;
+        r[i].got = dv[i].got;
+        r[i].expect = dv[i].expect;
+        if (mode == JFSX_CRC_GEN) HIP_OK(hipMemcpyAsync(r[i].crc, dv[i].crc, 4 * nseg_of(r[i].len), hipMemcpyDeviceToHost, s));
+    }
+    HIP_OK(hipStreamSynchronize(s));
+    return 0;
+}
+
+}  // namespace
+
+// ===========================================================================
+// exported C-ABI
+// ===========================================================================
+extern "C" {
+
+int jfsx_abi_version(void) { return JFSX_ABI_VERSION; }
+
+int jfsx_device_count(int *n) {
+    if (!n) return JFSX_EINVAL;
+    if (hipGetDeviceCount(n) != hipSuccess) {
+        *n = 0;
+        return JFSX_ENODEV;
+    }
+    return 0;
+}
+
+int jfsx_ctx_open(int device, uint32_t flags, jfsx_ctx **out) {
+    (void)flags;
+    if (!out) return JFSX_EINVAL;
+    *out = nullptr;
+    int nd = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess || device < 0 || device >= nd) return JFSX_ENODEV;
+    HIP_OK(hipSetDevice(device));
+    jfsx_ctx *c = new jfsx_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return JFSX_EIO;
+    }
+    std::vector<uint32_t> aes, crc, crcx;
+    make_aes_table(aes);
+    make_crc_tables(crc, crcx);
+    const size_t nbytes = 4 * (aes.size() + crc.size() + crcx.size());
+    if (hipMalloc((void **)&c->d_tab, nbytes) != hipSuccess) {
+        hipStreamDestroy(c->stream);
+        delete c;
+        return JFSX_ENOMEM;
+    }
+    std::vector<uint32_t> all;
+    all.insert(all.end(), aes.begin(), aes.end());
+    all.insert(all.end(), crc.begin(), crc.end());
+    all.insert(all.end(), crcx.begin(), crcx.end());
+    if (hipMemcpy(c->d_tab, all.data(), nbytes, hipMemcpyHostToDevice) != hipSuccess) {
+        jfsx_ctx_close(c);
+        return JFSX_EIO;
+    }
+    c->tabs.aes = c->d_tab;
+    c->tabs.crc = c->d_tab + aes.size();
+    c->tabs.crcx = c->d_tab + aes.size() + crc.size();
+    if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        jfsx_ctx_close(c);
+        return JFSX_EIO;
+    }
+    *out = c;
+    return 0;
+}
+
+int jfsx_ctx_close(jfsx_ctx *c) {
+    if (!c) return JFSX_EINVAL;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->d_tab) hipFree(c->d_tab);
+    if (c->d_ws) hipFree(c->d_ws);
+    if (c->d_stage) hipFree(c->d_stage);
+    if (c->h_ws) hipHostFree(c->h_ws);
+    if (c->ev0) hipEventDestroy(c->ev0);
+    if (c->ev1) hipEventDestroy(c->ev1);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+    return 0;
+}
+
+int jfsx_ctx_sync(jfsx_ctx *c) {
+    if (!c) return JFSX_EINVAL;
+    HIP_OK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+void *jfsx_ctx_stream(jfsx_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int jfsx_ctx_set_timing(jfsx_ctx *c, int enable) {
+    if (!c) return JFSX_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->timing = enable != 0;
+    return 0;
+}
+
+int jfsx_ctx_kernel_time(jfsx_ctx *c, double *ms_total, uint64_t *launches, int reset) {
+    if (!c) return JFSX_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (ms_total) *ms_total = c->ms_total;
+    if (launches) *launches = c->launches;
+    if (reset) {
+        c->ms_total = 0;
+        c->launches = 0;
+    }
+    return 0;
+}
+
+int jfsx_alloc_pinned(jfsx_ctx *c, size_t bytes, void **p) {
+    if (!c || !p) return JFSX_EINVAL;
+    HIP_OK(hipSetDevice(c->device));
+    return hipHostMalloc(p, bytes, hipHostMallocDefault) == hipSuccess ? 0 : JFSX_ENOMEM;
+}
+int jfsx_free_pinned(jfsx_ctx *c, void *p) {
+    if (!c) return JFSX_EINVAL;
+    HIP_OK(hipHostFree(p));
+    return 0;
+}
+int jfsx_alloc_device(jfsx_ctx *c, size_t bytes, void **p) {
+    if (!c || !p) return JFSX_EINVAL;
+    HIP_OK(hipSetDevice(c->device));
+    return hipMalloc(p, bytes) == hipSuccess ? 0 : JFSX_ENOMEM;
+}
+int jfsx_free_device(jfsx_ctx *c, void *p) {
+    if (!c) return JFSX_EINVAL;
+    HIP_OK(hipFree(p));
+    return 0;
+}
+int jfsx_memcpy_h2d(jfsx_ctx *c, void *dst, const void *src, size_t bytes) {
+    if (!c) return JFSX_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+int jfsx_memcpy_d2h(jfsx_ctx *c, void *dst, const void *src, size_t bytes) {
+    if (!c) return JFSX_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int jfsx_seal_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *blks, int crc_mode, int mem) {
+    if (!c || (n > 0 && !blks)) return JFSX_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    return mem == JFSX_MEM_HOST ? run_aead_host(c, algo, false, n, blks, crc_mode)
+                                : run_aead(c, algo, false, n, blks, crc_mode);
+}
+
+int jfsx_open_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *blks, int crc_mode, int mem) {
+    if (!c || (n > 0 && !blks)) return JFSX_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    return mem == JFSX_MEM_HOST ? run_aead_host(c, algo, true, n, blks, crc_mode)
+                                : run_aead(c, algo, true, n, blks, crc_mode);
+}
+
+int jfsx_crc32c_segments(jfsx_ctx *c, int n, jfsx_range *ranges, int mode, int mem) {
+    if (!c || (n > 0 && !ranges)) return JFSX_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    return mem == JFSX_MEM_HOST ? run_crc_host(c, n, ranges, mode) : run_crc(c, n, ranges, mode);
+}
+
+int jfsx_checksum(jfsx_ctx *c, const void *data, uint64_t len, uint8_t *out) {
+    if (!c || !out || (len && !data)) return JFSX_EINVAL;
+    jfsx_range r;
+    memset(&r, 0, sizeof(r));
+    r.data = data;
+    r.len = len;
+    r.crc = out;
+    if (len == 0) {
+        memset(out, 0, 4);  // disk_cache.go:1221: (0-1)/csBlock+1 = 1 entry, loop body never runs
+        return 0;
+    }
+    return jfsx_crc32c_segments(c, 1, &r, JFSX_CRC_GEN, JFSX_MEM_HOST);
+}
+
+int jfsx_cache_verify(jfsx_ctx *c, const void *file, uint64_t file_size, uint64_t length, int level, uint64_t off,
+                      uint64_t size, void *out, uint64_t *n_out, uint32_t *got, uint32_t *expect,
+                      int64_t *bad_seg) {
+    // cacheFile.ReadAt, disk_cache.go:1255-1329 -- range logic on the host,
+    // the CRC work on the GPU.
+    if (!c || !file || !n_out || level < 0 || level > 3) return JFSX_EINVAL;
+    const uint8_t *f = (const uint8_t *)file;
+    *n_out = 0;
+    *bad_seg = -1;
+    auto pread = [&](uint8_t *dst, uint64_t sz, uint64_t o, bool *eof) -> uint64_t {
+        uint64_t nn = 0;
+        *eof = false;
+        if (o < file_size) {
+            nn = std::min(sz, file_size - o);
+            if (nn) memcpy(dst, f + o, nn);
+        }
+        if (nn < sz) *eof = true;
+        return nn;
+    };
+    bool eof = false;
+    if (level == 0 || (level == 1 && (off != 0 || size != length))) {
+        *n_out = pread((uint8_t *)out, size, off, &eof);
+        return eof ? 2 : 0;
+    }
+    std::vector<uint8_t> tmp;
+    uint8_t *rb = (uint8_t *)out;
+    uint64_t rbsize = size, roff = off;
+    if (level == 3) {
+        roff = off / kSeg * kSeg;
+        uint64_t rend = off + size;
+        if (rend % kSeg != 0) {
+            rend = (rend / kSeg + 1) * kSeg;
+            if (rend > length) rend = length;
+        }
+        if (rend - roff != size) {
+            rbsize = rend - roff;
+            tmp.resize(std::max<uint64_t>(rbsize, 1));
+            rb = tmp.data();
+        }
+    }
+    const uint64_t nread = pread(rb, rbsize, roff, &eof);
+    int rc = 0;
+    if (eof) {
+        rc = 2;
+    } else {
+        uint64_t ioff = roff / kSeg, cstart = 0, clen = rbsize;
+        bool check = true;
+        if (level == 2) {
+            if (roff % kSeg != 0) {
+                const uint64_t o = kSeg - roff % kSeg;
+                if (clen <= o) check = false;
+                else {
+                    cstart += o;
+                    clen -= o;
+                    ioff += 1;
+                }
+            }
+            const uint64_t end = roff + nread;
+            if (check && end != length && end % kSeg != 0) {
+                if (clen <= end % kSeg) check = false;
+                else clen -= end % kSeg;
+            }
+        }
+        if (check) {
+            const uint64_t nexp = clen ? (clen - 1) / kSeg + 1 : 1;
+            std::vector<uint8_t> ebuf(4 * nexp);
+            bool eof2 = false;
+            pread(ebuf.data(), 4 * nexp, length + ioff * 4, &eof2);
+            if (eof2) {
+                rc = 2;
+            } else if (clen) {
+                // the engine needs 16-B aligned input: copy the window into pinned staging
+                void *stage = nullptr;
+                int e = jfsx_alloc_pinned(c, clen, &stage);
+                if (e) return e;
+                memcpy(stage, rb + cstart, clen);
+                jfsx_range r;
+                memset(&r, 0, sizeof(r));
+                r.data = stage;
+                r.len = clen;
+                r.crc = ebuf.data();
+                e = jfsx_crc32c_segments(c, 1, &r, JFSX_CRC_VERIFY, JFSX_MEM_HOST);
+                jfsx_free_pinned(c, stage);
+                if (e) return e;
+                if (r.status == JFSX_ECRC) {
+                    rc = JFSX_ECRC;
+                    if (got) *got = r.got;
+                    if (expect) *expect = r.expect;
+                    *bad_seg = (int64_t)ioff + r.bad_seg;
+                }
+            }
+        }
+    }
+    if (!tmp.empty() || (level == 3 && rb != (uint8_t *)out)) {
+        if (rc == 0) {
+            const uint64_t avail = rbsize - (off - roff);
+            const uint64_t cpy = std::min(avail, size);
+            if (cpy) memcpy(out, rb + (off - roff), cpy);
+            *n_out = cpy;
+        } else {
+            *n_out = 0;
+        }
+    } else {
+        *n_out = nread;
+    }
+    return rc;
+}
+
+int jfsx_parse_header(const void *obj, uint64_t olen, int *klen, int *nlen) {
+    const uint8_t *o = (const uint8_t *)obj;
+    if (!o || olen < 3) return JFSX_EMISFORMED;
+    const int kl = ((int)o[0] << 8) + o[1], nl = o[2];
+    if (klen) *klen = kl;
+    if (nlen) *nlen = nl;
+    if ((uint64_t)(3 + kl + nl) >= olen) return JFSX_EMISFORMED;  // encrypt.go:199-201
+    return 0;
+}
+
+int jfsx_data_encrypt(jfsx_ctx *c, int algo, const uint8_t key[32], const uint8_t nonce[12], const uint8_t *wrapped,
+                      int wlen, const void *plaintext, uint64_t len, void *out, uint64_t out_cap, uint64_t *out_len) {
+    // encrypt.go:182-193: [BE16 klen][nlen][wrapped key][nonce][Seal(plaintext)]
+    if (!c || !key || !nonce || wlen < 0 || wlen > 65535 || (wlen && !wrapped) || !out) return JFSX_EINVAL;
+    const uint64_t hdr = 3 + (uint64_t)wlen + 12;
+    if (out_cap < hdr + len + 16) return JFSX_EINVAL;
+    uint8_t *o = (uint8_t *)out;
+    o[0] = (uint8_t)(wlen >> 8);
+    o[1] = (uint8_t)(wlen & 0xff);
+    o[2] = 12;
+    if (wlen) memcpy(o + 3, wrapped, wlen);
+    memcpy(o + 3 + wlen, nonce, 12);
+    jfsx_blk b;
+    memset(&b, 0, sizeof(b));
+    memcpy(b.key, key, 32);
+    memcpy(b.nonce, nonce, 12);
+    b.src = plaintext;
+    b.dst = o + hdr;
+    b.len = len;
+    int rc = jfsx_seal_batch(c, algo, 1, &b, JFSX_CRC_NONE, JFSX_MEM_HOST);
+    if (rc) return rc;
+    memcpy(o + hdr + len, b.tag, 16);
+    if (out_len) *out_len = hdr + len + 16;
+    return 0;
+}
+
+int jfsx_data_decrypt(jfsx_ctx *c, int algo, const uint8_t key[32], const void *obj, uint64_t olen, void *out,
+                      uint64_t out_cap, uint64_t *out_len) {
+    // encrypt.go:196-216
+    if (!c || !key || !obj || !out) return JFSX_EINVAL;
+    int kl = 0, nl = 0;
+    int rc = jfsx_parse_header(obj, olen, &kl, &nl);
+    if (rc) return rc;
+    const uint8_t *o = (const uint8_t *)obj;
+    if (nl != 12) return JFSX_ETAG;  // aead.Open rejects a wrong nonce size (recovered as an error upstream)
+    const uint64_t hdr = 3 + (uint64_t)kl + nl;
+    if (olen - hdr < 16) return JFSX_ETAG;  // shorter than the tag: cipher: message authentication failed
+    const uint64_t len = olen - hdr - 16;
+    if (out_cap < len) return JFSX_EINVAL;
+    jfsx_blk b;
+    memset(&b, 0, sizeof(b));
+    memcpy(b.key, key, 32);
+    memcpy(b.nonce, o + 3 + kl, 12);
+    b.src = o + hdr;
+    b.dst = out;
+    b.len = len;
+    memcpy(b.tag, o + hdr + len, 16);
+    rc = jfsx_open_batch(c, algo, 1, &b, JFSX_CRC_NONE, JFSX_MEM_HOST);
+    if (rc) return rc;
+    if (b.status == JFSX_ETAG) return JFSX_ETAG;
+    if (out_len) *out_len = len;
+    return 0;
+}
+
+int jfsx_gen_synthetic(jfsx_ctx *c, void *dst, uint64_t len, uint64_t seed, uint64_t block) {
+    if (!c || (len && !dst) || !aligned16(dst)) return JFSX_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    if (len) launch_gen_synthetic(c->stream, (uint8_t *)dst, len, seed, block);
+    HIP_OK(hipGetLastError());
+    return 0;
+}
+
+void jfsx_gen_key(uint64_t seed, uint64_t b, uint8_t key[32], uint8_t nonce[12]) {
+    auto mix64 = [](uint64_t z) {
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+        return z ^ (z >> 31);
+    };
+    const uint64_t G = 0x9E3779B97F4A7C15ULL;
+    for (int i = 0; i < 4; i++) {
+        uint64_t w = mix64((seed ^ 0x4B4559ULL) + G * ((b << 8) + i + 1));
+        memcpy(key + 8 * i, &w, 8);
+    }
+    uint64_t w0 = mix64((seed ^ 0x4E4F4E4345ULL) + G * ((b << 8) + 1));
+    uint64_t w1 = mix64((seed ^ 0x4E4F4E4345ULL) + G * ((b << 8) + 2));
+    memcpy(nonce, &w0, 8);
+    memcpy(nonce + 8, &w1, 4);
+}
+
+int jfsx_debug_tables(uint32_t *aes, uint32_t *crc, uint32_t *crcx) {
+    std::vector<uint32_t> a, c, x;
+    make_aes_table(a);
+    make_crc_tables(c, x);
+    if (aes) memcpy(aes, a.data(), 4 * a.size());
+    if (crc) memcpy(crc, c.data(), 4 * c.size());
+    if (crcx) memcpy(crcx, x.data(), 4 * x.size());
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,83 @@
+// jfsx_dev.h -- device helpers shared by the transform kernels (gfx950).
+#pragma once
+#include "jfsx_internal.h"
+
+namespace jfsx {
+
+__device__ __forceinline__ uint32_t lds_u32(const char *lds, uint32_t byteaddr) {
+    return *reinterpret_cast<const uint32_t *>(lds + byteaddr);
+}
+__device__ __forceinline__ uint4 lds_u4(const char *lds, uint32_t byteaddr) {
+    return *reinterpret_cast<const uint4 *>(lds + byteaddr);
+}
+
+#define CRC_T(t, x, k) lds_u32(lds, ((((x) >> (8 * (k))) & 0xffu) << 2) + CB + 1024u * (t))
+
+// crc_raw(A, 16-byte piece) = crc_raw(0, piece ^ shift(A, 1008 B) in the first word)
+template <uint32_t CB>
+__device__ __forceinline__ uint32_t crc_piece(const char *lds, uint32_t A, uint32_t p0, uint32_t p1, uint32_t p2,
+                                              uint32_t p3) {
+    uint32_t s = CRC_T(16, A, 0) ^ CRC_T(17, A, 1) ^ CRC_T(18, A, 2) ^ CRC_T(19, A, 3);
+    uint32_t q = p0 ^ s;
+    return CRC_T(0, q, 0) ^ CRC_T(1, q, 1) ^ CRC_T(2, q, 2) ^ CRC_T(3, q, 3) ^ CRC_T(4, p1, 0) ^ CRC_T(5, p1, 1) ^
+           CRC_T(6, p1, 2) ^ CRC_T(7, p1, 3) ^ CRC_T(8, p2, 0) ^ CRC_T(9, p2, 1) ^ CRC_T(10, p2, 2) ^
+           CRC_T(11, p2, 3) ^ CRC_T(12, p3, 0) ^ CRC_T(13, p3, 1) ^ CRC_T(14, p3, 2) ^ CRC_T(15, p3, 3);
+}
+
+// byte-serial tail: crc_raw(shift(A,1008), first n bytes of the piece)
+template <uint32_t CB>
+__device__ __noinline__ uint32_t crc_partial(const char *lds, uint32_t A, const uint32_t p[4], int n) {
+    uint32_t c = CRC_T(16, A, 0) ^ CRC_T(17, A, 1) ^ CRC_T(18, A, 2) ^ CRC_T(19, A, 3);
+    for (int i = 0; i < n; i++) {
+        uint32_t byte = (p[i >> 2] >> (8 * (i & 3))) & 0xffu;
+        c = lds_u32(lds, (((c ^ byte) & 0xffu) << 2) + CB + 1024u * 15) ^ (c >> 8);
+    }
+    return c;
+}
+
+// guarded 16-byte load of [o, o+16) clipped at end (zero fill)
+__device__ __forceinline__ uint4 load_piece(const uint8_t *src, uint64_t o, uint64_t end) {
+    if (o + 16 <= end) return *reinterpret_cast<const uint4 *>(src + o);
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (uint64_t i = o; i < end && i < o + 16; i++) w[(i - o) >> 2] |= (uint32_t)src[i] << (8 * ((i - o) & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ void store_piece(uint8_t *dst, uint64_t o, uint64_t end, uint4 v) {
+    if (o + 16 <= end) {
+        *reinterpret_cast<uint4 *>(dst + o) = v;
+        return;
+    }
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    for (uint64_t i = o; i < end && i < o + 16; i++) dst[i] = (uint8_t)(w[(i - o) >> 2] >> (8 * ((i - o) & 3)));
+}
+
+
+__device__ __forceinline__ void crc_verify_block(const BlkDev &blk, BlkOut &o, uint32_t lane) {
+    // compare computed (native) vs expected (BE bytes); first failing segment
+    const uint64_t nseg = (blk.len + kSeg - 1) / kSeg;
+    for (uint64_t base = 0; base < nseg; base += 64) {
+        const uint64_t s = base + lane;
+        bool bad = false;
+        uint32_t got = 0, ex = 0;
+        if (s < nseg) {
+            got = blk.crc_calc[s];
+            const uint8_t *e = blk.crc + 4 * s;
+            ex = ((uint32_t)e[0] << 24) | ((uint32_t)e[1] << 16) | ((uint32_t)e[2] << 8) | e[3];
+            bad = got != ex;
+        }
+        const uint64_t m = __ballot(bad);
+        if (m) {
+            const int first = __builtin_ctzll(m);
+            const uint32_t g2 = __shfl(got, first, 64), e2 = __shfl(ex, first, 64);
+            if (lane == 0) {
+                o.bad_seg = (int32_t)(base + first);
+                o.got = g2;
+                o.expect = e2;
+            }
+            return;
+        }
+    }
+}
+
+}  // namespace jfsx

@@ -1,0 +1,216 @@
+// jfsx_internal.h -- shared structures and device helpers of libjfsx (gfx950).
+//
+// Data layout in HBM (per batch, all device resident):
+//   BlkDev[n]      pointers/lengths of each block, slot range for partial tags
+//   KeyIn[n]       32-B key + 12-B nonce per block
+//   GcmSched[n]    per-key schedule written by gcm_keysetup (4.9 KiB/key)
+//   Task[t]        (block, byte range) handled by one workgroup
+//   partial[s]     per-wave GHASH / Poly1305 partial sums, s = task*16 + wave
+//   pexp[s]        power of H (or r) that lifts partial[s] to its final place
+//   crc scratch    computed CRCs for VERIFY mode (compared in finalize)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/jfsx.h"
+
+namespace jfsx {
+
+constexpr int kSeg = 32768;         // csBlock (disk_cache.go:1207)
+constexpr int kWaves = 16;          // waves per transform workgroup
+constexpr int kThreads = kWaves * 64;
+constexpr int kMaxTaskBytes = 4 << 20;
+constexpr uint32_t kCrcPoly = 0x82F63B78u;  // reflected Castagnoli
+
+struct KeyIn {
+    uint32_t key[8];
+    uint32_t nonce[3];
+    uint32_t pad;
+};
+
+struct BlkDev {
+    const uint8_t *src;
+    uint8_t *dst;
+    uint64_t len;
+    uint8_t *crc;          // GEN: BE32 out; VERIFY: expected BE32 in
+    uint32_t *crc_calc;    // VERIFY: computed CRCs (native u32), else null
+    uint32_t slot0;        // first partial slot of this block
+    uint32_t nslots;       // number of partial slots (16 per task)
+    const uint8_t *tag_in; // OPEN: expected tag (device copy), else null
+};
+
+struct Task {
+    uint32_t blk;
+    uint32_t slot0;
+    uint64_t c0, c1;  // byte range of the block; c0 % kSeg == 0
+};
+
+struct BlkOut {        // written by finalize, copied back to the host
+    uint32_t tag[4];
+    int32_t status;
+    int32_t bad_seg;
+    uint32_t got, expect;
+};
+
+// per-key AES-256-GCM schedule
+struct GcmSched {
+    uint32_t rk[60];         // round keys, little-endian dwords of the byte schedule
+    uint32_t k1[4];          // round-1 constants of the counter block (columns' constant terms ^ rk[4..7])
+    uint32_t c012[3];        // round-0 state words 0..2 (nonce ^ rk[0..2])
+    uint32_t pad;
+    uint32_t init[4];        // E_K(J0) ^ GHASH contribution of the length block (memory order)
+    uint32_t basis[128][4];  // x^i * H^64, memory order
+    uint32_t hpow[68][4];    // H^k, memory order (k = 0..67)
+    uint32_t h2k[32][4];     // H^(2^k), memory order
+};
+
+// per-key ChaCha20-Poly1305 schedule
+struct CpSched {
+    uint32_t key[8];
+    uint32_t nonce[3];
+    uint32_t pad0;
+    uint32_t s[4];           // Poly1305 s (key bytes 16..31 of keystream block 0)
+    uint32_t r256[5];        // r^256 (26-bit limbs) -- lane stride multiplier
+    uint32_t pad1[3];
+    uint32_t rpow[260][5];   // r^k (26-bit limbs), k = 0..259
+    uint32_t r2k[32][5];     // r^(2^k)
+    uint32_t init[5];        // r^1 * (length block) contribution, 26-bit limbs
+    uint32_t pad2[3];
+};
+
+// ---------------------------------------------------------------------------
+// GF(2^128) in GCM convention.  "BE words": w[0] holds bytes 0..3 big-endian;
+// bit 31 of w[0] is the coefficient of x^0.  Memory order = the 16 bytes as
+// stored, loaded as little-endian dwords (w[k] = bswap(d[k])).
+// ---------------------------------------------------------------------------
+struct g128 {
+    uint32_t w[4];
+};
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+__device__ __forceinline__ g128 g_from_mem(const uint32_t d[4]) {
+    g128 r;
+    for (int k = 0; k < 4; k++) r.w[k] = bswap32(d[k]);
+    return r;
+}
+__device__ __forceinline__ void g_to_mem(const g128 &a, uint32_t d[4]) {
+    for (int k = 0; k < 4; k++) d[k] = bswap32(a.w[k]);
+}
+
+// multiply by x (right shift in this convention, reduce with 0xE1 << 120)
+__device__ __forceinline__ g128 g_mulx(g128 v) {
+    uint32_t lsb = v.w[3] & 1u;
+    v.w[3] = __builtin_amdgcn_alignbit(v.w[2], v.w[3], 1);
+    v.w[2] = __builtin_amdgcn_alignbit(v.w[1], v.w[2], 1);
+    v.w[1] = __builtin_amdgcn_alignbit(v.w[0], v.w[1], 1);
+    v.w[0] = (v.w[0] >> 1) ^ (0xE1000000u & (0u - lsb));
+    return v;
+}
+
+// generic bit-serial product (SP 800-38D Algorithm 1)
+__device__ __noinline__ g128 g_mul(g128 x, g128 y) {
+    g128 z = {{0, 0, 0, 0}};
+    g128 v = y;
+#pragma unroll 1
+    for (int k = 0; k < 4; k++) {
+        uint32_t xw = x.w[k];
+#pragma unroll 8
+        for (int i = 0; i < 32; i++) {
+            uint32_t m = 0u - (xw >> 31);
+            xw <<= 1;
+            z.w[0] ^= v.w[0] & m;
+            z.w[1] ^= v.w[1] & m;
+            z.w[2] ^= v.w[2] & m;
+            z.w[3] ^= v.w[3] & m;
+            v = g_mulx(v);
+        }
+    }
+    return z;
+}
+
+// spread the low 16 bits of x to the even bit positions
+__device__ __forceinline__ uint32_t spread16(uint32_t x) {
+    x &= 0xFFFFu;
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    x = (x | (x << 1)) & 0x55555555u;
+    return x;
+}
+
+// squaring is linear over GF(2): coefficient i -> 2i, then reduce
+__device__ __forceinline__ g128 g_sqr(g128 a) {
+    uint32_t W[8];
+    for (int k = 0; k < 4; k++) {
+        W[2 * k] = spread16(a.w[k] >> 16) << 1;
+        W[2 * k + 1] = spread16(a.w[k]) << 1;
+    }
+    // high half H = W[4..7] (x^128..x^255): add H*(1 + x + x^2 + x^7) at x^0
+    uint32_t h0 = W[4], h1 = W[5], h2 = W[6], h3 = W[7];
+    uint32_t o = (h3 << 31) ^ (h3 << 30) ^ (h3 << 25);  // bits pushed past x^127
+    g128 r;
+    r.w[0] = W[0] ^ h0 ^ (h0 >> 1) ^ (h0 >> 2) ^ (h0 >> 7);
+    r.w[1] = W[1] ^ h1 ^ __builtin_amdgcn_alignbit(h0, h1, 1) ^ __builtin_amdgcn_alignbit(h0, h1, 2) ^
+             __builtin_amdgcn_alignbit(h0, h1, 7);
+    r.w[2] = W[2] ^ h2 ^ __builtin_amdgcn_alignbit(h1, h2, 1) ^ __builtin_amdgcn_alignbit(h1, h2, 2) ^
+             __builtin_amdgcn_alignbit(h1, h2, 7);
+    r.w[3] = W[3] ^ h3 ^ __builtin_amdgcn_alignbit(h2, h3, 1) ^ __builtin_amdgcn_alignbit(h2, h3, 2) ^
+             __builtin_amdgcn_alignbit(h2, h3, 7);
+    r.w[0] ^= o ^ (o >> 1) ^ (o >> 2) ^ (o >> 7);
+    return r;
+}
+
+// ---------------------------------------------------------------------------
+// CRC32C in GF(2)[x]/P, reflected: bit 31 is the coefficient of x^0.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+#pragma unroll 8
+    for (int i = 0; i < 32; i++) {
+        p ^= b & (0u - (a >> 31));
+        a <<= 1;
+        b = (b >> 1) ^ (kCrcPoly & (0u - (b & 1u)));
+    }
+    return p;
+}
+
+// x^(8n) mod P using x8pow[k] = x^(8*2^k) mod P
+__device__ __forceinline__ uint32_t crc_xpow8(uint64_t n, const uint32_t *x8pow) {
+    uint32_t r = 0x80000000u;  // x^0
+    for (int k = 0; n; k++, n >>= 1)
+        if (n & 1) r = crc_mulmod(x8pow[k], r);
+    return r;
+}
+
+// wave-wide XOR reduction
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
+    for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off, 64);
+    return v;
+}
+
+}  // namespace jfsx
+
+// launchers (defined in the .hip files, called by jfsx_api.cpp)
+struct JfsxTables;
+namespace jfsx {
+struct DevTables {
+    const uint32_t *aes;    // 16384 dwords: T0|T2 replicated x32 per index
+    const uint32_t *crc;    // 20 x 256 dwords: U0..U15 (slice-by-16), S0..S3 (shift 1008 B)
+    const uint32_t *crcx;   // 64 lane shift constants, 32 x8pow, K_full
+};
+void launch_gcm_keysetup(hipStream_t s, int n, const KeyIn *keys, const BlkDev *blks, GcmSched *sched,
+                         DevTables t);
+void launch_gcm_main(hipStream_t s, int ntasks, bool open, int crc_mode, const Task *tasks, const BlkDev *blks,
+                     const GcmSched *sched, uint32_t *partial, uint32_t *pexp, DevTables t);
+void launch_gcm_finalize(hipStream_t s, int n, bool open, int crc_mode, const BlkDev *blks, const GcmSched *sched,
+                         const uint32_t *partial, const uint32_t *pexp, BlkOut *out);
+void launch_cp_keysetup(hipStream_t s, int n, const KeyIn *keys, const BlkDev *blks, CpSched *sched);
+void launch_cp_main(hipStream_t s, int ntasks, bool open, int crc_mode, const Task *tasks, const BlkDev *blks,
+                    const CpSched *sched, uint32_t *partial, uint32_t *pexp, DevTables t);
+void launch_cp_finalize(hipStream_t s, int n, bool open, int crc_mode, const BlkDev *blks, const CpSched *sched,
+                        const uint32_t *partial, const uint32_t *pexp, BlkOut *out);
+void launch_crc_segments(hipStream_t s, int ntasks, const Task *tasks, const BlkDev *blks, DevTables t);
+void launch_crc_finalize(hipStream_t s, int n, int crc_mode, const BlkDev *blks, BlkOut *out);
+void launch_gen_synthetic(hipStream_t s, uint8_t *dst, uint64_t len, uint64_t seed, uint64_t block);
+}  // namespace jfsx

@@ -1,0 +1,339 @@
+"""ctypes binding of libjfsx.so (include/jfsx.h).
+
+This is the host side of the drop-in boundary.  Every compute call goes
+through the HIP library; there is no CPU fallback: if libjfsx.so is missing
+or no GPU is visible, constructing an Engine raises.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libjfsx.so")
+
+AES256GCM = 0
+CHACHA20P1305 = 1
+CRC_NONE, CRC_GEN, CRC_VERIFY = 0, 1, 2
+MEM_DEVICE, MEM_HOST = 0, 1
+OK, ETAG, ECRC = 0, 1, 2
+EINVAL, ENODEV, EIO, ENOMEM, EMISFORMED = -22, -19, -5, -12, -74
+SEG = 32 << 10
+
+# every symbol include/jfsx.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "jfsx_abi_version", "jfsx_device_count", "jfsx_ctx_open", "jfsx_ctx_close", "jfsx_ctx_sync",
+    "jfsx_ctx_stream", "jfsx_ctx_set_timing", "jfsx_ctx_kernel_time", "jfsx_alloc_pinned",
+    "jfsx_free_pinned", "jfsx_alloc_device", "jfsx_free_device", "jfsx_memcpy_h2d", "jfsx_memcpy_d2h",
+    "jfsx_seal_batch", "jfsx_open_batch", "jfsx_crc32c_segments", "jfsx_checksum", "jfsx_cache_verify",
+    "jfsx_data_encrypt", "jfsx_data_decrypt", "jfsx_parse_header", "jfsx_gen_synthetic", "jfsx_gen_key",
+    "jfsx_debug_tables",
+]
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code, what):
+        super().__init__("%s failed: jfsx error %d" % (what, code))
+        self.code = code
+
+
+class jfsx_blk(ctypes.Structure):
+    _fields_ = [
+        ("key", ctypes.c_uint8 * 32), ("nonce", ctypes.c_uint8 * 12), ("reserved", ctypes.c_uint32),
+        ("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("len", ctypes.c_uint64),
+        ("tag", ctypes.c_uint8 * 16), ("crc", ctypes.c_void_p), ("status", ctypes.c_int32),
+        ("crc_bad_seg", ctypes.c_int32), ("crc_got", ctypes.c_uint32), ("crc_expect", ctypes.c_uint32),
+    ]
+
+
+class jfsx_range(ctypes.Structure):
+    _fields_ = [
+        ("data", ctypes.c_void_p), ("len", ctypes.c_uint64), ("crc", ctypes.c_void_p),
+        ("status", ctypes.c_int32), ("bad_seg", ctypes.c_int32), ("got", ctypes.c_uint32),
+        ("expect", ctypes.c_uint32),
+    ]
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path=LIB_PATH):
+    """Load libjfsx.so and declare its signatures.  Raises if it is absent."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise ImportError("libjfsx.so not built (%s); run __graft_entry__.build()" % path)
+        L = ctypes.CDLL(path)
+        P, I, U64, U32, SZ = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_size_t
+        PP = ctypes.POINTER(ctypes.c_void_p)
+        sig = {
+            "jfsx_abi_version": (I, []),
+            "jfsx_device_count": (I, [ctypes.POINTER(I)]),
+            "jfsx_ctx_open": (I, [I, U32, PP]),
+            "jfsx_ctx_close": (I, [P]),
+            "jfsx_ctx_sync": (I, [P]),
+            "jfsx_ctx_stream": (P, [P]),
+            "jfsx_ctx_set_timing": (I, [P, I]),
+            "jfsx_ctx_kernel_time": (I, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64), I]),
+            "jfsx_alloc_pinned": (I, [P, SZ, PP]),
+            "jfsx_free_pinned": (I, [P, P]),
+            "jfsx_alloc_device": (I, [P, SZ, PP]),
+            "jfsx_free_device": (I, [P, P]),
+            "jfsx_memcpy_h2d": (I, [P, P, P, SZ]),
+            "jfsx_memcpy_d2h": (I, [P, P, P, SZ]),
+            "jfsx_seal_batch": (I, [P, I, I, ctypes.POINTER(jfsx_blk), I, I]),
+            "jfsx_open_batch": (I, [P, I, I, ctypes.POINTER(jfsx_blk), I, I]),
+            "jfsx_crc32c_segments": (I, [P, I, ctypes.POINTER(jfsx_range), I, I]),
+            "jfsx_checksum": (I, [P, P, U64, P]),
+            "jfsx_cache_verify": (I, [P, P, U64, U64, I, U64, U64, P, ctypes.POINTER(U64),
+                                      ctypes.POINTER(U32), ctypes.POINTER(U32), ctypes.POINTER(ctypes.c_int64)]),
+            "jfsx_data_encrypt": (I, [P, I, P, P, P, I, P, U64, P, U64, ctypes.POINTER(U64)]),
+            "jfsx_data_decrypt": (I, [P, I, P, P, U64, P, U64, ctypes.POINTER(U64)]),
+            "jfsx_parse_header": (I, [P, U64, ctypes.POINTER(I), ctypes.POINTER(I)]),
+            "jfsx_gen_synthetic": (I, [P, P, U64, U64, U64]),
+            "jfsx_gen_key": (None, [U64, U64, P, P]),
+            "jfsx_debug_tables": (I, [P, P, P]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+        return L
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    if isinstance(a, DeviceBuffer):
+        return a.ptr
+    if isinstance(a, int):
+        return a
+    raise TypeError(type(a))
+
+
+def _u8(b):
+    if isinstance(b, np.ndarray):
+        return np.ascontiguousarray(b.reshape(-1).view(np.uint8))
+    return np.frombuffer(bytes(b), dtype=np.uint8).copy()
+
+
+def debug_tables():
+    """Host-built lookup tables (no device needed)."""
+    L = load_library()
+    aes = np.empty(16384, np.uint32)
+    crc = np.empty(5120, np.uint32)
+    crcx = np.empty(128, np.uint32)
+    L.jfsx_debug_tables(aes.ctypes.data, crc.ctypes.data, crcx.ctypes.data)
+    return aes, crc, crcx
+
+
+def gen_key(seed, block):
+    key = np.empty(32, np.uint8)
+    nonce = np.empty(12, np.uint8)
+    load_library().jfsx_gen_key(seed, block, key.ctypes.data, nonce.ctypes.data)
+    return key.tobytes(), nonce.tobytes()
+
+
+def device_count():
+    n = ctypes.c_int()
+    rc = load_library().jfsx_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0
+
+
+class DeviceBuffer:
+    """Device memory owned by an Engine (hipMalloc through the C-ABI)."""
+
+    def __init__(self, eng, nbytes):
+        self.eng = eng
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        rc = eng.L.jfsx_alloc_device(eng.ctx, max(self.nbytes, 16), ctypes.byref(p))
+        if rc:
+            raise EngineError(rc, "jfsx_alloc_device(%d)" % nbytes)
+        self.ptr = p.value
+
+    def free(self):
+        if self.ptr:
+            self.eng.L.jfsx_free_device(self.eng.ctx, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def upload(self, host, offset=0):
+        h = _u8(host)
+        if h.size:
+            self.eng._check(self.eng.L.jfsx_memcpy_h2d(self.eng.ctx, self.ptr + offset, h.ctypes.data, h.size),
+                            "h2d")
+
+    def download(self, nbytes=None, offset=0):
+        n = self.nbytes - offset if nbytes is None else nbytes
+        out = np.empty(max(n, 1), np.uint8)
+        if n:
+            self.eng._check(self.eng.L.jfsx_memcpy_d2h(self.eng.ctx, out.ctypes.data, self.ptr + offset, n), "d2h")
+        return out[:n]
+
+
+class Engine:
+    """One GPU context (device ordinal + HIP stream + workspace)."""
+
+    def __init__(self, device=0):
+        self.L = load_library()
+        if device_count() <= device:
+            raise RuntimeError("jfsx: no HIP device %d visible (the engine has no CPU path)" % device)
+        ctx = ctypes.c_void_p()
+        rc = self.L.jfsx_ctx_open(device, 0, ctypes.byref(ctx))
+        if rc:
+            raise EngineError(rc, "jfsx_ctx_open(%d)" % device)
+        self.ctx = ctx.value
+        self.device = device
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.L.jfsx_ctx_close(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc:
+            raise EngineError(rc, what)
+
+    # -- memory ----------------------------------------------------------
+    def alloc(self, nbytes):
+        return DeviceBuffer(self, nbytes)
+
+    def gen_synthetic(self, buf, length, seed, block, offset=0):
+        self._check(self.L.jfsx_gen_synthetic(self.ctx, buf.ptr + offset, length, seed, block), "gen_synthetic")
+
+    def sync(self):
+        self._check(self.L.jfsx_ctx_sync(self.ctx), "sync")
+
+    def set_timing(self, on):
+        self.L.jfsx_ctx_set_timing(self.ctx, 1 if on else 0)
+
+    def kernel_time(self, reset=True):
+        ms = ctypes.c_double()
+        n = ctypes.c_uint64()
+        self.L.jfsx_ctx_kernel_time(self.ctx, ctypes.byref(ms), ctypes.byref(n), 1 if reset else 0)
+        return ms.value, n.value
+
+    # -- batches -----------------------------------------------------------
+    @staticmethod
+    def make_blocks(specs):
+        """specs: iterable of dicts with key, nonce, src, dst, len, [tag], [crc] (pointers as ints)."""
+        specs = list(specs)
+        arr = (jfsx_blk * max(len(specs), 1))()
+        for i, s in enumerate(specs):
+            b = arr[i]
+            ctypes.memmove(b.key, bytes(s["key"]), 32)
+            ctypes.memmove(b.nonce, bytes(s["nonce"]), 12)
+            b.src = s.get("src")
+            b.dst = s.get("dst")
+            b.len = s["len"]
+            if s.get("tag") is not None:
+                ctypes.memmove(b.tag, bytes(s["tag"]), 16)
+            b.crc = s.get("crc")
+        return arr, len(specs)
+
+    def seal_batch(self, algo, blks, n, crc_mode=CRC_GEN, mem=MEM_DEVICE):
+        self._check(self.L.jfsx_seal_batch(self.ctx, algo, n, blks, crc_mode, mem), "jfsx_seal_batch")
+
+    def open_batch(self, algo, blks, n, crc_mode=CRC_NONE, mem=MEM_DEVICE):
+        self._check(self.L.jfsx_open_batch(self.ctx, algo, n, blks, crc_mode, mem), "jfsx_open_batch")
+
+    def crc32c_segments(self, ranges, n, mode=CRC_GEN, mem=MEM_DEVICE):
+        self._check(self.L.jfsx_crc32c_segments(self.ctx, n, ranges, mode, mem), "jfsx_crc32c_segments")
+
+    # -- host-memory conveniences -------------------------------------------
+    def seal(self, algo, key, nonce, plaintext, crc=False):
+        """Seal one host buffer; returns (ciphertext, tag[, crc bytes])."""
+        p = _u8(plaintext)
+        out = np.empty(max(p.size, 1), np.uint8)
+        cbuf = np.zeros(4 * max(1, -(-p.size // SEG)), np.uint8)
+        arr, n = self.make_blocks([{"key": key, "nonce": nonce, "src": p.ctypes.data if p.size else None,
+                                    "dst": out.ctypes.data, "len": p.size,
+                                    "crc": cbuf.ctypes.data if crc else None}])
+        self.seal_batch(algo, arr, n, CRC_GEN if crc else CRC_NONE, MEM_HOST)
+        c, tag = out[:p.size].tobytes(), bytes(arr[0].tag)
+        return (c, tag, cbuf.tobytes()) if crc else (c, tag)
+
+    def open(self, algo, key, nonce, ciphertext, tag, crc=None):
+        """Open one host buffer; returns plaintext or None on authentication failure."""
+        c = _u8(ciphertext)
+        out = np.zeros(max(c.size, 1), np.uint8)
+        cb = _u8(crc) if crc is not None else None
+        arr, n = self.make_blocks([{"key": key, "nonce": nonce, "src": c.ctypes.data if c.size else None,
+                                    "dst": out.ctypes.data, "len": c.size, "tag": tag,
+                                    "crc": cb.ctypes.data if cb is not None else None}])
+        self.open_batch(algo, arr, n, CRC_VERIFY if cb is not None else CRC_NONE, MEM_HOST)
+        b = arr[0]
+        if b.status == ETAG:
+            return None
+        if b.status == ECRC:
+            raise ChecksumError(b.crc_got, b.crc_expect, b.crc_bad_seg)
+        return out[:c.size].tobytes()
+
+    def checksum(self, data):
+        d = _u8(data)
+        out = np.empty(4 * max(1, -(-d.size // SEG)), np.uint8)
+        self._check(self.L.jfsx_checksum(self.ctx, d.ctypes.data if d.size else None, d.size, out.ctypes.data),
+                    "jfsx_checksum")
+        return out.tobytes()
+
+    def cache_verify(self, file_img, length, level, off, size):
+        """cacheFile.ReadAt on an in-memory cache file image.
+        Returns (rc, data, n, got, expect, bad_seg)."""
+        f = _u8(file_img)
+        out = np.zeros(max(size, 1), np.uint8)
+        n = ctypes.c_uint64()
+        got = ctypes.c_uint32()
+        exp = ctypes.c_uint32()
+        seg = ctypes.c_int64()
+        rc = self.L.jfsx_cache_verify(self.ctx, f.ctypes.data, f.size, length, level, off, size, out.ctypes.data,
+                                      ctypes.byref(n), ctypes.byref(got), ctypes.byref(exp), ctypes.byref(seg))
+        if rc < 0:
+            raise EngineError(rc, "jfsx_cache_verify")
+        return rc, out[:size].tobytes(), n.value, got.value, exp.value, seg.value
+
+    def data_encrypt(self, algo, key, nonce, wrapped, plaintext):
+        p = _u8(plaintext)
+        cap = 3 + len(wrapped) + 12 + p.size + 16
+        out = np.empty(cap, np.uint8)
+        w = _u8(wrapped)
+        olen = ctypes.c_uint64()
+        self._check(self.L.jfsx_data_encrypt(self.ctx, algo, bytes(key), bytes(nonce),
+                                             w.ctypes.data if w.size else None, w.size,
+                                             p.ctypes.data if p.size else None, p.size, out.ctypes.data, cap,
+                                             ctypes.byref(olen)), "jfsx_data_encrypt")
+        return out[:olen.value].tobytes()
+
+    def data_decrypt(self, algo, key, obj):
+        o = _u8(obj)
+        out = np.empty(max(o.size, 1), np.uint8)
+        olen = ctypes.c_uint64()
+        rc = self.L.jfsx_data_decrypt(self.ctx, algo, bytes(key), o.ctypes.data, o.size, out.ctypes.data,
+                                      out.size, ctypes.byref(olen))
+        return rc, out[:olen.value].tobytes() if rc == 0 else b""
+
+
+class ChecksumError(Exception):
+    """"data checksum %d != expect %d" (pkg/chunk/disk_cache.go:1324)."""
+
+    def __init__(self, got, expect, seg=-1):
+        super().__init__("data checksum %d != expect %d" % (got, expect))
+        self.got, self.expect, self.seg = got, expect, seg
