@@ -15,8 +15,8 @@ def pytest_configure(config):
 
 def _gpu_available():
     try:
-        import torch
-        return torch.cuda.is_available()
+        from juicefs_amd import engine
+        return engine.device_count() > 0
     except Exception:
         return False
 
