@@ -38,6 +38,7 @@ def parse():
     ap.add_argument("--algo", choices=["aes256gcm", "chacha20poly1305"], default="aes256gcm")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--crc", choices=["full", "none"], default="full", help="seal: CRC32C full or none (ablation)")
     ap.add_argument("--verify", type=int, default=4, help="blocks re-checked against the oracle after timing")
     return ap.parse_args()
 
@@ -133,7 +134,7 @@ def main():
         blks, n = eng.make_blocks(specs)
         if args.mode == "seal":
             def step():
-                eng.seal_batch(algo, blks, n, E.CRC_GEN, E.MEM_DEVICE)
+                eng.seal_batch(algo, blks, n, E.CRC_GEN if args.crc == "full" else E.CRC_NONE, E.MEM_DEVICE)
         else:
             # Open + CRC verify (BASELINE configs[3]): make a sealed image first
             eng.seal_batch(algo, blks, n, E.CRC_GEN, E.MEM_DEVICE)

@@ -187,7 +187,7 @@ Plan plan_tasks(const std::vector<uint64_t> &lens, uint64_t seg_per_task_max) {
             t.c0 = c0;
             t.c1 = std::min(c0 + ch, lens[b]);
             p.tasks.push_back(t);
-            p.nslots += kWaves;
+            p.nslots += kSlotsPerTask;
         }
     }
     return p;
@@ -254,7 +254,7 @@ int run_aead(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mo
     for (size_t t = 0; t < nt; t++) {
         BlkDev &bd = hb[plan.tasks[t].blk];
         if (bd.nslots == 0) bd.slot0 = plan.tasks[t].slot0;
-        bd.nslots += kWaves;
+        bd.nslots += kSlotsPerTask;
     }
     if (nt) memcpy(h + o_task, plan.tasks.data(), sizeof(Task) * nt);
     hipStream_t s = c->stream;
@@ -465,7 +465,7 @@ int jfsx_ctx_open(int device, uint32_t flags, jfsx_ctx **out) {
     make_crc_tables(crc, crcx);
     const size_t nbytes = 4 * (aes.size() + crc.size() + crcx.size());
     if (hipMalloc((void **)&c->d_tab, nbytes) != hipSuccess) {
-        hipStreamDestroy(c->stream);
+        (void)hipStreamDestroy(c->stream);
         delete c;
         return JFSX_ENOMEM;
     }
@@ -490,15 +490,15 @@ int jfsx_ctx_open(int device, uint32_t flags, jfsx_ctx **out) {
 
 int jfsx_ctx_close(jfsx_ctx *c) {
     if (!c) return JFSX_EINVAL;
-    hipSetDevice(c->device);
-    if (c->stream) hipStreamSynchronize(c->stream);
-    if (c->d_tab) hipFree(c->d_tab);
-    if (c->d_ws) hipFree(c->d_ws);
-    if (c->d_stage) hipFree(c->d_stage);
-    if (c->h_ws) hipHostFree(c->h_ws);
-    if (c->ev0) hipEventDestroy(c->ev0);
-    if (c->ev1) hipEventDestroy(c->ev1);
-    if (c->stream) hipStreamDestroy(c->stream);
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->d_tab) (void)hipFree(c->d_tab);
+    if (c->d_ws) (void)hipFree(c->d_ws);
+    if (c->d_stage) (void)hipFree(c->d_stage);
+    if (c->h_ws) (void)hipHostFree(c->h_ws);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return 0;
 }

@@ -17,11 +17,14 @@ __device__ __forceinline__ uint4 lds_u4(const char *lds, uint32_t byteaddr) {
 template <uint32_t CB>
 __device__ __forceinline__ uint32_t crc_piece(const char *lds, uint32_t A, uint32_t p0, uint32_t p1, uint32_t p2,
                                               uint32_t p3) {
-    uint32_t s = CRC_T(16, A, 0) ^ CRC_T(17, A, 1) ^ CRC_T(18, A, 2) ^ CRC_T(19, A, 3);
+#define X3(a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), 0x96)
+    uint32_t s = X3(CRC_T(16, A, 0), CRC_T(17, A, 1), CRC_T(18, A, 2)) ^ CRC_T(19, A, 3);
     uint32_t q = p0 ^ s;
-    return CRC_T(0, q, 0) ^ CRC_T(1, q, 1) ^ CRC_T(2, q, 2) ^ CRC_T(3, q, 3) ^ CRC_T(4, p1, 0) ^ CRC_T(5, p1, 1) ^
-           CRC_T(6, p1, 2) ^ CRC_T(7, p1, 3) ^ CRC_T(8, p2, 0) ^ CRC_T(9, p2, 1) ^ CRC_T(10, p2, 2) ^
-           CRC_T(11, p2, 3) ^ CRC_T(12, p3, 0) ^ CRC_T(13, p3, 1) ^ CRC_T(14, p3, 2) ^ CRC_T(15, p3, 3);
+    return X3(X3(X3(CRC_T(0, q, 0), CRC_T(1, q, 1), CRC_T(2, q, 2)), X3(CRC_T(3, q, 3), CRC_T(4, p1, 0), CRC_T(5, p1, 1)),
+                 X3(CRC_T(6, p1, 2), CRC_T(7, p1, 3), CRC_T(8, p2, 0))),
+              X3(CRC_T(9, p2, 1), CRC_T(10, p2, 2), CRC_T(11, p2, 3)),
+              X3(CRC_T(12, p3, 0), CRC_T(13, p3, 1), X3(CRC_T(14, p3, 2), CRC_T(15, p3, 3), 0u)));
+#undef X3
 }
 
 // byte-serial tail: crc_raw(shift(A,1008), first n bytes of the piece)

@@ -30,71 +30,230 @@ namespace jfsx {
 // LDS map of gcm_main (bytes): [0, 64K) AES T0|T2, [64K, 128K) GHASH table,
 // [128K, 148K) CRC tables, [148K, +2K) GHASH basis staging.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kLdsAes = 0;
-constexpr uint32_t kLdsGh = 65536;
+constexpr uint32_t kLdsGh = 0;       // GHASH T[b][j]: byte (b << 8) | (j << 4)
+constexpr uint32_t kLdsAes = 65536;  // AES [idx][T0 x32 | T2 x32]: byte 65536 | (idx << 8) | (r << 2)
 constexpr uint32_t kLdsCrc = 131072;
 constexpr uint32_t kLdsBasis = 131072 + 20480;
 constexpr uint32_t kLdsBytes = kLdsBasis + 2048;
 
 __device__ __forceinline__ uint32_t rotl8(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 24); }
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
 
-// byte k of w moved to bits 8..15, lane offset kept in bits 0..7: the byte
-// address of T0[byte] for this lane's replica (v_perm_b32, one VALU op)
-#define AES_SEL(k) (0x0c0c0000u | ((4u + (k)) << 8))
+// byte k of w moved to bits 8..15, the lane's replica offset (bits 0..7) and the
+// table base (bit 16) taken from loff: the LDS byte address of T0[byte] for this
+// lane's replica in one v_perm_b32
+#define AES_SEL(k) (0x0c020000u | ((4u + (k)) << 8))
 #define TA(w, k) lds_u32(lds, __builtin_amdgcn_perm((w), loff, AES_SEL(k)))
 #define TB(w, k) lds_u32(lds, __builtin_amdgcn_perm((w), loff, AES_SEL(k)) + 128u)
 
-// One full AES round on LE column words (T1 = rotl8 T0, T3 = rotl8 T2).
-#define AES_ROUND(o0, o1, o2, o3, i0, i1, i2, i3, r)                                        \
-    o0 = TA(i0, 0) ^ rotl8(TA(i1, 1)) ^ TB(i2, 2) ^ rotl8(TB(i3, 3)) ^ rk[4 * (r) + 0];      \
-    o1 = TA(i1, 0) ^ rotl8(TA(i2, 1)) ^ TB(i3, 2) ^ rotl8(TB(i0, 3)) ^ rk[4 * (r) + 1];      \
-    o2 = TA(i2, 0) ^ rotl8(TA(i3, 1)) ^ TB(i0, 2) ^ rotl8(TB(i1, 3)) ^ rk[4 * (r) + 2];      \
-    o3 = TA(i3, 0) ^ rotl8(TA(i0, 1)) ^ TB(i1, 2) ^ rotl8(TB(i2, 3)) ^ rk[4 * (r) + 3];
+// One full AES round on LE column words.  T1 = rotl8 T0 and T3 = rotl8 T2, and
+// rotl8(a) ^ rotl8(b) = rotl8(a ^ b), so a column costs 4 v_perm (addresses),
+// 4 ds_read_b32, one xor, one alignbit and one 3-input xor (v_bitop3 0x96).
+#define AES_COL(o, i0, i1, i2, i3, rkv) \
+    o = xor3(TA(i0, 0), TB(i2, 2), rotl8(TA(i1, 1) ^ TB(i3, 3))) ^ (rkv);
+#define AES_ROUND(o0, o1, o2, o3, i0, i1, i2, i3, r) \
+    AES_COL(o0, i0, i1, i2, i3, rk[4 * (r) + 0])     \
+    AES_COL(o1, i1, i2, i3, i0, rk[4 * (r) + 1])     \
+    AES_COL(o2, i2, i3, i0, i1, rk[4 * (r) + 2])     \
+    AES_COL(o3, i3, i0, i1, i2, rk[4 * (r) + 3])
 
-#define AES_LAST(o, a, b, c, d, rkv) \
-    o = ((TB(a, 0) & 0xffu) | (TA(b, 1) & 0xff00u) | (TA(c, 2) & 0xff0000u) | (TB(d, 3) & 0xff000000u)) ^ (rkv);
+// last round: S-box bytes are byte 0 of T2, bytes 1/2 of T0, byte 3 of T2
+#define AES_LAST(o, a, b, c, d, rkv)                                                             \
+    o = __builtin_amdgcn_bitop3_b32(                                                             \
+            __builtin_amdgcn_bitop3_b32(TB(a, 0), TA(b, 1), 0xffu, 0xe4) /* select: c ? a : b */,       \
+            __builtin_amdgcn_bitop3_b32(TA(c, 2), TB(d, 3), 0x00ff0000u, 0xe4),                 \
+            0x0000ffffu, 0xe4) ^ (rkv);
 
-// Keystream block for counter value ctr (the BE32 in bytes 12..15).
-__device__ __forceinline__ void aes_ctr_block(const char *lds, uint32_t loff, const uint32_t *rk,
-                                              const uint32_t *k1, uint32_t ctr, uint32_t ks[4]) {
-    uint32_t x3 = __builtin_bswap32(ctr) ^ rk[3];
-    // round 1: columns' constant terms precomputed (k1); only x3 varies
-    uint32_t a0 = k1[0] ^ rotl8(TB(x3, 3));
-    uint32_t a1 = k1[1] ^ TB(x3, 2);
-    uint32_t a2 = k1[2] ^ rotl8(TA(x3, 1));
-    uint32_t a3 = k1[3] ^ TA(x3, 0);
-    uint32_t b0, b1, b2, b3;
-    AES_ROUND(b0, b1, b2, b3, a0, a1, a2, a3, 2);
-    AES_ROUND(a0, a1, a2, a3, b0, b1, b2, b3, 3);
-    AES_ROUND(b0, b1, b2, b3, a0, a1, a2, a3, 4);
-    AES_ROUND(a0, a1, a2, a3, b0, b1, b2, b3, 5);
-    AES_ROUND(b0, b1, b2, b3, a0, a1, a2, a3, 6);
-    AES_ROUND(a0, a1, a2, a3, b0, b1, b2, b3, 7);
-    AES_ROUND(b0, b1, b2, b3, a0, a1, a2, a3, 8);
-    AES_ROUND(a0, a1, a2, a3, b0, b1, b2, b3, 9);
-    AES_ROUND(b0, b1, b2, b3, a0, a1, a2, a3, 10);
-    AES_ROUND(a0, a1, a2, a3, b0, b1, b2, b3, 11);
-    AES_ROUND(b0, b1, b2, b3, a0, a1, a2, a3, 12);
-    AES_ROUND(a0, a1, a2, a3, b0, b1, b2, b3, 13);
-    AES_LAST(ks[0], a0, a1, a2, a3, rk[56]);
-    AES_LAST(ks[1], a1, a2, a3, a0, rk[57]);
-    AES_LAST(ks[2], a2, a3, a0, a1, rk[58]);
-    AES_LAST(ks[3], a3, a0, a1, a2, rk[59]);
-}
-
-// acc * H^64 with the byte-sliced table: XOR_j T[j][byte_j(acc)]
-__device__ __forceinline__ void ghash_mul_tab(const char *lds, uint32_t acc[4]) {
-    uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
+// Keystream blocks for NS independent counters (the chains interleave for ILP).
+template <int NS>
+__device__ __forceinline__ void aes_ctr_blocks(const char *lds, uint32_t loff, const uint32_t *rk, const uint32_t *k1,
+                                               const uint32_t (&ctr)[NS], uint32_t (&ks)[NS][4]) {
+    uint32_t a[NS][4], b[NS][4];
 #pragma unroll
-    for (int j = 0; j < 16; j++) {
-        uint32_t b = (acc[j >> 2] >> (8 * (j & 3))) & 0xffu;
-        uint4 t = lds_u4(lds, (b << 4) + kLdsGh + 4096u * j);
-        z0 ^= t.x; z1 ^= t.y; z2 ^= t.z; z3 ^= t.w;
+    for (int s = 0; s < NS; s++) {
+        const uint32_t x3 = __builtin_bswap32(ctr[s]) ^ rk[3];
+        // round 1: the columns' constant terms are precomputed (k1); only x3 varies
+        a[s][0] = k1[0] ^ rotl8(TB(x3, 3));
+        a[s][1] = k1[1] ^ TB(x3, 2);
+        a[s][2] = k1[2] ^ rotl8(TA(x3, 1));
+        a[s][3] = k1[3] ^ TA(x3, 0);
     }
-    acc[0] = z0; acc[1] = z1; acc[2] = z2; acc[3] = z3;
+#pragma unroll
+    for (int r = 2; r <= 13; r += 2) {
+#pragma unroll
+        for (int s = 0; s < NS; s++) { AES_ROUND(b[s][0], b[s][1], b[s][2], b[s][3], a[s][0], a[s][1], a[s][2], a[s][3], r); }
+#pragma unroll
+        for (int s = 0; s < NS; s++) { AES_ROUND(a[s][0], a[s][1], a[s][2], a[s][3], b[s][0], b[s][1], b[s][2], b[s][3], r + 1); }
+    }
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        AES_LAST(ks[s][0], a[s][0], a[s][1], a[s][2], a[s][3], rk[56]);
+        AES_LAST(ks[s][1], a[s][1], a[s][2], a[s][3], a[s][0], rk[57]);
+        AES_LAST(ks[s][2], a[s][2], a[s][3], a[s][0], a[s][1], rk[58]);
+        AES_LAST(ks[s][3], a[s][3], a[s][0], a[s][1], a[s][2], rk[59]);
+    }
 }
 
+// GHASH "multiply by H^64" with the byte-sliced table T[b][j] = (byte b at
+// position j) * H^64.  Bank-conflict-free: lane l keeps its accumulator rotated
+// by k = (l & 15) >> 2 dwords (R[i] = acc[(i + k) & 3]) and visits the 16 byte
+// positions in the lane-dependent order j(t) = 4((t/4 + k) & 3) + ((t + l) & 3),
+// so the 16 lanes of every ds_read_b128 group read 16 distinct 16-byte slots
+// (slot = j).  One v_perm per lookup builds (b << 8) | (j << 4).
+struct GhLane {
+    uint32_t sel[4];  // v_perm selectors: byte0 <- off byte t&3, byte1 <- R[t/4] byte (t + l) & 3
+    uint32_t off[4];  // j(t) << 4 for t = 4*dd + 0..3, one byte each
+    bool r1, r2;      // rotation bits of k
+};
+
+__device__ __forceinline__ GhLane gh_lane(uint32_t lane) {
+    GhLane g;
+    const uint32_t q = lane & 15, k = q >> 2;
+#pragma unroll
+    for (int bb = 0; bb < 4; bb++) g.sel[bb] = 0x0c0c0000u | ((4u + ((bb + q) & 3)) << 8) | (uint32_t)bb;
+#pragma unroll
+    for (int dd = 0; dd < 4; dd++) {
+        uint32_t o = 0;
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) {
+            const uint32_t j = 4 * ((dd + k) & 3) + ((bb + q) & 3);
+            o |= (j << 4) << (8 * bb);
+        }
+        g.off[dd] = o;
+    }
+    g.r1 = (k & 1) != 0;
+    g.r2 = (k & 2) != 0;
+    return g;
+}
+
+// R = rho(a): R[i] = a[(i + k) & 3]
+__device__ __forceinline__ void gh_rho(const uint32_t a[4], const GhLane &g, uint32_t R[4]) {
+    uint32_t u[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) u[i] = g.r2 ? a[(i + 2) & 3] : a[i];
+#pragma unroll
+    for (int i = 0; i < 4; i++) R[i] = g.r1 ? u[(i + 1) & 3] : u[i];
+}
+// a = rho^-1(R): a[i] = R[(i - k) & 3]
+__device__ __forceinline__ void gh_rho_inv(const uint32_t R[4], const GhLane &g, uint32_t a[4]) {
+    uint32_t u[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) u[i] = g.r1 ? R[(i + 3) & 3] : R[i];
+#pragma unroll
+    for (int i = 0; i < 4; i++) a[i] = g.r2 ? u[(i + 2) & 3] : u[i];
+}
+
+// One Horner step in the rotated frame: R <- rho(unrho(R) * H^64 ^ c)
+__device__ __forceinline__ void ghash_step(const char *lds, uint32_t R[4], const GhLane &g, uint4 c) {
+    uint4 t[16];
+#pragma unroll
+    for (int dd = 0; dd < 4; dd++)
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++)
+            t[4 * dd + bb] = lds_u4(lds, kLdsGh + __builtin_amdgcn_perm(R[dd], g.off[dd], g.sel[bb]));
+    // 16-way XOR as a 3-input tree (v_bitop3), then the new block
+#define GX(f, cf) xor3(xor3(xor3(t[0].f, t[1].f, t[2].f), xor3(t[3].f, t[4].f, t[5].f), xor3(t[6].f, t[7].f, t[8].f)), \
+                       xor3(t[9].f, t[10].f, t[11].f), xor3(xor3(t[12].f, t[13].f, t[14].f), t[15].f, cf))
+    const uint32_t S[4] = {GX(x, c.x), GX(y, c.y), GX(z, c.z), GX(w, c.w)};
+#undef GX
+    gh_rho(S, g, R);
+}
+
+// Per-stream state of one wave: a contiguous, segment-aligned sub-chunk.
+struct Stream {
+    uint64_t sub0, sub1;  // byte range of the block
+    uint32_t acc[4];      // GHASH lane accumulator, memory order, rotated by rho (see GhLane)
+    uint64_t jlast;       // last 16-B block index folded into acc
+    bool has;
+    uint32_t A, lend;     // CRC lane accumulator, end of its last piece (segment relative)
+    uint64_t seg0;        // start of the current segment
+};
+
+// CRC32C of one finished segment: shift lane CRCs to the segment end, reduce, store
+template <int CRCMODE>
+__device__ __forceinline__ void crc_segment_end(const BlkDev &blk, const DevTables &tab, uint32_t lane, uint32_t xl,
+                                                uint64_t seg0, uint64_t seg1, uint32_t A, uint32_t lend) {
+    const uint32_t Lseg = (uint32_t)(seg1 - seg0);
+    uint32_t v, K;
+    if (Lseg == (uint32_t)kSeg) {
+        v = crc_mulmod(xl, A);
+        K = tab.crcx[96];
+    } else {
+        v = crc_mulmod(crc_xpow8(Lseg - lend, tab.crcx + 64), A);
+        K = crc_mulmod(crc_xpow8(Lseg, tab.crcx + 64), 0xffffffffu);
+    }
+    const uint32_t raw = wave_xor(v);
+    if (lane == 0) {
+        const uint32_t crc = ~(K ^ raw);
+        const uint64_t si = seg0 / kSeg;
+        if (CRCMODE == 1)
+            *reinterpret_cast<uint32_t *>(blk.crc + 4 * si) = __builtin_bswap32(crc);
+        else
+            blk.crc_calc[si] = crc;
+    }
+}
+
+// Generic (guarded) processing of one row of one stream: handles the ragged
+// tail of a block (partial 16-B piece, lanes past the end, partial segment).
 template <bool OPEN, int CRCMODE>
+__device__ __noinline__ Stream row_generic(const char *lds, uint32_t loff, const GhLane gl, const GcmSched *sch,
+                                           const BlkDev blk, const DevTables tab, uint32_t lane, uint32_t xl, Stream st,
+                                           uint64_t row) {
+    uint32_t rk[60];
+#pragma unroll
+    for (int i = 0; i < 60; i++) rk[i] = sch->rk[i];
+    const uint32_t k1[4] = {sch->k1[0], sch->k1[1], sch->k1[2], sch->k1[3]};
+    const uint64_t o = row + 16 * lane;
+    const uint64_t end = st.sub1;
+    const bool valid = o < end, full = o + 16 <= end;
+    uint4 d = load_piece(blk.src, o, end);
+    const uint32_t ctr[1] = {(uint32_t)((o >> 4) + 2)};
+    uint32_t ks[1][4];
+    aes_ctr_blocks<1>(lds, loff, rk, k1, ctr, ks);
+    uint4 x = make_uint4(d.x ^ ks[0][0], d.y ^ ks[0][1], d.z ^ ks[0][2], d.w ^ ks[0][3]);
+    uint4 c = OPEN ? d : x, p = OPEN ? x : d;
+    if (!full) {
+        const int nv = valid ? (int)(end - o) : 0;
+        uint32_t m[4];
+        for (int k = 0; k < 4; k++) {
+            int bytes = nv - 4 * k;
+            m[k] = bytes >= 4 ? 0xffffffffu : (bytes <= 0 ? 0u : ((1u << (8 * bytes)) - 1u));
+        }
+        c.x &= m[0]; c.y &= m[1]; c.z &= m[2]; c.w &= m[3];
+        p.x &= m[0]; p.y &= m[1]; p.z &= m[2]; p.w &= m[3];
+    }
+    if (valid) store_piece(blk.dst, o, end, OPEN ? p : c);
+    uint32_t t[4] = {st.acc[0], st.acc[1], st.acc[2], st.acc[3]};
+    ghash_step(lds, t, gl, c);
+    if (valid) {
+        st.acc[0] = t[0]; st.acc[1] = t[1]; st.acc[2] = t[2]; st.acc[3] = t[3];
+        st.jlast = o >> 4;
+        st.has = true;
+    }
+    if (CRCMODE) {
+        if (full) {
+            st.A = crc_piece<kLdsCrc>(lds, st.A, p.x, p.y, p.z, p.w);
+            st.lend = (uint32_t)(o + 16 - st.seg0);
+        } else if (valid) {
+            const uint32_t pw[4] = {p.x, p.y, p.z, p.w};
+            st.A = crc_partial<kLdsCrc>(lds, st.A, pw, (int)(end - o));
+            st.lend = (uint32_t)(end - st.seg0);
+        }
+        const uint64_t seg1 = st.seg0 + kSeg < end ? st.seg0 + kSeg : end;
+        if (row + 1024 >= seg1) {
+            crc_segment_end<CRCMODE>(blk, tab, lane, xl, st.seg0, seg1, st.A, st.lend);
+            st.A = 0;
+            st.lend = 0;
+            st.seg0 = seg1;
+        }
+    }
+    return st;
+}
+
+// gcm_main: one workgroup per task; each wave runs NS streams in lock-step.
+template <bool OPEN, int CRCMODE, int NS>
 __global__ __launch_bounds__(kThreads) void gcm_main_k(const Task *__restrict__ tasks,
                                                        const BlkDev *__restrict__ blks,
                                                        const GcmSched *__restrict__ sched,
@@ -111,9 +270,11 @@ __global__ __launch_bounds__(kThreads) void gcm_main_k(const Task *__restrict__ 
         const uint4 *ga = reinterpret_cast<const uint4 *>(tab.aes);
         uint4 *la = reinterpret_cast<uint4 *>(lds + kLdsAes);
         for (uint32_t i = tid; i < 4096; i += kThreads) la[i] = ga[i];
-        const uint4 *gc = reinterpret_cast<const uint4 *>(tab.crc);
-        uint4 *lc = reinterpret_cast<uint4 *>(lds + kLdsCrc);
-        for (uint32_t i = tid; i < 1280; i += kThreads) lc[i] = gc[i];
+        if (CRCMODE) {
+            const uint4 *gc = reinterpret_cast<const uint4 *>(tab.crc);
+            uint4 *lc = reinterpret_cast<uint4 *>(lds + kLdsCrc);
+            for (uint32_t i = tid; i < 1280; i += kThreads) lc[i] = gc[i];
+        }
         if (tid < 128)
             reinterpret_cast<uint4 *>(lds + kLdsBasis)[tid] = reinterpret_cast<const uint4 *>(sch->basis)[tid];
     }
@@ -122,7 +283,7 @@ __global__ __launch_bounds__(kThreads) void gcm_main_k(const Task *__restrict__ 
         uint4 *lg = reinterpret_cast<uint4 *>(lds + kLdsGh);
         const uint4 *lb = reinterpret_cast<const uint4 *>(lds + kLdsBasis);
         for (uint32_t e = tid; e < 4096; e += kThreads) {
-            uint32_t j = e >> 8, b = e & 255;
+            uint32_t b = e >> 4, j = e & 15;  // entry (b, j) at byte (b << 8) | (j << 4)
             uint4 z = make_uint4(0, 0, 0, 0);
 #pragma unroll
             for (int k = 0; k < 8; k++) {
@@ -142,117 +303,123 @@ __global__ __launch_bounds__(kThreads) void gcm_main_k(const Task *__restrict__ 
     uint32_t k1[4] = {sch->k1[0], sch->k1[1], sch->k1[2], sch->k1[3]};
 
     const uint32_t wave = tid >> 6, lane = tid & 63;
-    const uint32_t loff = (lane & 31) << 2;
+    const uint32_t loff = ((lane & 31) << 2) | 0x00010000u;  // AES replica offset | table base
+    const GhLane gl = gh_lane(lane);
+    const uint32_t xl = CRCMODE ? tab.crcx[lane] : 0u;
     const uint64_t c0 = task.c0, c1 = task.c1;
     const uint32_t nseg = (uint32_t)((c1 - c0 + kSeg - 1) / kSeg);
-    const uint32_t sa = wave * nseg / kWaves, sb = (wave + 1) * nseg / kWaves;
-    const uint64_t sub0 = c0 + (uint64_t)sa * kSeg;
-    const uint64_t sub1 = sb > sa ? (c0 + (uint64_t)sb * kSeg < c1 ? c0 + (uint64_t)sb * kSeg : c1) : sub0;
+    constexpr uint32_t V = kWaves * NS;  // virtual waves (streams) per task
+
+    Stream st[NS];
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        const uint32_t v = wave * NS + s;
+        const uint32_t sa = v * nseg / V, sb = (v + 1) * nseg / V;
+        st[s].sub0 = c0 + (uint64_t)sa * kSeg;
+        st[s].sub1 = sb > sa ? (c0 + (uint64_t)sb * kSeg < c1 ? c0 + (uint64_t)sb * kSeg : c1) : st[s].sub0;
+        st[s].acc[0] = st[s].acc[1] = st[s].acc[2] = st[s].acc[3] = 0;
+        st[s].jlast = 0;
+        st[s].has = false;
+        st[s].A = 0;
+        st[s].lend = 0;
+        st[s].seg0 = st[s].sub0;
+    }
+    // rows that are full for every non-empty stream: the fast path.  Empty
+    // streams (tasks with fewer segments than streams) alias stream 0's loads
+    // and skip every side effect (wave-uniform branch).
+    bool act[NS];
+    uint64_t rf = ~0ull, ld0[NS];
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        act[s] = st[s].sub1 > st[s].sub0;
+        ld0[s] = act[s] ? st[s].sub0 : st[0].sub0;
+        if (act[s]) {
+            const uint64_t fr = (st[s].sub1 - st[s].sub0) / 1024;
+            rf = fr < rf ? fr : rf;
+        }
+    }
+    if (rf == ~0ull) rf = 0;
     const uint8_t *src = blk.src;
     uint8_t *dst = blk.dst;
-    const uint32_t xl = CRCMODE ? tab.crcx[lane] : 0u;
+    const uint64_t lo = 16 * lane;
 
-    uint32_t acc[4] = {0, 0, 0, 0};
-    uint64_t jlast = 0;
-    bool has = false;
-    uint32_t A = 0, lend = 0;
-    uint64_t seg0 = sub0;
-
-    const uint64_t nrows = (sub1 - sub0 + 1023) / 1024;
-    uint4 nxt = make_uint4(0, 0, 0, 0);
-    if (nrows) nxt = load_piece(src, sub0 + 16 * lane, sub1);
-    for (uint64_t r = 0; r < nrows; r++) {
-        const uint64_t row = sub0 + 1024 * r;
-        const uint64_t o = row + 16 * lane;
-        uint4 d = nxt;
-        if (r + 1 < nrows) nxt = load_piece(src, o + 1024, sub1);
-        const bool valid = o < sub1;
-        const bool full = o + 16 <= sub1;
-        const uint64_t j = o >> 4;
-        uint32_t ks[4];
-        aes_ctr_block(lds, loff, rk, k1, (uint32_t)(j + 2), ks);
-        uint4 x = make_uint4(d.x ^ ks[0], d.y ^ ks[1], d.z ^ ks[2], d.w ^ ks[3]);
-        uint4 c = OPEN ? d : x;   // ciphertext
-        uint4 p = OPEN ? x : d;   // plaintext
-        if (!full) {
-            // zero the bytes past the end (GHASH pads C with zeros)
-            const int nv = valid ? (int)(sub1 - o) : 0;
-            uint32_t m[4];
-            for (int k = 0; k < 4; k++) {
-                int bytes = nv - 4 * k;
-                m[k] = bytes >= 4 ? 0xffffffffu : (bytes <= 0 ? 0u : ((1u << (8 * bytes)) - 1u));
-            }
-            c.x &= m[0]; c.y &= m[1]; c.z &= m[2]; c.w &= m[3];
-            p.x &= m[0]; p.y &= m[1]; p.z &= m[2]; p.w &= m[3];
+    uint4 nxt[NS];
+#pragma unroll
+    for (int s = 0; s < NS; s++)
+        nxt[s] = rf ? *reinterpret_cast<const uint4 *>(src + ld0[s] + lo) : make_uint4(0, 0, 0, 0);
+    for (uint64_t r = 0; r < rf; r++) {
+        uint4 d[NS];
+        uint32_t ctr[NS];
+#pragma unroll
+        for (int s = 0; s < NS; s++) {
+            d[s] = nxt[s];
+            const uint64_t o = ld0[s] + 1024 * r + lo;
+            if (r + 1 < rf) nxt[s] = *reinterpret_cast<const uint4 *>(src + o + 1024);
+            ctr[s] = (uint32_t)((o >> 4) + 2);
         }
-        if (valid) store_piece(dst, o, sub1, OPEN ? p : c);
-        // GHASH Horner step
-        {
-            uint32_t t[4] = {acc[0], acc[1], acc[2], acc[3]};
-            ghash_mul_tab(lds, t);
-            if (valid) {
-                acc[0] = t[0] ^ c.x; acc[1] = t[1] ^ c.y; acc[2] = t[2] ^ c.z; acc[3] = t[3] ^ c.w;
-                jlast = j;
-                has = true;
-            }
+        uint32_t ks[NS][4];
+        aes_ctr_blocks<NS>(lds, loff, rk, k1, ctr, ks);
+#pragma unroll
+        for (int s = 0; s < NS; s++) {
+            if (!act[s]) continue;
+            const uint64_t o = st[s].sub0 + 1024 * r + lo;
+            const uint4 x = make_uint4(d[s].x ^ ks[s][0], d[s].y ^ ks[s][1], d[s].z ^ ks[s][2], d[s].w ^ ks[s][3]);
+            const uint4 c = OPEN ? d[s] : x, p = OPEN ? x : d[s];
+            *reinterpret_cast<uint4 *>(dst + o) = OPEN ? p : c;
+            ghash_step(lds, st[s].acc, gl, c);
+            if (CRCMODE) st[s].A = crc_piece<kLdsCrc>(lds, st[s].A, p.x, p.y, p.z, p.w);
         }
-        if (CRCMODE) {
-            if (full) {
-                A = crc_piece<kLdsCrc>(lds, A, p.x, p.y, p.z, p.w);
-                lend = (uint32_t)(o + 16 - seg0);
-            } else if (valid) {
-                const uint32_t pw[4] = {p.x, p.y, p.z, p.w};
-                A = crc_partial<kLdsCrc>(lds, A, pw, (int)(sub1 - o));
-                lend = (uint32_t)(sub1 - seg0);
-            }
-            const uint64_t seg1 = seg0 + kSeg < sub1 ? seg0 + kSeg : sub1;
-            if (row + 1024 >= seg1) {  // segment end
-                const uint32_t Lseg = (uint32_t)(seg1 - seg0);
-                uint32_t v;
-                uint32_t K;
-                if (Lseg == (uint32_t)kSeg) {
-                    v = crc_mulmod(xl, A);
-                    K = tab.crcx[64 + 32];
-                } else {
-                    v = crc_mulmod(crc_xpow8(Lseg - lend, tab.crcx + 64), A);
-                    K = crc_mulmod(crc_xpow8(Lseg, tab.crcx + 64), 0xffffffffu);
-                }
-                const uint32_t raw = wave_xor(v);
-                if (lane == 0) {
-                    const uint32_t crc = ~(K ^ raw);
-                    const uint64_t si = seg0 / kSeg;
-                    if (CRCMODE == 1) {
-                        *reinterpret_cast<uint32_t *>(blk.crc + 4 * si) = __builtin_bswap32(crc);
-                    } else {
-                        blk.crc_calc[si] = crc;
-                    }
-                }
-                A = 0;
-                lend = 0;
-                seg0 = seg1;
+        if (CRCMODE && (r & 31) == 31) {
+#pragma unroll
+            for (int s = 0; s < NS; s++) {
+                if (!act[s]) continue;
+                crc_segment_end<CRCMODE>(blk, tab, lane, xl, st[s].seg0, st[s].seg0 + kSeg, st[s].A, 0);
+                st[s].A = 0;
+                st[s].seg0 += kSeg;
             }
         }
     }
-
-    // ---- wave epilogue: lift lane accumulators to the wave end, reduce ----
-    const uint64_t wend = (sub1 + 15) >> 4;  // blocks before the wave end
-    g128 z = {{0, 0, 0, 0}};
-    if (has) {
-        const uint32_t e = (uint32_t)(wend + 1 - jlast);  // in [2, 65]
-        g128 h = g_from_mem(sch->hpow[e]);
-        z = g_mul(g_from_mem(acc), h);
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        if (rf && act[s]) {
+            st[s].has = true;
+            st[s].jlast = (st[s].sub0 + 1024 * (rf - 1) + lo) >> 4;
+            st[s].lend = (uint32_t)(st[s].sub0 + 1024 * rf - st[s].seg0);  // only meaningful if mid-segment
+            if (st[s].lend) st[s].lend = st[s].lend - 1024 + (uint32_t)lo + 16;
+        }
+        // ragged remainder of this stream (block tail or unequal streams)
+        for (uint64_t row = st[s].sub0 + 1024 * rf; row < st[s].sub1; row += 1024)
+            st[s] = row_generic<OPEN, CRCMODE>(lds, loff, gl, sch, blk, tab, lane, xl, st[s], row);
+        // a stream that ended mid-segment on the fast path still owes that segment's CRC
+        if (CRCMODE && act[s] && st[s].seg0 < st[s].sub1) {
+            crc_segment_end<CRCMODE>(blk, tab, lane, xl, st[s].seg0, st[s].sub1, st[s].A, st[s].lend);
+            st[s].seg0 = st[s].sub1;
+        }
     }
-    uint32_t zm[4];
-    g_to_mem(z, zm);
-    for (int k = 0; k < 4; k++) zm[k] = wave_xor(zm[k]);
-    if (lane == 0) {
-        const uint32_t slot = task.slot0 + wave;
-        partial[4 * slot + 0] = zm[0];
-        partial[4 * slot + 1] = zm[1];
-        partial[4 * slot + 2] = zm[2];
-        partial[4 * slot + 3] = zm[3];
-        const uint64_t nblk = (blk.len + 15) >> 4;
-        pexp[slot] = (uint32_t)(nblk - wend);
+
+    // ---- stream epilogues: lift lane accumulators to the stream end, reduce ----
+    const uint64_t nblk = (blk.len + 15) >> 4;
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        const uint64_t wend = (st[s].sub1 + 15) >> 4;  // blocks before the stream end
+        g128 z = {{0, 0, 0, 0}};
+        if (st[s].has && st[s].sub1 > st[s].sub0) {
+            const uint32_t e = (uint32_t)(wend + 1 - st[s].jlast);  // in [2, 65]
+            uint32_t a[4];
+            gh_rho_inv(st[s].acc, gl, a);
+            z = g_mul(g_from_mem(a), g_from_mem(sch->hpow[e]));
+        }
+        uint32_t zm[4];
+        g_to_mem(z, zm);
+        for (int k = 0; k < 4; k++) zm[k] = wave_xor(zm[k]);
+        if (lane == 0) {
+            const uint32_t slot = task.slot0 + wave * NS + s;
+            partial[4 * slot + 0] = zm[0];
+            partial[4 * slot + 1] = zm[1];
+            partial[4 * slot + 2] = zm[2];
+            partial[4 * slot + 3] = zm[3];
+            pexp[slot] = (uint32_t)(nblk - wend);
+        }
     }
 }
 
@@ -421,7 +588,7 @@ void launch_gcm_main(hipStream_t s, int ntasks, bool open, int crc_mode, const T
                      const GcmSched *sched, uint32_t *partial, uint32_t *pexp, DevTables t) {
     if (ntasks <= 0) return;
     dim3 g(ntasks), bl(kThreads);
-#define L(O, C) hipLaunchKernelGGL((gcm_main_k<O, C>), g, bl, 0, s, tasks, blks, sched, partial, pexp, t)
+#define L(O, C) hipLaunchKernelGGL((gcm_main_k<O, C, kStreams>), g, bl, 0, s, tasks, blks, sched, partial, pexp, t)
     if (open) {
         if (crc_mode == 0) L(true, 0); else if (crc_mode == 1) L(true, 1); else L(true, 2);
     } else {

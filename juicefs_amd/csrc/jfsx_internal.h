@@ -17,8 +17,16 @@
 namespace jfsx {
 
 constexpr int kSeg = 32768;         // csBlock (disk_cache.go:1207)
-constexpr int kWaves = 16;          // waves per transform workgroup
+#ifndef JFSX_WAVES
+#define JFSX_WAVES 16
+#endif
+constexpr int kWaves = JFSX_WAVES;  // waves per transform workgroup
 constexpr int kThreads = kWaves * 64;
+#ifndef JFSX_STREAMS
+#define JFSX_STREAMS 1
+#endif
+constexpr int kStreams = JFSX_STREAMS;         // independent segment streams per wave (ILP)
+constexpr int kSlotsPerTask = kWaves * kStreams;  // GHASH/Poly partial slots per task
 constexpr int kMaxTaskBytes = 4 << 20;
 constexpr uint32_t kCrcPoly = 0x82F63B78u;  // reflected Castagnoli
 

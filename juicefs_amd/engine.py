@@ -11,7 +11,7 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libjfsx.so")
+LIB_PATH = os.environ.get("JFSX_LIB") or os.path.join(_HERE, "libjfsx.so")
 
 AES256GCM = 0
 CHACHA20P1305 = 1
