@@ -200,7 +200,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": None,
-                         "kernel": "gcm_main_k" if args.mode != "crc" else "crc_segments_k",
+                         "kernel": ("crc_segments_k" if args.mode == "crc" else
+                                    ("gcm_main_k" if args.algo == "aes256gcm" else "cp_main_k")),
                          "kernel_avg_ms": round(k_avg_ms, 3), "algorithmic_bytes_per_launch": algo_bytes},
             "cpu_baseline": cpu,
             "verified_blocks": verified,

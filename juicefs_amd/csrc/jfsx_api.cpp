@@ -90,18 +90,24 @@ void make_crc_tables(std::vector<uint32_t> &crc, std::vector<uint32_t> &crcx) {
             if (n & 1) r = crc_mulmod_h(x8[k], r);
         return r;
     };
-    crc.assign(20 * 256, 0);
+    crc.assign(24 * 256, 0);
     for (int j = 0; j < 16; j++) {
         const uint32_t xp = xpow8(15 - j);
         for (int b = 0; b < 256; b++) crc[j * 256 + b] = crc_mulmod_h(xp, T[b]);
     }
-    const uint32_t x1008 = xpow8(1008);
+    // S tables: shift a lane CRC across the gap to its next piece -- 1008 B for
+    // 16-B pieces at 1 KiB row stride (GCM), 4032 B for 64-B chunks at 4 KiB (ChaCha)
+    const uint32_t x1008 = xpow8(1008), x4032 = xpow8(4032);
     for (int k = 0; k < 4; k++)
-        for (uint32_t v = 0; v < 256; v++) crc[(16 + k) * 256 + v] = crc_mulmod_h(x1008, v << (8 * k));
-    crcx.assign(128, 0);
+        for (uint32_t v = 0; v < 256; v++) {
+            crc[(16 + k) * 256 + v] = crc_mulmod_h(x1008, v << (8 * k));
+            crc[(20 + k) * 256 + v] = crc_mulmod_h(x4032, v << (8 * k));
+        }
+    crcx.assign(192, 0);
     for (int l = 0; l < 64; l++) crcx[l] = xpow8(16 * (63 - l));
     for (int k = 0; k < 32; k++) crcx[64 + k] = x8[k];
     crcx[96] = crc_mulmod_h(xpow8(kSeg), 0xffffffffu);
+    for (int l = 0; l < 64; l++) crcx[128 + l] = xpow8(64 * (63 - l));
 }
 
 inline uint64_t nseg_of(uint64_t len) { return len ? (len + kSeg - 1) / kSeg : 1; }
@@ -165,16 +171,16 @@ int ensure_host(jfsx_ctx *c, size_t need) {
 
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// Split each block into <= CH-byte tasks (CH a multiple of 16 segments), one
-// workgroup each; 16 partial slots per task.
-Plan plan_tasks(const std::vector<uint64_t> &lens, uint64_t seg_per_task_max) {
+// Split each block into <= max_bytes tasks (a multiple of waves segments), one
+// workgroup each; `slots` partial slots per task.
+Plan plan_tasks(const std::vector<uint64_t> &lens, uint64_t max_bytes, uint32_t waves, uint32_t slots,
+                uint64_t want) {
     Plan p;
     uint64_t total = 0;
     for (uint64_t l : lens) total += l;
-    const uint64_t unit = (uint64_t)kWaves * kSeg;  // 512 KiB
-    uint64_t ch = seg_per_task_max * kSeg;
-    // enough workgroups to fill 256 CUs twice when the batch is small
-    const uint64_t want = 512;
+    const uint64_t unit = (uint64_t)waves * kSeg;
+    uint64_t ch = max_bytes;
+    // enough workgroups to fill the 256 CUs when the batch is small
     if (total / ch < want) {
         uint64_t c = (total / want + unit - 1) / unit * unit;
         ch = std::max(unit, std::min(ch, c));
@@ -187,7 +193,7 @@ Plan plan_tasks(const std::vector<uint64_t> &lens, uint64_t seg_per_task_max) {
             t.c0 = c0;
             t.c1 = std::min(c0 + ch, lens[b]);
             p.tasks.push_back(t);
-            p.nslots += kSlotsPerTask;
+            p.nslots += slots;
         }
     }
     return p;
@@ -200,7 +206,7 @@ int run_aead(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mo
     if (algo != JFSX_AES256GCM && algo != JFSX_CHACHA20P1305) return JFSX_EINVAL;
     if (crc_mode < 0 || crc_mode > 2 || n < 0) return JFSX_EINVAL;
     if (n == 0) return 0;
-    if (algo == JFSX_CHACHA20P1305) return JFSX_EINVAL;  // TODO(round 1): ChaCha20-Poly1305 kernels
+    const bool gcm = algo == JFSX_AES256GCM;
     std::vector<uint64_t> lens(n);
     uint64_t crc_calc_words = 0;
     for (int i = 0; i < n; i++) {
@@ -211,7 +217,9 @@ int run_aead(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mo
         lens[i] = b.len;
         if (crc_mode == JFSX_CRC_VERIFY) crc_calc_words += nseg_of(b.len);
     }
-    Plan plan = plan_tasks(lens, kMaxTaskBytes / kSeg);
+    const uint32_t slots = gcm ? kSlotsPerTask : kCpWaves;
+    Plan plan = gcm ? plan_tasks(lens, kMaxTaskBytes, kWaves, slots, 512)
+                    : plan_tasks(lens, kCpTaskBytes, kCpWaves, slots, 2048);
     const size_t nt = plan.tasks.size();
     // device workspace layout
     size_t off = 0;
@@ -221,7 +229,7 @@ int run_aead(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mo
     const size_t o_tagin = off; off = align256(off + 16 * (size_t)n);
     const size_t h_bytes = off;  // everything above is uploaded from the pinned mirror
     const size_t o_out = off; off = align256(off + sizeof(BlkOut) * n);
-    const size_t o_sched = off; off = align256(off + sizeof(GcmSched) * n);
+    const size_t o_sched = off; off = align256(off + (gcm ? sizeof(GcmSched) : sizeof(CpSched)) * n);
     const size_t o_part = off; off = align256(off + 32 * std::max<uint64_t>(plan.nslots, 1));
     const size_t o_pexp = off; off = align256(off + 4 * std::max<uint64_t>(plan.nslots, 1));
     const size_t o_calc = off; off = align256(off + 4 * std::max<uint64_t>(crc_calc_words, 1));
@@ -254,7 +262,7 @@ int run_aead(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mo
     for (size_t t = 0; t < nt; t++) {
         BlkDev &bd = hb[plan.tasks[t].blk];
         if (bd.nslots == 0) bd.slot0 = plan.tasks[t].slot0;
-        bd.nslots += kSlotsPerTask;
+        bd.nslots += slots;
     }
     if (nt) memcpy(h + o_task, plan.tasks.data(), sizeof(Task) * nt);
     hipStream_t s = c->stream;
@@ -265,15 +273,24 @@ int run_aead(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mo
     const KeyIn *dk = (const KeyIn *)(d + o_keys);
     const BlkDev *db = (const BlkDev *)(d + o_blk);
     const Task *dt = (const Task *)(d + o_task);
-    GcmSched *dsch = (GcmSched *)(d + o_sched);
     uint32_t *dpart = (uint32_t *)(d + o_part);
     uint32_t *dpexp = (uint32_t *)(d + o_pexp);
     BlkOut *dout = (BlkOut *)(d + o_out);
-    launch_gcm_keysetup(s, n, dk, db, dsch, c->tabs);
-    if (c->timing) HIP_OK(hipEventRecord(c->ev0, s));
-    launch_gcm_main(s, (int)nt, open, crc_mode, dt, db, dsch, dpart, dpexp, c->tabs);
-    if (c->timing) HIP_OK(hipEventRecord(c->ev1, s));
-    launch_gcm_finalize(s, n, open, crc_mode, db, dsch, dpart, dpexp, dout);
+    if (gcm) {
+        GcmSched *dsch = (GcmSched *)(d + o_sched);
+        launch_gcm_keysetup(s, n, dk, db, dsch, c->tabs);
+        if (c->timing) HIP_OK(hipEventRecord(c->ev0, s));
+        launch_gcm_main(s, (int)nt, open, crc_mode, dt, db, dsch, dpart, dpexp, c->tabs);
+        if (c->timing) HIP_OK(hipEventRecord(c->ev1, s));
+        launch_gcm_finalize(s, n, open, crc_mode, db, dsch, dpart, dpexp, dout);
+    } else {
+        CpSched *dsch = (CpSched *)(d + o_sched);
+        launch_cp_keysetup(s, n, dk, db, dsch);
+        if (c->timing) HIP_OK(hipEventRecord(c->ev0, s));
+        launch_cp_main(s, (int)nt, open, crc_mode, dt, db, dsch, dpart, dpexp, c->tabs);
+        if (c->timing) HIP_OK(hipEventRecord(c->ev1, s));
+        launch_cp_finalize(s, n, open, crc_mode, db, dsch, dpart, dpexp, dout);
+    }
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(h, dout, sizeof(BlkOut) * n, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
@@ -802,7 +819,7 @@ void jfsx_gen_key(uint64_t seed, uint64_t b, uint8_t key[32], uint8_t nonce[12])
 
 int jfsx_debug_tables(uint32_t *aes, uint32_t *crc, uint32_t *crcx) {
     std::vector<uint32_t> a, c, x;
-    make_aes_table(a);
+    make_aes_table(a);  // 16384 / 6144 / 192 dwords
     make_crc_tables(c, x);
     if (aes) memcpy(aes, a.data(), 4 * a.size());
     if (crc) memcpy(crc, c.data(), 4 * c.size());

@@ -14,11 +14,12 @@ __device__ __forceinline__ uint4 lds_u4(const char *lds, uint32_t byteaddr) {
 #define CRC_T(t, x, k) lds_u32(lds, ((((x) >> (8 * (k))) & 0xffu) << 2) + CB + 1024u * (t))
 
 // crc_raw(A, 16-byte piece) = crc_raw(0, piece ^ shift(A, 1008 B) in the first word)
-template <uint32_t CB>
+// S = 16: shift by 1008 B first; S = 20: shift by 4032 B; S < 0: no shift
+template <uint32_t CB, int S = 16>
 __device__ __forceinline__ uint32_t crc_piece(const char *lds, uint32_t A, uint32_t p0, uint32_t p1, uint32_t p2,
                                               uint32_t p3) {
 #define X3(a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), 0x96)
-    uint32_t s = X3(CRC_T(16, A, 0), CRC_T(17, A, 1), CRC_T(18, A, 2)) ^ CRC_T(19, A, 3);
+    uint32_t s = S < 0 ? A : X3(CRC_T(S, A, 0), CRC_T(S + 1, A, 1), CRC_T(S + 2, A, 2)) ^ CRC_T(S + 3, A, 3);
     uint32_t q = p0 ^ s;
     return X3(X3(X3(CRC_T(0, q, 0), CRC_T(1, q, 1), CRC_T(2, q, 2)), X3(CRC_T(3, q, 3), CRC_T(4, p1, 0), CRC_T(5, p1, 1)),
                  X3(CRC_T(6, p1, 2), CRC_T(7, p1, 3), CRC_T(8, p2, 0))),
@@ -28,9 +29,9 @@ __device__ __forceinline__ uint32_t crc_piece(const char *lds, uint32_t A, uint3
 }
 
 // byte-serial tail: crc_raw(shift(A,1008), first n bytes of the piece)
-template <uint32_t CB>
+template <uint32_t CB, int S = 16>
 __device__ __noinline__ uint32_t crc_partial(const char *lds, uint32_t A, const uint32_t p[4], int n) {
-    uint32_t c = CRC_T(16, A, 0) ^ CRC_T(17, A, 1) ^ CRC_T(18, A, 2) ^ CRC_T(19, A, 3);
+    uint32_t c = S < 0 ? A : CRC_T(S, A, 0) ^ CRC_T(S + 1, A, 1) ^ CRC_T(S + 2, A, 2) ^ CRC_T(S + 3, A, 3);
     for (int i = 0; i < n; i++) {
         uint32_t byte = (p[i >> 2] >> (8 * (i & 3))) & 0xffu;
         c = lds_u32(lds, (((c ^ byte) & 0xffu) << 2) + CB + 1024u * 15) ^ (c >> 8);

@@ -72,19 +72,21 @@ struct GcmSched {
     uint32_t h2k[32][4];     // H^(2^k), memory order
 };
 
-// per-key ChaCha20-Poly1305 schedule
+// per-key ChaCha20-Poly1305 schedule (Poly1305 values in 26-bit limbs)
 struct CpSched {
     uint32_t key[8];
     uint32_t nonce[3];
     uint32_t pad0;
-    uint32_t s[4];           // Poly1305 s (key bytes 16..31 of keystream block 0)
-    uint32_t r256[5];        // r^256 (26-bit limbs) -- lane stride multiplier
-    uint32_t pad1[3];
-    uint32_t rpow[260][5];   // r^k (26-bit limbs), k = 0..259
-    uint32_t r2k[32][5];     // r^(2^k)
-    uint32_t init[5];        // r^1 * (length block) contribution, 26-bit limbs
-    uint32_t pad2[3];
+    uint32_t s[4];          // Poly1305 s (keystream block 0, bytes 16..31)
+    uint32_t r[5];          // clamped r
+    uint32_t r253[5];       // r^253: gap between a lane's row chunks (4 KiB rows)
+    uint32_t init[5];       // (length block) * r
+    uint32_t pad1;
+    uint32_t r2k[32][5];    // r^(2^k)
 };
+
+constexpr int kCpWaves = 4;                 // waves per ChaCha20-Poly1305 workgroup
+constexpr int kCpTaskBytes = 1 << 20;       // bytes per ChaCha task (<= kCpWaves * segments)
 
 // ---------------------------------------------------------------------------
 // GF(2^128) in GCM convention.  "BE words": w[0] holds bytes 0..3 big-endian;

@@ -50,7 +50,7 @@ def _seal_device(eng, algo, items, crc_mode=E.CRC_GEN):
     return outs
 
 
-@pytest.mark.parametrize("v", [v for v in _gold() if v["algo"] == "aes256gcm"], ids=lambda v: str(v["len"]))
+@pytest.mark.parametrize("v", _gold(), ids=lambda v: "%s-%d" % (v["algo"], v["len"]))
 def test_seal_golden_device(eng, v):
     algo = ALGOS[v["algo"]]
     p = orc.gen_block(v["seed"], v["block"], v["len"])
@@ -62,24 +62,26 @@ def test_seal_golden_device(eng, v):
     assert crc.hex() == v["crc"]
 
 
-def test_seal_ragged_batch_vs_oracle(eng):
-    rng = np.random.default_rng(1)
+@pytest.mark.parametrize("algo", [E.AES256GCM, E.CHACHA20P1305])
+def test_seal_ragged_batch_vs_oracle(eng, algo):
+    rng = np.random.default_rng(1 + algo)
     lens = [0, 1, 15, 16, 17, 1023, 1024, 1025, 32767, 32768, 32769, 65536 + 7, 524288, 524288 + 16,
             (1 << 20) + 3] + [int(x) for x in rng.integers(1, 3 << 20, 17)]
     items = []
     for i, n in enumerate(lens):
         key, nonce = orc.gen_key(11, i)
         items.append((key, nonce, orc.gen_block(11, i, n)))
-    outs = _seal_device(eng, E.AES256GCM, items)
+    outs = _seal_device(eng, algo, items)
     for (key, nonce, p), (c, tag, crc, st) in zip(items, outs):
-        c2, t2 = orc.seal(orc.AES256GCM, key, nonce, p, fast=True)
+        c2, t2 = orc.seal(ORC[algo], key, nonce, p, fast=True)
         assert st == E.OK
         assert tag == t2, "len %d" % p.size
         assert c == c2, "len %d" % p.size
         assert crc == orc.checksum(p, hw=True), "len %d" % p.size
 
 
-def test_open_verify_roundtrip_and_failures(eng):
+@pytest.mark.parametrize("algo", [E.AES256GCM, E.CHACHA20P1305])
+def test_open_verify_roundtrip_and_failures(eng, algo):
     lens = [0, 5, 4096, 100000, 1 << 20, (4 << 20) - 5]
     bufs = []
     specs = []
@@ -87,7 +89,7 @@ def test_open_verify_roundtrip_and_failures(eng):
     for i, n in enumerate(lens):
         key, nonce = orc.gen_key(21, i)
         p = orc.gen_block(21, i, n)
-        c, tag = orc.seal(orc.AES256GCM, key, nonce, p, fast=True)
+        c, tag = orc.seal(ORC[algo], key, nonce, p, fast=True)
         crc = bytearray(orc.checksum(p, hw=True))
         if i == 3:
             tag = bytes([tag[0] ^ 1]) + tag[1:]            # tag corruption -> ETAG
@@ -103,7 +105,7 @@ def test_open_verify_roundtrip_and_failures(eng):
                       "crc": cb.ptr})
         exp.append((p, bytes(crc)))
     arr, nb = eng.make_blocks(specs)
-    eng.open_batch(E.AES256GCM, arr, nb, E.CRC_VERIFY, E.MEM_DEVICE)
+    eng.open_batch(algo, arr, nb, E.CRC_VERIFY, E.MEM_DEVICE)
     for i, (p, crc) in enumerate(exp):
         b = arr[i]
         if i == 3:
@@ -119,17 +121,18 @@ def test_open_verify_roundtrip_and_failures(eng):
         assert bufs[3 * i + 1].download(p.size).tobytes() == p.tobytes()
 
 
-def test_host_mode_seal_open(eng):
+@pytest.mark.parametrize("algo", [E.AES256GCM, E.CHACHA20P1305])
+def test_host_mode_seal_open(eng, algo):
     key, nonce = orc.gen_key(3, 3)
     for n in (0, 1, 77, 32768 * 3 + 11, 1 << 20):
         p = orc.gen_block(3, n, n)
-        c, tag, crc = eng.seal(E.AES256GCM, key, nonce, p, crc=True)
-        c2, t2 = orc.seal(orc.AES256GCM, key, nonce, p, fast=True)
+        c, tag, crc = eng.seal(algo, key, nonce, p, crc=True)
+        c2, t2 = orc.seal(ORC[algo], key, nonce, p, fast=True)
         assert (c, tag) == (c2, t2)
         assert crc == orc.checksum(p)
-        assert eng.open(E.AES256GCM, key, nonce, c, tag, crc=crc) == p.tobytes()
+        assert eng.open(algo, key, nonce, c, tag, crc=crc) == p.tobytes()
         bad = bytes([tag[0] ^ 0x80]) + tag[1:]
-        assert eng.open(E.AES256GCM, key, nonce, c, bad) is None
+        assert eng.open(algo, key, nonce, c, bad) is None
 
 
 @pytest.mark.parametrize("n", [0, 1, 16, 1000, 32767, 32768, 32769, 98309, 102400, 1 << 20, (4 << 20) - 1])
@@ -167,24 +170,26 @@ def test_crc_segments_device_gen_verify(eng):
             assert arr[i].status == E.OK
 
 
-def test_object_format_vs_oracle(eng):
+@pytest.mark.parametrize("algo", [E.AES256GCM, E.CHACHA20P1305])
+def test_object_format_vs_oracle(eng, algo):
     wrapped = bytes(range(256))
     for n in (0, 5, 4096 + 3):
         key, nonce = orc.gen_key(4, n)
         p = orc.gen_block(4, n, n)
-        obj = eng.data_encrypt(E.AES256GCM, key, nonce, wrapped, p)
-        assert obj == orc.data_encrypt(orc.AES256GCM, key, nonce, wrapped, p)
-        rc, back = eng.data_decrypt(E.AES256GCM, key, obj)
+        obj = eng.data_encrypt(algo, key, nonce, wrapped, p)
+        assert obj == orc.data_encrypt(ORC[algo], key, nonce, wrapped, p)
+        rc, back = eng.data_decrypt(algo, key, obj)
         assert rc == 0 and back == p.tobytes()
-        assert eng.data_decrypt(E.AES256GCM, key, obj[:271])[0] == E.EMISFORMED
+        assert eng.data_decrypt(algo, key, obj[:271])[0] == E.EMISFORMED
         bad = bytearray(obj)
         bad[-3] ^= 4
-        assert eng.data_decrypt(E.AES256GCM, key, bytes(bad))[0] == E.ETAG
+        assert eng.data_decrypt(algo, key, bytes(bad))[0] == E.ETAG
 
 
-def test_large_batch_sample_vs_oracle(eng):
-    """64 x 4 MiB device batch; every block checked against the AES-NI oracle."""
-    nb, L = 64, 4 << 20
+@pytest.mark.parametrize("algo", [E.AES256GCM, E.CHACHA20P1305])
+def test_large_batch_sample_vs_oracle(eng, algo):
+    """64 (GCM) / 16 (ChaCha) x 4 MiB device batch, every block checked against the oracle."""
+    nb, L = (64 if algo == E.AES256GCM else 16), 4 << 20
     src = eng.alloc(nb * L)
     dst = eng.alloc(nb * L)
     crc = eng.alloc(nb * 512)
@@ -196,12 +201,12 @@ def test_large_batch_sample_vs_oracle(eng):
                       "crc": crc.ptr + 512 * b})
     eng.sync()
     arr, n = eng.make_blocks(specs)
-    eng.seal_batch(E.AES256GCM, arr, n, E.CRC_GEN, E.MEM_DEVICE)
+    eng.seal_batch(algo, arr, n, E.CRC_GEN, E.MEM_DEVICE)
     cs = crc.download()
     for b in range(nb):
         p = orc.gen_block(0x4A465321, b, L)
         key, nonce = orc.gen_key(0x4A465321, b)
-        c, tag = orc.seal(orc.AES256GCM, key, nonce, p, fast=True)
+        c, tag = orc.seal(ORC[algo], key, nonce, p, fast=True)
         assert bytes(arr[b].tag) == tag, b
         assert dst.download(L, offset=b * L).tobytes() == c, b
         assert cs[512 * b:512 * (b + 1)].tobytes() == orc.checksum(p, hw=True), b
