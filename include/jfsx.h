@@ -117,6 +117,10 @@ void *jfsx_ctx_stream(jfsx_ctx *ctx);
  * every batch on the context's stream; query returns the summed milliseconds
  * and the number of launches since the last reset */
 int jfsx_ctx_set_timing(jfsx_ctx *ctx, int enable);
+/* host-ingest pipeline slot size (default 256 MiB): JFSX_MEM_HOST batches are
+ * streamed through 3 device staging slots of this size, H2D | transform | D2H
+ * overlapped on three streams */
+int jfsx_ctx_set_slot_bytes(jfsx_ctx *ctx, uint64_t bytes);
 int jfsx_ctx_kernel_time(jfsx_ctx *ctx, double *ms_total, uint64_t *launches, int reset);
 
 /* memory helpers (engine-owned pinned staging, device buffers) */

@@ -117,22 +117,35 @@ struct Plan {
     uint64_t nslots = 0;
 };
 
+// Device + pinned-host scratch for one in-flight batch.
+struct Workspace {
+    char *d = nullptr;  // descriptors, schedules, partials, results (device)
+    size_t dcap = 0;
+    char *h = nullptr;  // pinned mirror: descriptors up, results down
+    size_t hcap = 0;
+    char *stage = nullptr;  // host-ingest staging for block data (device)
+    size_t scap = 0;
+    int n = 0;              // blocks of the batch in flight
+    uint64_t nt = 0;        // tasks of the batch in flight
+};
+
+constexpr int kRing = 3;  // host-ingest pipeline depth (H2D | transform | D2H)
+
 }  // namespace
 
 struct jfsx_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;  // transform stream
+    hipStream_t s_in = nullptr;    // host-ingest H2D
+    hipStream_t s_out = nullptr;   // host-ingest D2H
     std::mutex mu;
     uint32_t *d_tab = nullptr;  // aes | crc | crcx
     DevTables tabs{};
-    char *d_ws = nullptr;
-    size_t ws_cap = 0;
-    char *h_ws = nullptr;  // pinned
-    size_t hws_cap = 0;
-    char *d_stage = nullptr;
-    size_t stage_cap = 0;
+    Workspace ws[kRing];
+    hipEvent_t ev_in[kRing] = {}, ev_comp[kRing] = {}, ev_out[kRing] = {};
+    hipEvent_t ev_k0[kRing] = {}, ev_k1[kRing] = {};  // main-kernel timing per slot
+    size_t slot_bytes = (size_t)256 << 20;
     bool timing = false;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double ms_total = 0;
     uint64_t launches = 0;
 };
@@ -142,7 +155,7 @@ namespace {
 int ensure_dev(jfsx_ctx *c, char **buf, size_t *cap, size_t need) {
     if (need <= *cap) return 0;
     if (*buf) {
-        HIP_OK(hipStreamSynchronize(c->stream));
+        HIP_OK(hipDeviceSynchronize());
         HIP_OK(hipFree(*buf));
         *buf = nullptr;
         *cap = 0;
@@ -154,18 +167,18 @@ int ensure_dev(jfsx_ctx *c, char **buf, size_t *cap, size_t need) {
     return 0;
 }
 
-int ensure_host(jfsx_ctx *c, size_t need) {
-    if (need <= c->hws_cap) return 0;
-    if (c->h_ws) {
-        HIP_OK(hipStreamSynchronize(c->stream));
-        HIP_OK(hipHostFree(c->h_ws));
-        c->h_ws = nullptr;
-        c->hws_cap = 0;
+int ensure_host(char **buf, size_t *cap, size_t need) {
+    if (need <= *cap) return 0;
+    if (*buf) {
+        HIP_OK(hipDeviceSynchronize());
+        HIP_OK(hipHostFree(*buf));
+        *buf = nullptr;
+        *cap = 0;
     }
     size_t n = std::max(need, (size_t)1 << 20);
     n = (n + 0xFFFFF) & ~(size_t)0xFFFFF;
-    if (hipHostMalloc((void **)&c->h_ws, n, hipHostMallocDefault) != hipSuccess) return JFSX_ENOMEM;
-    c->hws_cap = n;
+    if (hipHostMalloc((void **)buf, n, hipHostMallocDefault) != hipSuccess) return JFSX_ENOMEM;
+    *cap = n;
     return 0;
 }
 
@@ -201,21 +214,31 @@ Plan plan_tasks(const std::vector<uint64_t> &lens, uint64_t max_bytes, uint32_t 
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
 
-// Core of seal/open for device-resident buffers.
-int run_aead(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mode) {
+int check_aead_args(int algo, int n, const jfsx_blk *blks, int crc_mode, bool device) {
     if (algo != JFSX_AES256GCM && algo != JFSX_CHACHA20P1305) return JFSX_EINVAL;
     if (crc_mode < 0 || crc_mode > 2 || n < 0) return JFSX_EINVAL;
-    if (n == 0) return 0;
+    for (int i = 0; i < n; i++) {
+        const jfsx_blk &b = blks[i];
+        if (b.len && (!b.src || !b.dst)) return JFSX_EINVAL;
+        if (device && b.len && (!aligned16(b.src) || !aligned16(b.dst))) return JFSX_EINVAL;
+        if (b.len >= ((uint64_t)1 << 32) * 16) return JFSX_EINVAL;  // GCM 32-bit block counter
+        if (algo == JFSX_CHACHA20P1305 && b.len > ((uint64_t)1 << 32) * 64 - 64) return JFSX_EINVAL;
+        if (crc_mode && !b.crc) return JFSX_EINVAL;
+    }
+    return 0;
+}
+
+// Enqueue keysetup -> transform -> finalize -> result copy for n device-resident
+// blocks on stream s, using workspace w.  Results land in w.h (BlkOut[n]) once
+// the stream reaches that point; finish_aead() copies them into blks.
+int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, int k, int algo, bool open, int n, const jfsx_blk *blks,
+                 int crc_mode) {
     const bool gcm = algo == JFSX_AES256GCM;
     std::vector<uint64_t> lens(n);
     uint64_t crc_calc_words = 0;
     for (int i = 0; i < n; i++) {
-        const jfsx_blk &b = blks[i];
-        if (b.len && (!b.src || !b.dst || !aligned16(b.src) || !aligned16(b.dst))) return JFSX_EINVAL;
-        if (b.len >= ((uint64_t)1 << 32) * 16) return JFSX_EINVAL;
-        if (crc_mode && !b.crc) return JFSX_EINVAL;
-        lens[i] = b.len;
-        if (crc_mode == JFSX_CRC_VERIFY) crc_calc_words += nseg_of(b.len);
+        lens[i] = blks[i].len;
+        if (crc_mode == JFSX_CRC_VERIFY) crc_calc_words += nseg_of(blks[i].len);
     }
     const uint32_t slots = gcm ? kSlotsPerTask : kCpWaves;
     Plan plan = gcm ? plan_tasks(lens, kMaxTaskBytes, kWaves, slots, 512)
@@ -234,9 +257,9 @@ int run_aead(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mo
     const size_t o_pexp = off; off = align256(off + 4 * std::max<uint64_t>(plan.nslots, 1));
     const size_t o_calc = off; off = align256(off + 4 * std::max<uint64_t>(crc_calc_words, 1));
     int rc;
-    if ((rc = ensure_dev(c, &c->d_ws, &c->ws_cap, off))) return rc;
-    if ((rc = ensure_host(c, std::max(h_bytes, sizeof(BlkOut) * n)))) return rc;
-    char *h = c->h_ws, *d = c->d_ws;
+    if ((rc = ensure_dev(c, &w.d, &w.dcap, off))) return rc;
+    if ((rc = ensure_host(&w.h, &w.hcap, std::max(h_bytes, sizeof(BlkOut) * n)))) return rc;
+    char *h = w.h, *d = w.d;
     KeyIn *hk = (KeyIn *)(h + o_keys);
     BlkDev *hb = (BlkDev *)(h + o_blk);
     uint64_t calc = 0;
@@ -265,7 +288,6 @@ int run_aead(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mo
         bd.nslots += slots;
     }
     if (nt) memcpy(h + o_task, plan.tasks.data(), sizeof(Task) * nt);
-    hipStream_t s = c->stream;
     HIP_OK(hipMemcpyAsync(d, h, h_bytes, hipMemcpyHostToDevice, s));
     if (crc_mode == JFSX_CRC_GEN)
         for (int i = 0; i < n; i++)
@@ -279,29 +301,35 @@ int run_aead(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mo
     if (gcm) {
         GcmSched *dsch = (GcmSched *)(d + o_sched);
         launch_gcm_keysetup(s, n, dk, db, dsch, c->tabs);
-        if (c->timing) HIP_OK(hipEventRecord(c->ev0, s));
+        if (c->timing) HIP_OK(hipEventRecord(c->ev_k0[k], s));
         launch_gcm_main(s, (int)nt, open, crc_mode, dt, db, dsch, dpart, dpexp, c->tabs);
-        if (c->timing) HIP_OK(hipEventRecord(c->ev1, s));
+        if (c->timing) HIP_OK(hipEventRecord(c->ev_k1[k], s));
         launch_gcm_finalize(s, n, open, crc_mode, db, dsch, dpart, dpexp, dout);
     } else {
         CpSched *dsch = (CpSched *)(d + o_sched);
         launch_cp_keysetup(s, n, dk, db, dsch);
-        if (c->timing) HIP_OK(hipEventRecord(c->ev0, s));
+        if (c->timing) HIP_OK(hipEventRecord(c->ev_k0[k], s));
         launch_cp_main(s, (int)nt, open, crc_mode, dt, db, dsch, dpart, dpexp, c->tabs);
-        if (c->timing) HIP_OK(hipEventRecord(c->ev1, s));
+        if (c->timing) HIP_OK(hipEventRecord(c->ev_k1[k], s));
         launch_cp_finalize(s, n, open, crc_mode, db, dsch, dpart, dpexp, dout);
     }
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(h, dout, sizeof(BlkOut) * n, hipMemcpyDeviceToHost, s));
-    HIP_OK(hipStreamSynchronize(s));
-    if (c->timing && nt) {
+    w.n = n;
+    w.nt = nt;
+    return 0;
+}
+
+// After the batch's stream work completed: per-block results into blks.
+int finish_aead(jfsx_ctx *c, Workspace &w, int k, bool open, jfsx_blk *blks) {
+    if (c->timing && w.nt) {
         float ms = 0;
-        HIP_OK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        HIP_OK(hipEventElapsedTime(&ms, c->ev_k0[k], c->ev_k1[k]));
         c->ms_total += ms;
         c->launches += 1;
     }
-    const BlkOut *ho = (const BlkOut *)h;
-    for (int i = 0; i < n; i++) {
+    const BlkOut *ho = (const BlkOut *)w.h;
+    for (int i = 0; i < w.n; i++) {
         jfsx_blk &b = blks[i];
         if (!open) memcpy(b.tag, ho[i].tag, 16);
         b.status = ho[i].status;
@@ -309,49 +337,146 @@ int run_aead(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mo
         b.crc_got = ho[i].got;
         b.crc_expect = ho[i].expect;
     }
+    w.n = 0;
+    w.nt = 0;
     return 0;
 }
 
-// Host-memory batches: stage through device buffers (synchronous).
+// Device-resident batch: one enqueue, one sync.
+int run_aead(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mode) {
+    int rc = check_aead_args(algo, n, blks, crc_mode, true);
+    if (rc || n == 0) return rc;
+    if ((rc = enqueue_aead(c, c->ws[0], c->stream, 0, algo, open, n, blks, crc_mode))) return rc;
+    HIP_OK(hipStreamSynchronize(c->stream));
+    return finish_aead(c, c->ws[0], 0, open, blks);
+}
+
+// Host-memory batch (host ingest): blocks are grouped into slots of up to
+// slot_bytes and streamed through a ring of kRing device staging buffers:
+// H2D on s_in, transform on stream, D2H on s_out, chained by events, so the
+// copies of one slot overlap the transform of the next.  Open releases no
+// plaintext of a block whose tag failed: its destination is wiped before the
+// call returns.
 int run_aead_host(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mode) {
-    size_t need = 0;
-    for (int i = 0; i < n; i++) {
-        need += align256(blks[i].len) * 1;
-        if (crc_mode) need += align256(4 * nseg_of(blks[i].len));
-    }
-    int rc;
-    if ((rc = ensure_dev(c, &c->d_stage, &c->stage_cap, std::max<size_t>(need, 256)))) return rc;
-    std::vector<jfsx_blk> dv(blks, blks + n);
-    size_t off = 0;
-    hipStream_t s = c->stream;
-    for (int i = 0; i < n; i++) {
-        char *buf = c->d_stage + off;
-        off += align256(blks[i].len);
-        if (blks[i].len) HIP_OK(hipMemcpyAsync(buf, blks[i].src, blks[i].len, hipMemcpyHostToDevice, s));
-        dv[i].src = buf;
-        dv[i].dst = buf;
-        if (crc_mode) {
-            char *cb = c->d_stage + off;
-            off += align256(4 * nseg_of(blks[i].len));
-            if (crc_mode == JFSX_CRC_VERIFY)
-                HIP_OK(hipMemcpyAsync(cb, blks[i].crc, 4 * nseg_of(blks[i].len), hipMemcpyHostToDevice, s));
-            dv[i].crc = (uint8_t *)cb;
+    int rc = check_aead_args(algo, n, blks, crc_mode, false);
+    if (rc || n == 0) return rc;
+    // group blocks into slots
+    std::vector<std::pair<int, int>> groups;  // [b0, b1)
+    {
+        int b0 = 0;
+        size_t acc = 0;
+        for (int i = 0; i < n; i++) {
+            const size_t need = align256(blks[i].len) + (crc_mode ? align256(4 * nseg_of(blks[i].len)) : 0);
+            if (i > b0 && acc + need > c->slot_bytes) {
+                groups.push_back({b0, i});
+                b0 = i;
+                acc = 0;
+            }
+            acc += need;
         }
+        groups.push_back({b0, n});
     }
-    if ((rc = run_aead(c, algo, open, n, dv.data(), crc_mode))) return rc;
+    std::vector<jfsx_blk> dv(blks, blks + n);
+    int busy[kRing] = {-1, -1, -1};  // group in flight per slot
+    auto drain = [&](int k) -> int {
+        if (busy[k] < 0) return 0;
+        HIP_OK(hipEventSynchronize(c->ev_out[k]));
+        const int g = busy[k];
+        int r = finish_aead(c, c->ws[k], k, open, dv.data() + groups[g].first);
+        busy[k] = -1;
+        return r;
+    };
+    for (size_t g = 0; g < groups.size(); g++) {
+        const int k = (int)(g % kRing);
+        if ((rc = drain(k))) return rc;
+        Workspace &w = c->ws[k];
+        const int b0 = groups[g].first, b1 = groups[g].second;
+        size_t need = 0;
+        for (int i = b0; i < b1; i++)
+            need += align256(blks[i].len) + (crc_mode ? align256(4 * nseg_of(blks[i].len)) : 0);
+        if ((rc = ensure_dev(c, &w.stage, &w.scap, std::max<size_t>(need, 256)))) return rc;
+        size_t off = 0;
+        // data copies are coalesced over runs of blocks adjacent both in the
+        // caller's memory and in the staging slot (one DMA per run)
+        const char *run_h = nullptr;
+        char *run_d = nullptr;
+        size_t run_n = 0;
+        auto flush_in = [&]() -> int {
+            if (run_n) HIP_OK(hipMemcpyAsync(run_d, run_h, run_n, hipMemcpyHostToDevice, c->s_in));
+            run_n = 0;
+            return 0;
+        };
+        for (int i = b0; i < b1; i++) {
+            char *buf = w.stage + off;
+            off += align256(blks[i].len);
+            if (blks[i].len) {
+                const char *hs = (const char *)blks[i].src;
+                if (!(run_n && run_h + run_n == hs && run_d + run_n == buf) && (rc = flush_in())) return rc;
+                if (!run_n) {
+                    run_h = hs;
+                    run_d = buf;
+                }
+                run_n += blks[i].len;
+                if (align256(blks[i].len) != blks[i].len && (rc = flush_in())) return rc;
+            }
+            dv[i].src = buf;
+            dv[i].dst = buf;
+            if (crc_mode) {
+                char *cb = w.stage + off;
+                off += align256(4 * nseg_of(blks[i].len));
+                if ((rc = flush_in())) return rc;
+                if (crc_mode == JFSX_CRC_VERIFY)
+                    HIP_OK(hipMemcpyAsync(cb, blks[i].crc, 4 * nseg_of(blks[i].len), hipMemcpyHostToDevice, c->s_in));
+                dv[i].crc = (uint8_t *)cb;
+            }
+        }
+        if ((rc = flush_in())) return rc;
+        HIP_OK(hipEventRecord(c->ev_in[k], c->s_in));
+        HIP_OK(hipStreamWaitEvent(c->stream, c->ev_in[k], 0));
+        if ((rc = enqueue_aead(c, w, c->stream, k, algo, open, b1 - b0, dv.data() + b0, crc_mode))) return rc;
+        HIP_OK(hipEventRecord(c->ev_comp[k], c->stream));
+        HIP_OK(hipStreamWaitEvent(c->s_out, c->ev_comp[k], 0));
+        {
+            char *oh = nullptr;
+            const char *od = nullptr;
+            size_t on = 0;
+            auto flush_out = [&]() -> int {
+                if (on) HIP_OK(hipMemcpyAsync(oh, od, on, hipMemcpyDeviceToHost, c->s_out));
+                on = 0;
+                return 0;
+            };
+            for (int i = b0; i < b1; i++) {
+                if (!blks[i].len) continue;
+                char *hd = (char *)blks[i].dst;
+                const char *dd = (const char *)dv[i].dst;
+                if (!(on && oh + on == hd && od + on == dd) && (rc = flush_out())) return rc;
+                if (!on) {
+                    oh = hd;
+                    od = dd;
+                }
+                on += blks[i].len;
+                if (crc_mode || align256(blks[i].len) != blks[i].len)
+                    if ((rc = flush_out())) return rc;
+            }
+            if ((rc = flush_out())) return rc;
+            if (crc_mode == JFSX_CRC_GEN)
+                for (int i = b0; i < b1; i++)
+                    HIP_OK(hipMemcpyAsync(blks[i].crc, dv[i].crc, 4 * nseg_of(blks[i].len), hipMemcpyDeviceToHost,
+                                          c->s_out));
+        }
+        HIP_OK(hipEventRecord(c->ev_out[k], c->s_out));
+        busy[k] = (int)g;
+    }
+    for (int k = 0; k < kRing; k++)
+        if ((rc = drain(k))) return rc;
     for (int i = 0; i < n; i++) {
         blks[i].status = dv[i].status;
         blks[i].crc_bad_seg = dv[i].crc_bad_seg;
         blks[i].crc_got = dv[i].crc_got;
         blks[i].crc_expect = dv[i].crc_expect;
         if (!open) memcpy(blks[i].tag, dv[i].tag, 16);
-        // Open: plaintext is released only when the tag verified
-        if (blks[i].len && (!open || dv[i].status != JFSX_ETAG))
-            HIP_OK(hipMemcpyAsync(blks[i].dst, dv[i].dst, blks[i].len, hipMemcpyDeviceToHost, s));
-        if (crc_mode == JFSX_CRC_GEN)
-            HIP_OK(hipMemcpyAsync(blks[i].crc, dv[i].crc, 4 * nseg_of(blks[i].len), hipMemcpyDeviceToHost, s));
+        if (open && dv[i].status == JFSX_ETAG && blks[i].len) memset(blks[i].dst, 0, blks[i].len);
     }
-    HIP_OK(hipStreamSynchronize(s));
     return 0;
 }
 
@@ -375,9 +500,10 @@ int run_crc(jfsx_ctx *c, int n, jfsx_range *r, int mode) {
     const size_t o_out = off; off = align256(off + sizeof(BlkOut) * n);
     const size_t o_calc = off; off = align256(off + 4 * std::max<uint64_t>(calc_words, 1));
     int rc;
-    if ((rc = ensure_dev(c, &c->d_ws, &c->ws_cap, off))) return rc;
-    if ((rc = ensure_host(c, std::max(h_bytes, sizeof(BlkOut) * n)))) return rc;
-    char *h = c->h_ws, *d = c->d_ws;
+    Workspace &w = c->ws[0];
+    if ((rc = ensure_dev(c, &w.d, &w.dcap, off))) return rc;
+    if ((rc = ensure_host(&w.h, &w.hcap, std::max(h_bytes, sizeof(BlkOut) * n)))) return rc;
+    char *h = w.h, *d = w.d;
     BlkDev *hb = (BlkDev *)(h + o_blk);
     uint64_t calc = 0;
     for (int i = 0; i < n; i++) {
@@ -393,16 +519,16 @@ int run_crc(jfsx_ctx *c, int n, jfsx_range *r, int mode) {
     if (nt) memcpy(h + o_task, tasks.data(), sizeof(Task) * nt);
     hipStream_t s = c->stream;
     HIP_OK(hipMemcpyAsync(d, h, h_bytes, hipMemcpyHostToDevice, s));
-    if (c->timing) HIP_OK(hipEventRecord(c->ev0, s));
+    if (c->timing) HIP_OK(hipEventRecord(c->ev_k0[0], s));
     launch_crc_segments(s, (int)nt, (const Task *)(d + o_task), (const BlkDev *)(d + o_blk), c->tabs);
-    if (c->timing) HIP_OK(hipEventRecord(c->ev1, s));
+    if (c->timing) HIP_OK(hipEventRecord(c->ev_k1[0], s));
     launch_crc_finalize(s, n, mode, (const BlkDev *)(d + o_blk), (BlkOut *)(d + o_out));
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(h, d + o_out, sizeof(BlkOut) * n, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
     if (c->timing && nt) {
         float ms = 0;
-        HIP_OK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        HIP_OK(hipEventElapsedTime(&ms, c->ev_k0[0], c->ev_k1[0]));
         c->ms_total += ms;
         c->launches += 1;
     }
@@ -420,14 +546,15 @@ int run_crc_host(jfsx_ctx *c, int n, jfsx_range *r, int mode) {
     size_t need = 0;
     for (int i = 0; i < n; i++) need += align256(r[i].len) + align256(4 * nseg_of(r[i].len));
     int rc;
-    if ((rc = ensure_dev(c, &c->d_stage, &c->stage_cap, std::max<size_t>(need, 256)))) return rc;
+    Workspace &w = c->ws[0];
+    if ((rc = ensure_dev(c, &w.stage, &w.scap, std::max<size_t>(need, 256)))) return rc;
     std::vector<jfsx_range> dv(r, r + n);
     size_t off = 0;
     hipStream_t s = c->stream;
     for (int i = 0; i < n; i++) {
-        char *buf = c->d_stage + off;
+        char *buf = w.stage + off;
         off += align256(r[i].len);
-        char *cb = c->d_stage + off;
+        char *cb = w.stage + off;
         off += align256(4 * nseg_of(r[i].len));
         if (r[i].len) HIP_OK(hipMemcpyAsync(buf, r[i].data, r[i].len, hipMemcpyHostToDevice, s));
         if (mode == JFSX_CRC_VERIFY) HIP_OK(hipMemcpyAsync(cb, r[i].crc, 4 * nseg_of(r[i].len), hipMemcpyHostToDevice, s));
@@ -473,8 +600,10 @@ int jfsx_ctx_open(int device, uint32_t flags, jfsx_ctx **out) {
     HIP_OK(hipSetDevice(device));
     jfsx_ctx *c = new jfsx_ctx();
     c->device = device;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete c;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) != hipSuccess) {
+        jfsx_ctx_close(c);
         return JFSX_EIO;
     }
     std::vector<uint32_t> aes, crc, crcx;
@@ -497,9 +626,14 @@ int jfsx_ctx_open(int device, uint32_t flags, jfsx_ctx **out) {
     c->tabs.aes = c->d_tab;
     c->tabs.crc = c->d_tab + aes.size();
     c->tabs.crcx = c->d_tab + aes.size() + crc.size();
-    if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
-        jfsx_ctx_close(c);
-        return JFSX_EIO;
+    for (int k = 0; k < kRing; k++) {
+        if (hipEventCreateWithFlags(&c->ev_in[k], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_comp[k], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_out[k], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreate(&c->ev_k0[k]) != hipSuccess || hipEventCreate(&c->ev_k1[k]) != hipSuccess) {
+            jfsx_ctx_close(c);
+            return JFSX_EIO;
+        }
     }
     *out = c;
     return 0;
@@ -508,14 +642,20 @@ int jfsx_ctx_open(int device, uint32_t flags, jfsx_ctx **out) {
 int jfsx_ctx_close(jfsx_ctx *c) {
     if (!c) return JFSX_EINVAL;
     (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    (void)hipDeviceSynchronize();
     if (c->d_tab) (void)hipFree(c->d_tab);
-    if (c->d_ws) (void)hipFree(c->d_ws);
-    if (c->d_stage) (void)hipFree(c->d_stage);
-    if (c->h_ws) (void)hipHostFree(c->h_ws);
-    if (c->ev0) (void)hipEventDestroy(c->ev0);
-    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    for (int k = 0; k < kRing; k++) {
+        Workspace &w = c->ws[k];
+        if (w.d) (void)hipFree(w.d);
+        if (w.stage) (void)hipFree(w.stage);
+        if (w.h) (void)hipHostFree(w.h);
+        hipEvent_t evs[5] = {c->ev_in[k], c->ev_comp[k], c->ev_out[k], c->ev_k0[k], c->ev_k1[k]};
+        for (hipEvent_t e : evs)
+            if (e) (void)hipEventDestroy(e);
+    }
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->s_in) (void)hipStreamDestroy(c->s_in);
+    if (c->s_out) (void)hipStreamDestroy(c->s_out);
     delete c;
     return 0;
 }
@@ -523,6 +663,15 @@ int jfsx_ctx_close(jfsx_ctx *c) {
 int jfsx_ctx_sync(jfsx_ctx *c) {
     if (!c) return JFSX_EINVAL;
     HIP_OK(hipStreamSynchronize(c->stream));
+    HIP_OK(hipStreamSynchronize(c->s_in));
+    HIP_OK(hipStreamSynchronize(c->s_out));
+    return 0;
+}
+
+int jfsx_ctx_set_slot_bytes(jfsx_ctx *c, uint64_t bytes) {
+    if (!c || bytes < (1u << 20)) return JFSX_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->slot_bytes = (size_t)bytes;
     return 0;
 }
 

@@ -24,7 +24,7 @@ SEG = 32 << 10
 # every symbol include/jfsx.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "jfsx_abi_version", "jfsx_device_count", "jfsx_ctx_open", "jfsx_ctx_close", "jfsx_ctx_sync",
-    "jfsx_ctx_stream", "jfsx_ctx_set_timing", "jfsx_ctx_kernel_time", "jfsx_alloc_pinned",
+    "jfsx_ctx_stream", "jfsx_ctx_set_timing", "jfsx_ctx_set_slot_bytes", "jfsx_ctx_kernel_time", "jfsx_alloc_pinned",
     "jfsx_free_pinned", "jfsx_alloc_device", "jfsx_free_device", "jfsx_memcpy_h2d", "jfsx_memcpy_d2h",
     "jfsx_seal_batch", "jfsx_open_batch", "jfsx_crc32c_segments", "jfsx_checksum", "jfsx_cache_verify",
     "jfsx_data_encrypt", "jfsx_data_decrypt", "jfsx_parse_header", "jfsx_gen_synthetic", "jfsx_gen_key",
@@ -78,6 +78,7 @@ def load_library(path=LIB_PATH):
             "jfsx_ctx_sync": (I, [P]),
             "jfsx_ctx_stream": (P, [P]),
             "jfsx_ctx_set_timing": (I, [P, I]),
+            "jfsx_ctx_set_slot_bytes": (I, [P, U64]),
             "jfsx_ctx_kernel_time": (I, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64), I]),
             "jfsx_alloc_pinned": (I, [P, SZ, PP]),
             "jfsx_free_pinned": (I, [P, P]),
@@ -222,6 +223,17 @@ class Engine:
 
     def sync(self):
         self._check(self.L.jfsx_ctx_sync(self.ctx), "sync")
+
+    def set_slot_bytes(self, nbytes):
+        self._check(self.L.jfsx_ctx_set_slot_bytes(self.ctx, nbytes), "set_slot_bytes")
+
+    def alloc_pinned(self, nbytes):
+        p = ctypes.c_void_p()
+        self._check(self.L.jfsx_alloc_pinned(self.ctx, max(nbytes, 16), ctypes.byref(p)), "alloc_pinned")
+        return p.value
+
+    def free_pinned(self, ptr):
+        self.L.jfsx_free_pinned(self.ctx, ptr)
 
     def set_timing(self, on):
         self.L.jfsx_ctx_set_timing(self.ctx, 1 if on else 0)

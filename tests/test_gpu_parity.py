@@ -210,3 +210,48 @@ def test_large_batch_sample_vs_oracle(eng, algo):
         assert bytes(arr[b].tag) == tag, b
         assert dst.download(L, offset=b * L).tobytes() == c, b
         assert cs[512 * b:512 * (b + 1)].tobytes() == orc.checksum(p, hw=True), b
+
+
+@pytest.mark.parametrize("algo", [E.AES256GCM, E.CHACHA20P1305])
+def test_host_ingest_pipeline_ring(eng, algo):
+    """MEM_HOST batches streamed through the 3-slot ring (1 MiB slots -> many
+    groups), seal + CRC and open + verify, one tag failure wiped on Open."""
+    eng.set_slot_bytes(1 << 20)
+    try:
+        lens = [300000, 1 << 20, 5, 0, 777777, 2 << 20, 65536, 123457, 1 << 19, 4097]
+        ps, keys, outs, crcs = [], [], [], []
+        specs = []
+        for i, n in enumerate(lens):
+            key, nonce = orc.gen_key(31, i)
+            p = orc.gen_block(31, i, n)
+            o = np.zeros(max(n, 1), np.uint8)
+            cb = np.zeros(4 * max(1, -(-n // E.SEG)), np.uint8)
+            ps.append(p), keys.append((key, nonce)), outs.append(o), crcs.append(cb)
+            specs.append({"key": key, "nonce": nonce, "src": p.ctypes.data if n else None, "dst": o.ctypes.data,
+                          "len": n, "crc": cb.ctypes.data})
+        arr, nb = eng.make_blocks(specs)
+        eng.seal_batch(algo, arr, nb, E.CRC_GEN, E.MEM_HOST)
+        ospecs = []
+        plain = []
+        for i, n in enumerate(lens):
+            key, nonce = keys[i]
+            c, tag = orc.seal(ORC[algo], key, nonce, ps[i], fast=True)
+            assert bytes(arr[i].tag) == tag and outs[i][:n].tobytes() == c, i
+            assert crcs[i].tobytes() == orc.checksum(ps[i], hw=True), i
+            if i == 4:
+                tag = bytes([tag[0] ^ 2]) + tag[1:]
+            q = np.full(max(n, 1), 0xAB, np.uint8)
+            plain.append(q)
+            ospecs.append({"key": key, "nonce": nonce, "src": outs[i].ctypes.data, "dst": q.ctypes.data, "len": n,
+                           "tag": tag, "crc": crcs[i].ctypes.data})
+        oarr, nb = eng.make_blocks(ospecs)
+        eng.open_batch(algo, oarr, nb, E.CRC_VERIFY, E.MEM_HOST)
+        for i, n in enumerate(lens):
+            if i == 4:
+                assert oarr[i].status == E.ETAG
+                assert not plain[i][:n].any()  # nothing released
+            else:
+                assert oarr[i].status == E.OK, i
+                assert plain[i][:n].tobytes() == ps[i].tobytes(), i
+    finally:
+        eng.set_slot_bytes(256 << 20)
