@@ -395,9 +395,10 @@ int run_aead_host(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int c
         for (int i = b0; i < b1; i++)
             need += align256(blks[i].len) + (crc_mode ? align256(4 * nseg_of(blks[i].len)) : 0);
         if ((rc = ensure_dev(c, &w.stage, &w.scap, std::max<size_t>(need, 256)))) return rc;
-        size_t off = 0;
-        // data copies are coalesced over runs of blocks adjacent both in the
-        // caller's memory and in the staging slot (one DMA per run)
+        // slot layout: all block data first (coalesced DMA runs over blocks
+        // adjacent in both the caller's memory and the slot), then the CRCs
+        size_t off = 0, coff = 0;
+        for (int i = b0; i < b1; i++) coff += align256(blks[i].len);
         const char *run_h = nullptr;
         char *run_d = nullptr;
         size_t run_n = 0;
@@ -422,9 +423,8 @@ int run_aead_host(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int c
             dv[i].src = buf;
             dv[i].dst = buf;
             if (crc_mode) {
-                char *cb = w.stage + off;
-                off += align256(4 * nseg_of(blks[i].len));
-                if ((rc = flush_in())) return rc;
+                char *cb = w.stage + coff;
+                coff += align256(4 * nseg_of(blks[i].len));
                 if (crc_mode == JFSX_CRC_VERIFY)
                     HIP_OK(hipMemcpyAsync(cb, blks[i].crc, 4 * nseg_of(blks[i].len), hipMemcpyHostToDevice, c->s_in));
                 dv[i].crc = (uint8_t *)cb;
@@ -455,8 +455,7 @@ int run_aead_host(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int c
                     od = dd;
                 }
                 on += blks[i].len;
-                if (crc_mode || align256(blks[i].len) != blks[i].len)
-                    if ((rc = flush_out())) return rc;
+                if (align256(blks[i].len) != blks[i].len && (rc = flush_out())) return rc;
             }
             if ((rc = flush_out())) return rc;
             if (crc_mode == JFSX_CRC_GEN)
