@@ -47,32 +47,19 @@ def parse():
 
 
 def dist_setup(args):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
-        dist = tdist
-    return world, rank, local, dist
+    from juicefs_amd import shard
+    world, rank, local = shard.dist_env()
+    return world, rank, local, shard.init()
 
 
 def barrier(dist):
-    if dist is not None:
-        dist.barrier()
+    from juicefs_amd import shard
+    shard.barrier(dist)
 
 
 def max_over_ranks(dist, x, local):
-    if dist is None:
-        return x
-    import torch
-    dev = "cuda:%d" % local if torch.cuda.is_available() else "cpu"
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    from juicefs_amd import shard
+    return shard.max_over_ranks(dist, x, local)
 
 
 def cpu_baseline(args):
@@ -116,7 +103,7 @@ def main():
     src = eng.alloc(nb * L)
     dst = eng.alloc(nb * L) if args.mode != "crc" else None
     crc = eng.alloc(nb * 4 * nseg)
-    base = rank * nb  # global block index: blocks shard across ranks
+    base = rank * nb  # global block index: blocks shard across ranks (juicefs_amd.shard.shard)
     for b in range(nb):
         eng.gen_synthetic(src, L, SEED, base + b, offset=b * L)
     eng.sync()
