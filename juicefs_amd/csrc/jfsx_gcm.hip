@@ -147,6 +147,23 @@ __device__ __forceinline__ void gh_rho_inv(const uint32_t R[4], const GhLane &g,
 
 // One Horner step in the rotated frame: R <- rho(unrho(R) * H^64 ^ c)
 __device__ __forceinline__ void ghash_step(const char *lds, uint32_t R[4], const GhLane &g, uint4 c) {
+#if JFSX_GH8
+    // two halves of 8 lookups each: at most 32 VGPRs of table entries in flight
+    uint32_t S[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        uint4 t[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int dd = 2 * h + (q >> 2), bb = q & 3;
+            t[q] = lds_u4(lds, kLdsGh + __builtin_amdgcn_perm(R[dd], g.off[dd], g.sel[bb]));
+        }
+#define GX(f, i) S[i] = xor3(xor3(t[0].f, t[1].f, t[2].f), xor3(t[3].f, t[4].f, t[5].f), xor3(t[6].f, t[7].f, S[i]))
+        GX(x, 0); GX(y, 1); GX(z, 2); GX(w, 3);
+#undef GX
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#else
     uint4 t[16];
 #pragma unroll
     for (int dd = 0; dd < 4; dd++)
@@ -158,6 +175,7 @@ __device__ __forceinline__ void ghash_step(const char *lds, uint32_t R[4], const
                        xor3(t[9].f, t[10].f, t[11].f), xor3(xor3(t[12].f, t[13].f, t[14].f), t[15].f, cf))
     const uint32_t S[4] = {GX(x, c.x), GX(y, c.y), GX(z, c.z), GX(w, c.w)};
 #undef GX
+#endif
     gh_rho(S, g, R);
 }
 
@@ -347,7 +365,43 @@ __global__ __launch_bounds__(kThreads) void gcm_main_k(const Task *__restrict__ 
 #pragma unroll
     for (int s = 0; s < NS; s++)
         nxt[s] = rf ? *reinterpret_cast<const uint4 *>(src + ld0[s] + lo) : make_uint4(0, 0, 0, 0);
-    for (uint64_t r = 0; r < rf; r++) {
+    uint64_t r0 = 0;
+#if JFSX_U2
+    // two rows of one stream per iteration: the two AES chains interleave,
+    // GHASH/CRC stay sequential (register peak of one row)
+    if (NS == 1 && act[0] && rf >= 2) {
+        uint4 n0 = *reinterpret_cast<const uint4 *>(src + ld0[0] + lo);
+        uint4 n1 = *reinterpret_cast<const uint4 *>(src + ld0[0] + 1024 + lo);
+        for (; r0 + 1 < rf; r0 += 2) {
+            const uint4 dd[2] = {n0, n1};
+            const uint64_t o0 = ld0[0] + 1024 * r0 + lo;
+            if (r0 + 3 < rf) {
+                n0 = *reinterpret_cast<const uint4 *>(src + o0 + 2048);
+                n1 = *reinterpret_cast<const uint4 *>(src + o0 + 3072);
+            }
+            const uint32_t ctr2[2] = {(uint32_t)((o0 >> 4) + 2), (uint32_t)((o0 >> 4) + 66)};
+            uint32_t ks2[2][4];
+            aes_ctr_blocks<2>(lds, loff, rk, k1, ctr2, ks2);
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const uint64_t o = o0 + 1024 * u;
+                const uint4 x = make_uint4(dd[u].x ^ ks2[u][0], dd[u].y ^ ks2[u][1], dd[u].z ^ ks2[u][2],
+                                           dd[u].w ^ ks2[u][3]);
+                const uint4 c = OPEN ? dd[u] : x, p = OPEN ? x : dd[u];
+                *reinterpret_cast<uint4 *>(dst + o) = OPEN ? p : c;
+                ghash_step(lds, st[0].acc, gl, c);
+                if (CRCMODE) st[0].A = crc_piece<kLdsCrc>(lds, st[0].A, p.x, p.y, p.z, p.w);
+                if (CRCMODE && ((r0 + u) & 31) == 31) {
+                    crc_segment_end<CRCMODE>(blk, tab, lane, xl, st[0].seg0, st[0].seg0 + kSeg, st[0].A, 0);
+                    st[0].A = 0;
+                    st[0].seg0 += kSeg;
+                }
+            }
+        }
+        if (r0 < rf) nxt[0] = *reinterpret_cast<const uint4 *>(src + ld0[0] + 1024 * r0 + lo);
+    }
+#endif
+    for (uint64_t r = r0; r < rf; r++) {
         uint4 d[NS];
         uint32_t ctr[NS];
 #pragma unroll
