@@ -16,6 +16,8 @@
  *   jfsx_checksum        checksum(data) []byte                      pkg/chunk/disk_cache.go:1218-1231
  *   jfsx_crc32c_segments the CRC loop of cacheFile.ReadAt           pkg/chunk/disk_cache.go:1315-1327
  *   jfsx_cache_verify    cacheFile.ReadAt level logic + verify      pkg/chunk/disk_cache.go:1255-1329
+ *   jfsx_object_crc32c   generateChecksum / checksumReader of the   pkg/object/checksum.go:31-82
+ *   (+ JFSX_CRC_CT)      stored object, fused with Seal/Open        (s3.go:140-146,173-176)
  *   JFSX_AES256GCM /     NewDataEncryptor algo "aes256gcm-rsa" /    pkg/object/encrypt.go:142-162
  *   JFSX_CHACHA20P1305   "chacha20-rsa"
  *
@@ -42,7 +44,7 @@
 extern "C" {
 #endif
 
-#define JFSX_ABI_VERSION 1
+#define JFSX_ABI_VERSION 2
 
 /* algorithms (encrypt.go:142-145) */
 #define JFSX_AES256GCM 0     /* "aes256gcm-rsa" (also the "" default)   */
@@ -55,6 +57,11 @@ extern "C" {
 #define JFSX_CRC_NONE 0   /* no checksum                                  */
 #define JFSX_CRC_GEN 1    /* write crc[] (level != none on cache write)   */
 #define JFSX_CRC_VERIFY 2 /* compare against crc[] (cache read verify)    */
+/* flag OR'ed into GEN/VERIFY: the segment CRCs cover the ciphertext C (seal:
+ * output, open: input) instead of the plaintext -- the bytes the object store
+ * checksums (pkg/object/checksum.go:31-53, s3.go:173-176); fold them into the
+ * whole-object value with jfsx_object_crc32c. */
+#define JFSX_CRC_CT 4
 
 /* where src/dst/crc pointers of a batch live */
 #define JFSX_MEM_DEVICE 0 /* device memory (jfsx_alloc_device / hipMalloc) */
@@ -156,15 +163,33 @@ int jfsx_cache_verify(jfsx_ctx *ctx, const void *file, uint64_t file_size, uint6
 
 /* dataEncryptor.Encrypt with an already-wrapped key: writes
  * BE16(wlen) | 12 | wrapped | nonce | C | tag into out (host memory).
- * out_cap must be >= 3+wlen+12+len+16. */
+ * out_cap must be >= 3+wlen+12+len+16.  obj_crc (nullable) receives the
+ * object-store checksum of the whole output, generateChecksum's value
+ * (checksum.go:31-53), computed in the same pass as the Seal. */
 int jfsx_data_encrypt(jfsx_ctx *ctx, int algo, const uint8_t key[32], const uint8_t nonce[12],
                       const uint8_t *wrapped, int wlen, const void *plaintext, uint64_t len, void *out,
-                      uint64_t out_cap, uint64_t *out_len);
+                      uint64_t out_cap, uint64_t *out_len, uint32_t *obj_crc);
 /* dataEncryptor.Decrypt after the key is unwrapped: parses the header
  * (JFSX_EMISFORMED if 3+klen+nlen >= olen), opens, and writes the plaintext
- * to out only when the tag verifies (returns JFSX_ETAG otherwise). */
+ * to out only when the tag verifies (returns JFSX_ETAG otherwise).  With
+ * expect_crc non-null the object checksum is verified in the same pass
+ * (checksumReader, checksum.go:55-82): on mismatch returns JFSX_ECRC with the
+ * computed value in *got_crc ("verify checksum failed: %d != %d") and releases
+ * no plaintext; the checksum failure takes precedence over JFSX_ETAG. */
 int jfsx_data_decrypt(jfsx_ctx *ctx, int algo, const uint8_t key[32], const void *obj, uint64_t olen,
-                      void *out, uint64_t out_cap, uint64_t *out_len);
+                      void *out, uint64_t out_cap, uint64_t *out_len, const uint32_t *expect_crc,
+                      uint32_t *got_crc);
+
+/* crc32.Update(crc, MakeTable(Castagnoli), data) on the host (small spans:
+ * object header and tag) */
+uint32_t jfsx_crc32c_update(uint32_t crc, const void *data, uint64_t n);
+/* CRC32C of A||B from crc(A), crc(B), len(B) (GF(2) shift by x^(8 len B)) */
+uint32_t jfsx_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+/* object-store checksum of header || C || tag (checksum.go:31-53) from the
+ * big-endian 32 KiB segment CRCs of C that a GEN|CT batch returned */
+int jfsx_object_crc32c(const void *hdr, uint64_t hlen, const uint8_t *seg_crcs, uint64_t clen,
+                       const uint8_t *tag, uint32_t *out);
+
 /* header helper: returns wrapped-key length and offset/size of the nonce so a
  * caller can unwrap the key first (encrypt.go:197-205) */
 int jfsx_parse_header(const void *obj, uint64_t olen, int *klen, int *nlen);

@@ -216,7 +216,8 @@ bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
 
 int check_aead_args(int algo, int n, const jfsx_blk *blks, int crc_mode, bool device) {
     if (algo != JFSX_AES256GCM && algo != JFSX_CHACHA20P1305) return JFSX_EINVAL;
-    if (crc_mode < 0 || crc_mode > 2 || n < 0) return JFSX_EINVAL;
+    if (crc_mode < 0 || (crc_mode & ~(3 | JFSX_CRC_CT)) || (crc_mode & 3) == 3 || crc_mode == JFSX_CRC_CT || n < 0)
+        return JFSX_EINVAL;
     for (int i = 0; i < n; i++) {
         const jfsx_blk &b = blks[i];
         if (b.len && (!b.src || !b.dst)) return JFSX_EINVAL;
@@ -238,7 +239,7 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, int k, int algo, bool
     uint64_t crc_calc_words = 0;
     for (int i = 0; i < n; i++) {
         lens[i] = blks[i].len;
-        if (crc_mode == JFSX_CRC_VERIFY) crc_calc_words += nseg_of(blks[i].len);
+        if ((crc_mode & 3) == JFSX_CRC_VERIFY) crc_calc_words += nseg_of(blks[i].len);
     }
     const uint32_t slots = gcm ? kSlotsPerTask : kCpWaves;
     Plan plan = gcm ? plan_tasks(lens, kMaxTaskBytes, kWaves, slots, 512)
@@ -273,7 +274,7 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, int k, int algo, bool
         hb[i].len = b.len;
         hb[i].crc = b.crc;
         hb[i].crc_calc = nullptr;
-        if (crc_mode == JFSX_CRC_VERIFY) {
+        if ((crc_mode & 3) == JFSX_CRC_VERIFY) {
             hb[i].crc_calc = (uint32_t *)(d + o_calc) + calc;
             calc += nseg_of(b.len);
         }
@@ -289,7 +290,7 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, int k, int algo, bool
     }
     if (nt) memcpy(h + o_task, plan.tasks.data(), sizeof(Task) * nt);
     HIP_OK(hipMemcpyAsync(d, h, h_bytes, hipMemcpyHostToDevice, s));
-    if (crc_mode == JFSX_CRC_GEN)
+    if ((crc_mode & 3) == JFSX_CRC_GEN)
         for (int i = 0; i < n; i++)
             if (blks[i].len == 0) HIP_OK(hipMemsetAsync(blks[i].crc, 0, 4, s));
     const KeyIn *dk = (const KeyIn *)(d + o_keys);
@@ -425,7 +426,7 @@ int run_aead_host(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int c
             if (crc_mode) {
                 char *cb = w.stage + coff;
                 coff += align256(4 * nseg_of(blks[i].len));
-                if (crc_mode == JFSX_CRC_VERIFY)
+                if ((crc_mode & 3) == JFSX_CRC_VERIFY)
                     HIP_OK(hipMemcpyAsync(cb, blks[i].crc, 4 * nseg_of(blks[i].len), hipMemcpyHostToDevice, c->s_in));
                 dv[i].crc = (uint8_t *)cb;
             }
@@ -458,7 +459,7 @@ int run_aead_host(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int c
                 if (align256(blks[i].len) != blks[i].len && (rc = flush_out())) return rc;
             }
             if ((rc = flush_out())) return rc;
-            if (crc_mode == JFSX_CRC_GEN)
+            if ((crc_mode & 3) == JFSX_CRC_GEN)
                 for (int i = b0; i < b1; i++)
                     HIP_OK(hipMemcpyAsync(blks[i].crc, dv[i].crc, 4 * nseg_of(blks[i].len), hipMemcpyDeviceToHost,
                                           c->s_out));
@@ -885,8 +886,64 @@ int jfsx_parse_header(const void *obj, uint64_t olen, int *klen, int *nlen) {
     return 0;
 }
 
+// ---------------------------------------------------------------------------
+// host CRC32C helpers for the object checksum (pkg/object/checksum.go)
+// ---------------------------------------------------------------------------
+namespace {
+const uint32_t *crc_table1() {
+    static uint32_t t[256];
+    static std::once_flag once;
+    std::call_once(once, [] {
+        for (uint32_t i = 0; i < 256; i++) {
+            uint32_t v = i;
+            for (int k = 0; k < 8; k++) v = v & 1 ? (v >> 1) ^ kCrcPoly : v >> 1;
+            t[i] = v;
+        }
+    });
+    return t;
+}
+uint32_t h_xpow8(uint64_t n) {  // x^(8n) mod P
+    uint32_t r = 1u << 31, p = 1u << 23;
+    for (; n; n >>= 1) {
+        if (n & 1) r = crc_mulmod_h(p, r);
+        p = crc_mulmod_h(p, p);
+    }
+    return r;
+}
+uint32_t be32(const uint8_t *p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
+}  // namespace
+
+uint32_t jfsx_crc32c_update(uint32_t crc, const void *data, uint64_t n) {
+    // hash/crc32.Update(crc, MakeTable(Castagnoli), p): pre/post-inverted
+    const uint32_t *t = crc_table1();
+    const uint8_t *p = (const uint8_t *)data;
+    crc = ~crc;
+    for (uint64_t i = 0; i < n; i++) crc = t[(crc ^ p[i]) & 0xff] ^ (crc >> 8);
+    return ~crc;
+}
+
+uint32_t jfsx_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {
+    return len_b ? crc_mulmod_h(h_xpow8(len_b), crc_a) ^ crc_b : crc_a;
+}
+
+int jfsx_object_crc32c(const void *hdr, uint64_t hlen, const uint8_t *seg_crcs, uint64_t clen, const uint8_t *tag,
+                       uint32_t *out) {
+    // generateChecksum(header || C || tag) (checksum.go:31-53) from the
+    // engine's big-endian 32 KiB segment CRCs of C (crc_mode GEN|CT)
+    if (!out || (hlen && !hdr) || (clen && !seg_crcs) || !tag) return JFSX_EINVAL;
+    uint32_t crc = jfsx_crc32c_update(0, hdr, hlen);
+    const uint64_t ns = clen ? (clen - 1) / kSeg + 1 : 0;
+    for (uint64_t j = 0; j < ns; j++) {
+        const uint64_t lj = std::min<uint64_t>(kSeg, clen - j * kSeg);
+        crc = jfsx_crc32c_combine(crc, be32(seg_crcs + 4 * j), lj);
+    }
+    *out = jfsx_crc32c_update(crc, tag, 16);
+    return 0;
+}
+
 int jfsx_data_encrypt(jfsx_ctx *c, int algo, const uint8_t key[32], const uint8_t nonce[12], const uint8_t *wrapped,
-                      int wlen, const void *plaintext, uint64_t len, void *out, uint64_t out_cap, uint64_t *out_len) {
+                      int wlen, const void *plaintext, uint64_t len, void *out, uint64_t out_cap, uint64_t *out_len,
+                      uint32_t *obj_crc) {
     // encrypt.go:182-193: [BE16 klen][nlen][wrapped key][nonce][Seal(plaintext)]
     if (!c || !key || !nonce || wlen < 0 || wlen > 65535 || (wlen && !wrapped) || !out) return JFSX_EINVAL;
     const uint64_t hdr = 3 + (uint64_t)wlen + 12;
@@ -904,21 +961,29 @@ int jfsx_data_encrypt(jfsx_ctx *c, int algo, const uint8_t key[32], const uint8_
     b.src = plaintext;
     b.dst = o + hdr;
     b.len = len;
-    int rc = jfsx_seal_batch(c, algo, 1, &b, JFSX_CRC_NONE, JFSX_MEM_HOST);
+    std::vector<uint8_t> segs;
+    if (obj_crc) {
+        segs.resize(4 * nseg_of(len));
+        b.crc = segs.data();
+    }
+    int rc = jfsx_seal_batch(c, algo, 1, &b, obj_crc ? JFSX_CRC_GEN | JFSX_CRC_CT : JFSX_CRC_NONE, JFSX_MEM_HOST);
     if (rc) return rc;
     memcpy(o + hdr + len, b.tag, 16);
+    if (obj_crc && (rc = jfsx_object_crc32c(o, hdr, segs.data(), len, b.tag, obj_crc))) return rc;
     if (out_len) *out_len = hdr + len + 16;
     return 0;
 }
 
 int jfsx_data_decrypt(jfsx_ctx *c, int algo, const uint8_t key[32], const void *obj, uint64_t olen, void *out,
-                      uint64_t out_cap, uint64_t *out_len) {
-    // encrypt.go:196-216
+                      uint64_t out_cap, uint64_t *out_len, const uint32_t *expect_crc, uint32_t *got_crc) {
+    // encrypt.go:196-216; with expect_crc, the object checksum the store kept
+    // (checksum.go:55-82) is verified in the same pass over C
     if (!c || !key || !obj || !out) return JFSX_EINVAL;
     int kl = 0, nl = 0;
     int rc = jfsx_parse_header(obj, olen, &kl, &nl);
     if (rc) return rc;
     const uint8_t *o = (const uint8_t *)obj;
+    if (expect_crc && !got_crc) return JFSX_EINVAL;
     if (nl != 12) return JFSX_ETAG;  // aead.Open rejects a wrong nonce size (recovered as an error upstream)
     const uint64_t hdr = 3 + (uint64_t)kl + nl;
     if (olen - hdr < 16) return JFSX_ETAG;  // shorter than the tag: cipher: message authentication failed
@@ -932,8 +997,21 @@ int jfsx_data_decrypt(jfsx_ctx *c, int algo, const uint8_t key[32], const void *
     b.dst = out;
     b.len = len;
     memcpy(b.tag, o + hdr + len, 16);
-    rc = jfsx_open_batch(c, algo, 1, &b, JFSX_CRC_NONE, JFSX_MEM_HOST);
+    std::vector<uint8_t> segs;
+    if (expect_crc) {
+        segs.resize(4 * nseg_of(len));
+        b.crc = segs.data();
+    }
+    rc = jfsx_open_batch(c, algo, 1, &b, expect_crc ? JFSX_CRC_GEN | JFSX_CRC_CT : JFSX_CRC_NONE, JFSX_MEM_HOST);
     if (rc) return rc;
+    if (expect_crc) {
+        // the store's read fails first ("verify checksum failed"), before Decrypt sees the bytes
+        if ((rc = jfsx_object_crc32c(o, hdr, segs.data(), len, o + hdr + len, got_crc))) return rc;
+        if (*got_crc != *expect_crc) {
+            if (len) memset(out, 0, len);
+            return JFSX_ECRC;
+        }
+    }
     if (b.status == JFSX_ETAG) return JFSX_ETAG;
     if (out_len) *out_len = len;
     return 0;

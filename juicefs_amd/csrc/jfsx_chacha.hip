@@ -178,7 +178,7 @@ __device__ __forceinline__ void cp_segment_end(const BlkDev &blk, const DevTable
     if (lane == 0) {
         const uint32_t crc = ~(K ^ raw);
         const uint64_t si = seg0 / kSeg;
-        if (CRCMODE == 1)
+        if ((CRCMODE & 3) == 1)
             *reinterpret_cast<uint32_t *>(blk.crc + 4 * si) = __builtin_bswap32(crc);
         else
             blk.crc_calc[si] = crc;
@@ -220,15 +220,16 @@ __device__ __noinline__ CpStream cp_row_generic(const char *lds, const CpSched *
         }
         store_piece(blk.dst, o, end, OPEN ? p : c);
         st.A = p_add(p_mul(st.A, q == 0 ? r253 : r1), p_from_words(c.x, c.y, c.z, c.w, 1));
+        const uint4 cq = crc_src<CRCMODE>(c, p);
         st.jlast = o >> 4;
         st.has = true;
         if (CRCMODE) {
             if (full) {
-                st.C = q == 0 ? crc_piece<kLdsCrcCp, 20>(lds, st.C, p.x, p.y, p.z, p.w)
-                              : crc_piece<kLdsCrcCp, -1>(lds, st.C, p.x, p.y, p.z, p.w);
+                st.C = q == 0 ? crc_piece<kLdsCrcCp, 20>(lds, st.C, cq.x, cq.y, cq.z, cq.w)
+                              : crc_piece<kLdsCrcCp, -1>(lds, st.C, cq.x, cq.y, cq.z, cq.w);
                 st.lend = (uint32_t)(o + 16 - st.seg0);
             } else {
-                const uint32_t pw[4] = {p.x, p.y, p.z, p.w};
+                const uint32_t pw[4] = {cq.x, cq.y, cq.z, cq.w};
                 st.C = q == 0 ? crc_partial<kLdsCrcCp, 20>(lds, st.C, pw, (int)(end - o))
                               : crc_partial<kLdsCrcCp, -1>(lds, st.C, pw, (int)(end - o));
                 st.lend = (uint32_t)(end - st.seg0);
@@ -302,10 +303,11 @@ __global__ __launch_bounds__(kCpWaves * 64) void cp_main_k(const Task *__restric
                                        d[q].w ^ ks[4 * q + 3]);
             const uint4 c = OPEN ? d[q] : x, p = OPEN ? x : d[q];
             *reinterpret_cast<uint4 *>(dst + o + 16 * q) = OPEN ? p : c;
+            const uint4 cq = crc_src<CRCMODE>(c, p);
             st.A = p_add(p_mul(st.A, q == 0 ? r253 : r1), p_from_words(c.x, c.y, c.z, c.w, 1));
             if (CRCMODE) {
-                st.C = q == 0 ? crc_piece<kLdsCrcCp, 20>(lds, st.C, p.x, p.y, p.z, p.w)
-                              : crc_piece<kLdsCrcCp, -1>(lds, st.C, p.x, p.y, p.z, p.w);
+                st.C = q == 0 ? crc_piece<kLdsCrcCp, 20>(lds, st.C, cq.x, cq.y, cq.z, cq.w)
+                              : crc_piece<kLdsCrcCp, -1>(lds, st.C, cq.x, cq.y, cq.z, cq.w);
             }
         }
         if (CRCMODE && (r & 7) == 7) {
@@ -420,7 +422,7 @@ __global__ __launch_bounds__(64) void cp_finalize_k(const BlkDev *__restrict__ b
         for (int q = 0; q < 4; q++) d |= o.tag[q] ^ tg[q];
         if (d) o.status = JFSX_ETAG;
     }
-    if (CRCMODE == 2) {
+    if ((CRCMODE & 3) == 2) {
         crc_verify_block(blk, o, lane);
         if (o.bad_seg >= 0 && o.status == JFSX_OK) o.status = JFSX_ECRC;
     }
@@ -439,10 +441,17 @@ void launch_cp_main(hipStream_t s, int ntasks, bool open, int crc_mode, const Ta
     if (ntasks <= 0) return;
     dim3 g(ntasks), bl(kCpWaves * 64);
 #define L(O, C) hipLaunchKernelGGL((cp_main_k<O, C>), g, bl, 0, s, tasks, blks, sched, partial, pexp, t)
-    if (open) {
-        if (crc_mode == 0) L(true, 0); else if (crc_mode == 1) L(true, 1); else L(true, 2);
-    } else {
-        if (crc_mode == 0) L(false, 0); else if (crc_mode == 1) L(false, 1); else L(false, 2);
+    switch ((open ? 8 : 0) | crc_mode) {
+        case 8: L(true, 0); break;
+        case 9: L(true, 1); break;
+        case 10: L(true, 2); break;
+        case 13: L(true, 5); break;
+        case 14: L(true, 6); break;
+        case 0: L(false, 0); break;
+        case 1: L(false, 1); break;
+        case 2: L(false, 2); break;
+        case 5: L(false, 5); break;
+        case 6: L(false, 6); break;
     }
 #undef L
 }
@@ -452,9 +461,9 @@ void launch_cp_finalize(hipStream_t s, int n, bool open, int crc_mode, const Blk
     if (n <= 0) return;
 #define L(O, C) hipLaunchKernelGGL((cp_finalize_k<O, C>), dim3(n), dim3(64), 0, s, blks, sched, partial, pexp, out)
     if (open) {
-        if (crc_mode == 2) L(true, 2); else L(true, 0);
+        if ((crc_mode & 3) == 2) L(true, 2); else L(true, 0);
     } else {
-        if (crc_mode == 2) L(false, 2); else L(false, 0);
+        if ((crc_mode & 3) == 2) L(false, 2); else L(false, 0);
     }
 #undef L
 }

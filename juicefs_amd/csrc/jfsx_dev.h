@@ -29,6 +29,14 @@ __device__ __forceinline__ uint32_t crc_piece(const char *lds, uint32_t A, uint3
 }
 
 // byte-serial tail: crc_raw(shift(A,1008), first n bytes of the piece)
+// CRCMODE bit 2 (JFSX_CRC_CT): the segment CRCs cover the ciphertext side
+// (object checksum, pkg/object/checksum.go:31-53) instead of the plaintext
+// (cache-file checksum, disk_cache.go:1218-1231).
+template <int CRCMODE>
+__device__ __forceinline__ uint4 crc_src(uint4 c, uint4 p) {
+    return (CRCMODE & 4) ? c : p;
+}
+
 template <uint32_t CB, int S = 16>
 __device__ __noinline__ uint32_t crc_partial(const char *lds, uint32_t A, const uint32_t p[4], int n) {
     uint32_t c = S < 0 ? A : CRC_T(S, A, 0) ^ CRC_T(S + 1, A, 1) ^ CRC_T(S + 2, A, 2) ^ CRC_T(S + 3, A, 3);

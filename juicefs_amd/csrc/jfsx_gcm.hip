@@ -206,7 +206,7 @@ __device__ __forceinline__ void crc_segment_end(const BlkDev &blk, const DevTabl
     if (lane == 0) {
         const uint32_t crc = ~(K ^ raw);
         const uint64_t si = seg0 / kSeg;
-        if (CRCMODE == 1)
+        if ((CRCMODE & 3) == 1)
             *reinterpret_cast<uint32_t *>(blk.crc + 4 * si) = __builtin_bswap32(crc);
         else
             blk.crc_calc[si] = crc;
@@ -250,12 +250,13 @@ __device__ __noinline__ Stream row_generic(const char *lds, uint32_t loff, const
         st.jlast = o >> 4;
         st.has = true;
     }
+    const uint4 cq = crc_src<CRCMODE>(c, p);
     if (CRCMODE) {
         if (full) {
-            st.A = crc_piece<kLdsCrc>(lds, st.A, p.x, p.y, p.z, p.w);
+            st.A = crc_piece<kLdsCrc>(lds, st.A, cq.x, cq.y, cq.z, cq.w);
             st.lend = (uint32_t)(o + 16 - st.seg0);
         } else if (valid) {
-            const uint32_t pw[4] = {p.x, p.y, p.z, p.w};
+            const uint32_t pw[4] = {cq.x, cq.y, cq.z, cq.w};
             st.A = crc_partial<kLdsCrc>(lds, st.A, pw, (int)(end - o));
             st.lend = (uint32_t)(end - st.seg0);
         }
@@ -389,8 +390,9 @@ __global__ __launch_bounds__(kThreads) void gcm_main_k(const Task *__restrict__ 
                                            dd[u].w ^ ks2[u][3]);
                 const uint4 c = OPEN ? dd[u] : x, p = OPEN ? x : dd[u];
                 *reinterpret_cast<uint4 *>(dst + o) = OPEN ? p : c;
+                const uint4 cq = crc_src<CRCMODE>(c, p);
                 ghash_step(lds, st[0].acc, gl, c);
-                if (CRCMODE) st[0].A = crc_piece<kLdsCrc>(lds, st[0].A, p.x, p.y, p.z, p.w);
+                if (CRCMODE) st[0].A = crc_piece<kLdsCrc>(lds, st[0].A, cq.x, cq.y, cq.z, cq.w);
                 if (CRCMODE && ((r0 + u) & 31) == 31) {
                     crc_segment_end<CRCMODE>(blk, tab, lane, xl, st[0].seg0, st[0].seg0 + kSeg, st[0].A, 0);
                     st[0].A = 0;
@@ -420,8 +422,9 @@ __global__ __launch_bounds__(kThreads) void gcm_main_k(const Task *__restrict__ 
             const uint4 x = make_uint4(d[s].x ^ ks[s][0], d[s].y ^ ks[s][1], d[s].z ^ ks[s][2], d[s].w ^ ks[s][3]);
             const uint4 c = OPEN ? d[s] : x, p = OPEN ? x : d[s];
             *reinterpret_cast<uint4 *>(dst + o) = OPEN ? p : c;
+            const uint4 cq = crc_src<CRCMODE>(c, p);
             ghash_step(lds, st[s].acc, gl, c);
-            if (CRCMODE) st[s].A = crc_piece<kLdsCrc>(lds, st[s].A, p.x, p.y, p.z, p.w);
+            if (CRCMODE) st[s].A = crc_piece<kLdsCrc>(lds, st[s].A, cq.x, cq.y, cq.z, cq.w);
         }
         if (CRCMODE && (r & 31) == 31) {
 #pragma unroll
@@ -624,7 +627,7 @@ __global__ __launch_bounds__(64) void gcm_finalize_k(const BlkDev *__restrict__ 
         for (int q = 0; q < 4; q++) d |= acc[q] ^ t[q];
         if (d) o.status = JFSX_ETAG;
     }
-    if (CRCMODE == 2) {
+    if ((CRCMODE & 3) == 2) {
         crc_verify_block(blk, o, lane);
         if (o.bad_seg >= 0 && o.status == JFSX_OK) o.status = JFSX_ECRC;
     }
@@ -643,10 +646,17 @@ void launch_gcm_main(hipStream_t s, int ntasks, bool open, int crc_mode, const T
     if (ntasks <= 0) return;
     dim3 g(ntasks), bl(kThreads);
 #define L(O, C) hipLaunchKernelGGL((gcm_main_k<O, C, kStreams>), g, bl, 0, s, tasks, blks, sched, partial, pexp, t)
-    if (open) {
-        if (crc_mode == 0) L(true, 0); else if (crc_mode == 1) L(true, 1); else L(true, 2);
-    } else {
-        if (crc_mode == 0) L(false, 0); else if (crc_mode == 1) L(false, 1); else L(false, 2);
+    switch ((open ? 8 : 0) | crc_mode) {
+        case 8: L(true, 0); break;
+        case 9: L(true, 1); break;
+        case 10: L(true, 2); break;
+        case 13: L(true, 5); break;
+        case 14: L(true, 6); break;
+        case 0: L(false, 0); break;
+        case 1: L(false, 1); break;
+        case 2: L(false, 2); break;
+        case 5: L(false, 5); break;
+        case 6: L(false, 6); break;
     }
 #undef L
 }
@@ -656,9 +666,9 @@ void launch_gcm_finalize(hipStream_t s, int n, bool open, int crc_mode, const Bl
     if (n <= 0) return;
 #define L(O, C) hipLaunchKernelGGL((gcm_finalize_k<O, C>), dim3(n), dim3(64), 0, s, blks, sched, partial, pexp, out)
     if (open) {
-        if (crc_mode == 2) L(true, 2); else L(true, 0);
+        if ((crc_mode & 3) == 2) L(true, 2); else L(true, 0);
     } else {
-        if (crc_mode == 2) L(false, 2); else L(false, 0);
+        if ((crc_mode & 3) == 2) L(false, 2); else L(false, 0);
     }
 #undef L
 }

@@ -231,10 +231,13 @@ class DataEncryptor:
             raise r
         return r
 
-    def EncryptBatch(self, plaintexts):
-        """Encrypt many objects with one engine call (the shim's aggregation window)."""
+    def EncryptBatch(self, plaintexts, checksums=False):
+        """Encrypt many objects with one engine call (the shim's aggregation
+        window).  checksums=True also returns each stored object's CRC32C
+        (checksum.go:31-53), computed in the same pass (JFSX_CRC_CT): then the
+        result is a list of (object, checksum string)."""
         import numpy as np
-        specs, outs, hdrs = [], [], []
+        specs, outs, hdrs, segs = [], [], [], []
         for p in plaintexts:
             p = bytes(p)
             key = self._rand(self.keyLen)
@@ -245,19 +248,32 @@ class DataEncryptor:
             dst = np.empty(max(len(p), 1), np.uint8)
             outs.append((src, dst, len(p)))
             hdrs.append(hdr)
-            specs.append({"key": key, "nonce": nonce, "src": src.ctypes.data if p else None, "dst": dst.ctypes.data,
-                          "len": len(p)})
+            spec = {"key": key, "nonce": nonce, "src": src.ctypes.data if p else None, "dst": dst.ctypes.data,
+                    "len": len(p)}
+            if checksums:
+                sb = np.zeros(4 * max(1, -(-len(p) // (32 << 10))), np.uint8)
+                segs.append(sb)
+                spec["crc"] = sb.ctypes.data
+            specs.append(spec)
         if not specs:
             return []
         arr, n = self.eng.make_blocks(specs)
-        self.eng.seal_batch(self.algo, arr, n, E.CRC_NONE, E.MEM_HOST)
-        return [hdrs[i] + outs[i][1][:outs[i][2]].tobytes() + bytes(arr[i].tag) for i in range(n)]
+        self.eng.seal_batch(self.algo, arr, n, E.CRC_GEN | E.CRC_CT if checksums else E.CRC_NONE, E.MEM_HOST)
+        objs = [hdrs[i] + outs[i][1][:outs[i][2]].tobytes() + bytes(arr[i].tag) for i in range(n)]
+        if not checksums:
+            return objs
+        return [(objs[i], str(self.eng.object_crc32c(hdrs[i], segs[i], outs[i][2], bytes(arr[i].tag))))
+                for i in range(n)]
 
-    def DecryptBatch(self, ciphertexts):
-        """Returns, per object, the plaintext or the exception Decrypt would raise."""
+    def DecryptBatch(self, ciphertexts, checksums=None):
+        """Returns, per object, the plaintext or the exception Decrypt would
+        raise.  checksums (optional, one decimal string or None per object) are
+        the object-store CRC32Cs to verify in the same pass; a mismatch yields
+        the store's "verify checksum failed" error (checksum.go:65)."""
         import numpy as np
+        from .checksum import ChecksumVerifyError
         res = [None] * len(ciphertexts)
-        specs, idx, bufs = [], [], []
+        specs, idx, bufs, segs = [], [], [], []
         for i, c in enumerate(ciphertexts):
             c = bytes(c)
             if len(c) < 3:
@@ -288,12 +304,24 @@ class DataEncryptor:
             dst = np.zeros(max(n, 1), np.uint8)
             bufs.append((src, dst, n))
             idx.append(i)
-            specs.append({"key": key, "nonce": nonce, "src": src.ctypes.data if n else None, "dst": dst.ctypes.data,
-                          "len": n, "tag": ct[n:]})
+            spec = {"key": key, "nonce": nonce, "src": src.ctypes.data if n else None, "dst": dst.ctypes.data,
+                    "len": n, "tag": ct[n:]}
+            if checksums is not None:
+                sb = np.zeros(4 * max(1, -(-n // (32 << 10))), np.uint8)
+                segs.append((sb, c[:3 + keyLen + nonceLen], checksums[i]))
+                spec["crc"] = sb.ctypes.data
+            specs.append(spec)
         if specs:
             arr, cnt = self.eng.make_blocks(specs)
-            self.eng.open_batch(self.algo, arr, cnt, E.CRC_NONE, E.MEM_HOST)
+            self.eng.open_batch(self.algo, arr, cnt, E.CRC_GEN | E.CRC_CT if checksums is not None else E.CRC_NONE,
+                                E.MEM_HOST)
             for k, i in enumerate(idx):
+                if checksums is not None and segs[k][2] not in (None, ""):
+                    sb, hdr, want = segs[k]
+                    got = self.eng.object_crc32c(hdr, sb, bufs[k][2], bytes(arr[k].tag))
+                    if got != (int(want) & 0xFFFFFFFF):  # the store's read fails before Decrypt
+                        res[i] = ChecksumVerifyError(got, int(want) & 0xFFFFFFFF)
+                        continue
                 if arr[k].status == E.ETAG:
                     res[i] = EncryptError(_ERR_OPEN[self.algo])
                 else:
@@ -353,12 +381,28 @@ class Encrypted:
     def String(self):
         return "%s(encrypted)" % self.store.String()
 
+    def _fused(self):
+        # a store that keeps the object CRC32C as metadata (checksum.ChecksumStorage,
+        # the S3/OSS/COS path): hash the stored bytes inside the Seal/Open pass
+        return getattr(self.store, "GetChecksum", None) is not None and not self.store.disableChecksum \
+            and hasattr(self.enc, "EncryptBatch")
+
     def Get(self, key, off=0, limit=-1):
-        ciphertext = self.store.Get(key, 0, -1)
-        try:
-            plain = self.enc.Decrypt(ciphertext)
-        except Exception as e:
-            raise EncryptError("Decrypt: %s" % e)
+        if self._fused() and self.store.GetChecksum(key) is not None:
+            ciphertext = self.store.inner.Get(key, 0, -1)
+            r = self.enc.DecryptBatch([ciphertext], [self.store.GetChecksum(key)])[0]
+            from .checksum import ChecksumVerifyError
+            if isinstance(r, ChecksumVerifyError):
+                raise r  # a read error of the store (io.ReadAll), not wrapped
+            if isinstance(r, Exception):
+                raise EncryptError("Decrypt: %s" % r)
+            plain = r
+        else:
+            ciphertext = self.store.Get(key, 0, -1)
+            try:
+                plain = self.enc.Decrypt(ciphertext)
+            except Exception as e:
+                raise EncryptError("Decrypt: %s" % e)
         n = len(plain)
         if off > n:
             off = n
@@ -367,7 +411,11 @@ class Encrypted:
         return plain[off:off + limit]
 
     def Put(self, key, data):
-        self.store.Put(key, self.enc.Encrypt(bytes(data)))
+        if self._fused():
+            obj, cs = self.enc.EncryptBatch([bytes(data)], checksums=True)[0]
+            self.store.Put(key, obj, checksum=cs)
+        else:
+            self.store.Put(key, self.enc.Encrypt(bytes(data)))
 
     def Delete(self, key):
         self.store.Delete(key)

@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("JFSX_LIB") or os.path.join(_HERE, "libjfsx.so")
 AES256GCM = 0
 CHACHA20P1305 = 1
 CRC_NONE, CRC_GEN, CRC_VERIFY = 0, 1, 2
+CRC_CT = 4  # flag: segment CRCs over the ciphertext (object checksum)
 MEM_DEVICE, MEM_HOST = 0, 1
 OK, ETAG, ECRC = 0, 1, 2
 EINVAL, ENODEV, EIO, ENOMEM, EMISFORMED = -22, -19, -5, -12, -74
@@ -28,7 +29,7 @@ EXPORTS = [
     "jfsx_free_pinned", "jfsx_alloc_device", "jfsx_free_device", "jfsx_memcpy_h2d", "jfsx_memcpy_d2h",
     "jfsx_seal_batch", "jfsx_open_batch", "jfsx_crc32c_segments", "jfsx_checksum", "jfsx_cache_verify",
     "jfsx_data_encrypt", "jfsx_data_decrypt", "jfsx_parse_header", "jfsx_gen_synthetic", "jfsx_gen_key",
-    "jfsx_debug_tables",
+    "jfsx_debug_tables", "jfsx_crc32c_update", "jfsx_crc32c_combine", "jfsx_object_crc32c",
 ]
 
 
@@ -92,8 +93,11 @@ def load_library(path=LIB_PATH):
             "jfsx_checksum": (I, [P, P, U64, P]),
             "jfsx_cache_verify": (I, [P, P, U64, U64, I, U64, U64, P, ctypes.POINTER(U64),
                                       ctypes.POINTER(U32), ctypes.POINTER(U32), ctypes.POINTER(ctypes.c_int64)]),
-            "jfsx_data_encrypt": (I, [P, I, P, P, P, I, P, U64, P, U64, ctypes.POINTER(U64)]),
-            "jfsx_data_decrypt": (I, [P, I, P, P, U64, P, U64, ctypes.POINTER(U64)]),
+            "jfsx_data_encrypt": (I, [P, I, P, P, P, I, P, U64, P, U64, ctypes.POINTER(U64), P]),
+            "jfsx_data_decrypt": (I, [P, I, P, P, U64, P, U64, ctypes.POINTER(U64), P, P]),
+            "jfsx_crc32c_update": (ctypes.c_uint32, [ctypes.c_uint32, P, U64]),
+            "jfsx_crc32c_combine": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, U64]),
+            "jfsx_object_crc32c": (I, [P, U64, P, U64, P, P]),
             "jfsx_parse_header": (I, [P, U64, ctypes.POINTER(I), ctypes.POINTER(I)]),
             "jfsx_gen_synthetic": (I, [P, P, U64, U64, U64]),
             "jfsx_gen_key": (None, [U64, U64, P, P]),
@@ -322,25 +326,69 @@ class Engine:
             raise EngineError(rc, "jfsx_cache_verify")
         return rc, out[:size].tobytes(), n.value, got.value, exp.value, seg.value
 
-    def data_encrypt(self, algo, key, nonce, wrapped, plaintext):
+    def data_encrypt(self, algo, key, nonce, wrapped, plaintext, obj_crc=False):
+        """Object bytes (encrypt.go:182-193); with obj_crc=True also the
+        object-store checksum of them (checksum.go:31-53): (obj, crc)."""
         p = _u8(plaintext)
         cap = 3 + len(wrapped) + 12 + p.size + 16
         out = np.empty(cap, np.uint8)
         w = _u8(wrapped)
         olen = ctypes.c_uint64()
+        crc = ctypes.c_uint32()
         self._check(self.L.jfsx_data_encrypt(self.ctx, algo, bytes(key), bytes(nonce),
                                              w.ctypes.data if w.size else None, w.size,
                                              p.ctypes.data if p.size else None, p.size, out.ctypes.data, cap,
-                                             ctypes.byref(olen)), "jfsx_data_encrypt")
-        return out[:olen.value].tobytes()
+                                             ctypes.byref(olen), ctypes.byref(crc) if obj_crc else None),
+                    "jfsx_data_encrypt")
+        obj = out[:olen.value].tobytes()
+        return (obj, crc.value) if obj_crc else obj
 
-    def data_decrypt(self, algo, key, obj):
+    def data_decrypt(self, algo, key, obj, expect_crc=None):
+        """(rc, plaintext) -- rc JFSX_ECRC when expect_crc is given and the
+        object checksum differs; then .last_got_crc holds the computed value."""
         o = _u8(obj)
         out = np.empty(max(o.size, 1), np.uint8)
         olen = ctypes.c_uint64()
+        exp = ctypes.c_uint32(expect_crc or 0)
+        got = ctypes.c_uint32()
         rc = self.L.jfsx_data_decrypt(self.ctx, algo, bytes(key), o.ctypes.data, o.size, out.ctypes.data,
-                                      out.size, ctypes.byref(olen))
+                                      out.size, ctypes.byref(olen),
+                                      ctypes.byref(exp) if expect_crc is not None else None,
+                                      ctypes.byref(got) if expect_crc is not None else None)
+        self.last_got_crc = got.value
         return rc, out[:olen.value].tobytes() if rc == 0 else b""
+
+    def crc32c_update(self, crc, data):
+        return crc32c_update(crc, data)
+
+    def crc32c_combine(self, a, b, len_b):
+        return crc32c_combine(a, b, len_b)
+
+    def object_crc32c(self, hdr, seg_crcs, clen, tag):
+        return object_crc32c(hdr, seg_crcs, clen, tag)
+
+
+# host-side CRC32C helpers of the C-ABI (no device needed)
+def crc32c_update(crc, data):
+    """crc32.Update(crc, MakeTable(Castagnoli), data)."""
+    d = _u8(data)
+    return load_library().jfsx_crc32c_update(crc, d.ctypes.data if d.size else None, d.size)
+
+
+def crc32c_combine(a, b, len_b):
+    return load_library().jfsx_crc32c_combine(a, b, len_b)
+
+
+def object_crc32c(hdr, seg_crcs, clen, tag):
+    """generateChecksum's value of hdr || C || tag from C's BE segment CRCs."""
+    h, sc = _u8(hdr), _u8(seg_crcs)
+    out = ctypes.c_uint32()
+    rc = load_library().jfsx_object_crc32c(h.ctypes.data if h.size else None, h.size,
+                                           sc.ctypes.data if sc.size else None, clen, bytes(tag),
+                                           ctypes.byref(out))
+    if rc:
+        raise EngineError(rc, "jfsx_object_crc32c")
+    return out.value
 
 
 class ChecksumError(Exception):

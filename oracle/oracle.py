@@ -107,6 +107,12 @@ def checksum(data, hw=False):
     return out.tobytes()
 
 
+def object_checksum(obj, hw=False):
+    """generateChecksum (pkg/object/checksum.go:31-53): crc32.Update(0,
+    Castagnoli, whole stored object) as a decimal string."""
+    return str(crc32c(obj, 0, hw))
+
+
 def open_cache_file(file_size, length, level):
     return lib().orc_open_cache_file(file_size, length, LEVELS.get(level, level))
 
