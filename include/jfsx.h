@@ -113,7 +113,11 @@ typedef struct jfsx_range {
 int jfsx_abi_version(void);
 int jfsx_device_count(int *n);
 
-/* context = one GPU + one HIP stream + device workspace + pinned staging */
+/* context = one GPU + one HIP stream + device workspace + pinned staging.
+ * flags: 0, or JFSX_CTX_BITSLICE: AES-256-GCM computes the keystream of whole
+ * 32 KiB segments with the bitsliced AES on the VALU instead of the T-table
+ * AES in LDS (same bytes; a throughput trade-off). */
+#define JFSX_CTX_BITSLICE 1u
 int jfsx_ctx_open(int device, uint32_t flags, jfsx_ctx **out);
 int jfsx_ctx_close(jfsx_ctx *ctx);
 int jfsx_ctx_sync(jfsx_ctx *ctx);

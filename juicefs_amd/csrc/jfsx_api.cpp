@@ -146,6 +146,7 @@ struct jfsx_ctx {
     hipEvent_t ev_k0[kRing] = {}, ev_k1[kRing] = {};  // main-kernel timing per slot
     size_t slot_bytes = (size_t)256 << 20;
     bool timing = false;
+    bool bitslice = false;  // JFSX_CTX_BITSLICE
     double ms_total = 0;
     uint64_t launches = 0;
 };
@@ -303,7 +304,7 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, int k, int algo, bool
         GcmSched *dsch = (GcmSched *)(d + o_sched);
         launch_gcm_keysetup(s, n, dk, db, dsch, c->tabs);
         if (c->timing) HIP_OK(hipEventRecord(c->ev_k0[k], s));
-        launch_gcm_main(s, (int)nt, open, crc_mode, dt, db, dsch, dpart, dpexp, c->tabs);
+        launch_gcm_main(s, (int)nt, open, crc_mode, c->bitslice, dt, db, dsch, dpart, dpexp, c->tabs);
         if (c->timing) HIP_OK(hipEventRecord(c->ev_k1[k], s));
         launch_gcm_finalize(s, n, open, crc_mode, db, dsch, dpart, dpexp, dout);
     } else {
@@ -592,14 +593,14 @@ int jfsx_device_count(int *n) {
 }
 
 int jfsx_ctx_open(int device, uint32_t flags, jfsx_ctx **out) {
-    (void)flags;
-    if (!out) return JFSX_EINVAL;
+    if (!out || (flags & ~JFSX_CTX_BITSLICE)) return JFSX_EINVAL;
     *out = nullptr;
     int nd = 0;
     if (hipGetDeviceCount(&nd) != hipSuccess || device < 0 || device >= nd) return JFSX_ENODEV;
     HIP_OK(hipSetDevice(device));
     jfsx_ctx *c = new jfsx_ctx();
     c->device = device;
+    c->bitslice = (flags & JFSX_CTX_BITSLICE) != 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) != hipSuccess) {

@@ -294,7 +294,7 @@ __global__ __launch_bounds__(kCpWaves * 64) void cp_main_k(const Task *__restric
         const uint64_t o = sub0 + 4096 * r + lo;
         uint4 d[4];
 #pragma unroll
-        for (int q = 0; q < 4; q++) d[q] = *reinterpret_cast<const uint4 *>(src + o + 16 * q);
+        for (int q = 0; q < 4; q++) d[q] = gld16(src + o + 16 * q);
         uint32_t ks[16];
         chacha_block(key, nonce, (uint32_t)(o / 64 + 1), ks);
 #pragma unroll
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(kCpWaves * 64) void cp_main_k(const Task *__restric
             const uint4 x = make_uint4(d[q].x ^ ks[4 * q], d[q].y ^ ks[4 * q + 1], d[q].z ^ ks[4 * q + 2],
                                        d[q].w ^ ks[4 * q + 3]);
             const uint4 c = OPEN ? d[q] : x, p = OPEN ? x : d[q];
-            *reinterpret_cast<uint4 *>(dst + o + 16 * q) = OPEN ? p : c;
+            gst16(dst + o + 16 * q, OPEN ? p : c);
             const uint4 cq = crc_src<CRCMODE>(c, p);
             st.A = p_add(p_mul(st.A, q == 0 ? r253 : r1), p_from_words(c.x, c.y, c.z, c.w, 1));
             if (CRCMODE) {

@@ -47,9 +47,23 @@ __device__ __noinline__ uint32_t crc_partial(const char *lds, uint32_t A, const 
     return c;
 }
 
+// 16-byte global load / store through an address_space(1) pointer: global_*
+// instead of flat_* (flat ops count in both vmcnt and lgkmcnt, so every LDS
+// wait would also wait for the outstanding HBM traffic).
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) v4u gv4u;
+__device__ __forceinline__ uint4 gld16(const uint8_t *p) {
+    const v4u v = *(const gv4u *)(p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void gst16(uint8_t *p, uint4 v) {
+    v4u w = {v.x, v.y, v.z, v.w};
+    *(gv4u *)(p) = w;
+}
+
 // guarded 16-byte load of [o, o+16) clipped at end (zero fill)
 __device__ __forceinline__ uint4 load_piece(const uint8_t *src, uint64_t o, uint64_t end) {
-    if (o + 16 <= end) return *reinterpret_cast<const uint4 *>(src + o);
+    if (o + 16 <= end) return gld16(src + o);
     uint32_t w[4] = {0, 0, 0, 0};
     for (uint64_t i = o; i < end && i < o + 16; i++) w[(i - o) >> 2] |= (uint32_t)src[i] << (8 * ((i - o) & 3));
     return make_uint4(w[0], w[1], w[2], w[3]);
@@ -57,7 +71,7 @@ __device__ __forceinline__ uint4 load_piece(const uint8_t *src, uint64_t o, uint
 
 __device__ __forceinline__ void store_piece(uint8_t *dst, uint64_t o, uint64_t end, uint4 v) {
     if (o + 16 <= end) {
-        *reinterpret_cast<uint4 *>(dst + o) = v;
+        gst16(dst + o, v);
         return;
     }
     uint32_t w[4] = {v.x, v.y, v.z, v.w};

@@ -24,6 +24,16 @@
 //     compares the tag; in VERIFY compares CRCs (first failing segment).
 #include "jfsx_dev.h"
 
+#define JFSX_HD __device__ __forceinline__
+#define BS3(a, b, c, tt) __builtin_amdgcn_bitop3_b32((a), (b), (c), (tt))
+#define PERM(hi, lo, sel) __builtin_amdgcn_perm((hi), (lo), (sel))
+#define OPAQUE(x)                                 \
+    do {                                          \
+        (x) = __builtin_amdgcn_readfirstlane(x);  \
+        asm volatile("" : "+s"(x));               \
+    } while (0)
+#include "jfsx_aes_bs.h"
+
 namespace jfsx {
 
 // ---------------------------------------------------------------------------
@@ -147,7 +157,20 @@ __device__ __forceinline__ void gh_rho_inv(const uint32_t R[4], const GhLane &g,
 
 // One Horner step in the rotated frame: R <- rho(unrho(R) * H^64 ^ c)
 __device__ __forceinline__ void ghash_step(const char *lds, uint32_t R[4], const GhLane &g, uint4 c) {
-#if JFSX_GH8
+#if JFSX_GH8 == 4
+    // four quarters of 4 lookups each: at most 16 VGPRs of table entries in flight
+    uint32_t S[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+    for (int h = 0; h < 4; h++) {
+        uint4 t[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) t[q] = lds_u4(lds, kLdsGh + __builtin_amdgcn_perm(R[h], g.off[h], g.sel[q]));
+#define GX(f, i) S[i] = xor3(xor3(t[0].f, t[1].f, t[2].f), t[3].f, S[i])
+        GX(x, 0); GX(y, 1); GX(z, 2); GX(w, 3);
+#undef GX
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#elif JFSX_GH8
     // two halves of 8 lookups each: at most 32 VGPRs of table entries in flight
     uint32_t S[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
@@ -272,8 +295,17 @@ __device__ __noinline__ Stream row_generic(const char *lds, uint32_t loff, const
 }
 
 // gcm_main: one workgroup per task; each wave runs NS streams in lock-step.
-template <bool OPEN, int CRCMODE, int NS>
-__global__ __launch_bounds__(kThreads) void gcm_main_k(const Task *__restrict__ tasks,
+// BS = 0: T-table AES in LDS, 16 waves (4/SIMD, <= 128 VGPRs).
+// BS = 1: whole 32 KiB segments use the bitsliced AES on the VALU
+//         (jfsx_aes_bs.h; 128 VGPRs of state), 8 waves (2/SIMD, <= 256 VGPRs).
+template <int BS>
+struct GcmShape {
+    static constexpr uint32_t waves = BS ? 8u : (uint32_t)kWaves;
+    static constexpr uint32_t threads = waves * 64u;
+};
+
+template <bool OPEN, int CRCMODE, int NS, int BS>
+__global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *__restrict__ tasks,
                                                        const BlkDev *__restrict__ blks,
                                                        const GcmSched *__restrict__ sched,
                                                        uint32_t *__restrict__ partial, uint32_t *__restrict__ pexp,
@@ -288,11 +320,11 @@ __global__ __launch_bounds__(kThreads) void gcm_main_k(const Task *__restrict__ 
     {
         const uint4 *ga = reinterpret_cast<const uint4 *>(tab.aes);
         uint4 *la = reinterpret_cast<uint4 *>(lds + kLdsAes);
-        for (uint32_t i = tid; i < 4096; i += kThreads) la[i] = ga[i];
+        for (uint32_t i = tid; i < 4096; i += GcmShape<BS>::threads) la[i] = ga[i];
         if (CRCMODE) {
             const uint4 *gc = reinterpret_cast<const uint4 *>(tab.crc);
             uint4 *lc = reinterpret_cast<uint4 *>(lds + kLdsCrc);
-            for (uint32_t i = tid; i < 1280; i += kThreads) lc[i] = gc[i];
+            for (uint32_t i = tid; i < 1280; i += GcmShape<BS>::threads) lc[i] = gc[i];
         }
         if (tid < 128)
             reinterpret_cast<uint4 *>(lds + kLdsBasis)[tid] = reinterpret_cast<const uint4 *>(sch->basis)[tid];
@@ -301,7 +333,7 @@ __global__ __launch_bounds__(kThreads) void gcm_main_k(const Task *__restrict__ 
     {
         uint4 *lg = reinterpret_cast<uint4 *>(lds + kLdsGh);
         const uint4 *lb = reinterpret_cast<const uint4 *>(lds + kLdsBasis);
-        for (uint32_t e = tid; e < 4096; e += kThreads) {
+        for (uint32_t e = tid; e < 4096; e += GcmShape<BS>::threads) {
             uint32_t b = e >> 4, j = e & 15;  // entry (b, j) at byte (b << 8) | (j << 4)
             uint4 z = make_uint4(0, 0, 0, 0);
 #pragma unroll
@@ -316,18 +348,13 @@ __global__ __launch_bounds__(kThreads) void gcm_main_k(const Task *__restrict__ 
     }
     __syncthreads();
 
-    uint32_t rk[60];
-#pragma unroll
-    for (int i = 0; i < 60; i++) rk[i] = sch->rk[i];
-    uint32_t k1[4] = {sch->k1[0], sch->k1[1], sch->k1[2], sch->k1[3]};
-
-    const uint32_t wave = tid >> 6, lane = tid & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;  // wave index in an SGPR
     const uint32_t loff = ((lane & 31) << 2) | 0x00010000u;  // AES replica offset | table base
     const GhLane gl = gh_lane(lane);
     const uint32_t xl = CRCMODE ? tab.crcx[lane] : 0u;
     const uint64_t c0 = task.c0, c1 = task.c1;
     const uint32_t nseg = (uint32_t)((c1 - c0 + kSeg - 1) / kSeg);
-    constexpr uint32_t V = kWaves * NS;  // virtual waves (streams) per task
+    constexpr uint32_t V = GcmShape<BS>::waves * NS;  // virtual waves (streams) per task
 
     Stream st[NS];
 #pragma unroll
@@ -362,23 +389,68 @@ __global__ __launch_bounds__(kThreads) void gcm_main_k(const Task *__restrict__ 
     uint8_t *dst = blk.dst;
     const uint64_t lo = 16 * lane;
 
+    uint64_t r0 = 0;
+    // BS: whole 32 KiB segments take their 32 rows of keystream from one
+    // bitsliced AES pass (lane slot k = row k), then the rows stream through
+    // XOR / store / GHASH / CRC with the keystream in registers.
+    if (BS && NS == 1 && act[0] && rf >= 32) {
+        const uint64_t nfs = rf / 32;
+        const uint32_t nrk[3] = {sch->c012[0], sch->c012[1], sch->c012[2]};
+        const uint32_t rk3 = sch->rk[3];
+        constexpr int PF = 4;  // rows of loads in flight
+        uint4 pf[PF];
+#pragma unroll
+        for (int q = 0; q < PF; q++) pf[q] = gld16(src + ld0[0] + 1024 * q + lo);
+        for (uint64_t sg = 0; sg < nfs; sg++) {
+            const uint64_t base = ld0[0] + (uint64_t)kSeg * sg;
+            uint32_t ks[128];
+            jfsx_bs::ctr32(ks, nrk, rk3, (uint32_t)((base >> 4) + lane + 2),
+                           [&](int r, int w) { return sch->bsu[r][w]; }, sch->r1c);
+            const bool more = sg + 1 < nfs;
+#pragma unroll
+            for (int k = 0; k < 32; k++) {
+                const uint4 d = pf[k % PF];
+                const uint64_t o = base + 1024 * k + lo;
+                if (k + PF < 32 || more) pf[k % PF] = gld16(src + o + 1024 * PF);
+                const uint4 x = make_uint4(d.x ^ ks[k], d.y ^ ks[32 + k], d.z ^ ks[64 + k], d.w ^ ks[96 + k]);
+                const uint4 c = OPEN ? d : x, p = OPEN ? x : d;
+                gst16(dst + o, OPEN ? p : c);
+                const uint4 cq = crc_src<CRCMODE>(c, p);
+#ifndef JFSX_ABLATE_GHASH
+                ghash_step(lds, st[0].acc, gl, c);
+#endif
+                if (CRCMODE) st[0].A = crc_piece<kLdsCrc>(lds, st[0].A, cq.x, cq.y, cq.z, cq.w);
+            }
+            if (CRCMODE) {
+                crc_segment_end<CRCMODE>(blk, tab, lane, xl, st[0].seg0, st[0].seg0 + kSeg, st[0].A, 0);
+                st[0].A = 0;
+                st[0].seg0 += kSeg;
+            }
+        }
+        r0 = 32 * nfs;
+    }
+    // T-table AES (LDS) for the rows outside whole segments; the schedule is
+    // read here, after the bitsliced loop, so it holds no SGPRs through it
+    uint32_t rk[60];
+#pragma unroll
+    for (int i = 0; i < 60; i++) rk[i] = sch->rk[i];
+    uint32_t k1[4] = {sch->k1[0], sch->k1[1], sch->k1[2], sch->k1[3]};
     uint4 nxt[NS];
 #pragma unroll
     for (int s = 0; s < NS; s++)
-        nxt[s] = rf ? *reinterpret_cast<const uint4 *>(src + ld0[s] + lo) : make_uint4(0, 0, 0, 0);
-    uint64_t r0 = 0;
+        nxt[s] = r0 < rf ? gld16(src + ld0[s] + 1024 * r0 + lo) : make_uint4(0, 0, 0, 0);
 #if JFSX_U2
     // two rows of one stream per iteration: the two AES chains interleave,
     // GHASH/CRC stay sequential (register peak of one row)
-    if (NS == 1 && act[0] && rf >= 2) {
-        uint4 n0 = *reinterpret_cast<const uint4 *>(src + ld0[0] + lo);
-        uint4 n1 = *reinterpret_cast<const uint4 *>(src + ld0[0] + 1024 + lo);
+    if (NS == 1 && act[0] && rf >= r0 + 2) {
+        uint4 n0 = gld16(src + ld0[0] + 1024 * r0 + lo);
+        uint4 n1 = gld16(src + ld0[0] + 1024 * (r0 + 1) + lo);
         for (; r0 + 1 < rf; r0 += 2) {
             const uint4 dd[2] = {n0, n1};
             const uint64_t o0 = ld0[0] + 1024 * r0 + lo;
             if (r0 + 3 < rf) {
-                n0 = *reinterpret_cast<const uint4 *>(src + o0 + 2048);
-                n1 = *reinterpret_cast<const uint4 *>(src + o0 + 3072);
+                n0 = gld16(src + o0 + 2048);
+                n1 = gld16(src + o0 + 3072);
             }
             const uint32_t ctr2[2] = {(uint32_t)((o0 >> 4) + 2), (uint32_t)((o0 >> 4) + 66)};
             uint32_t ks2[2][4];
@@ -389,7 +461,7 @@ __global__ __launch_bounds__(kThreads) void gcm_main_k(const Task *__restrict__ 
                 const uint4 x = make_uint4(dd[u].x ^ ks2[u][0], dd[u].y ^ ks2[u][1], dd[u].z ^ ks2[u][2],
                                            dd[u].w ^ ks2[u][3]);
                 const uint4 c = OPEN ? dd[u] : x, p = OPEN ? x : dd[u];
-                *reinterpret_cast<uint4 *>(dst + o) = OPEN ? p : c;
+                gst16(dst + o, OPEN ? p : c);
                 const uint4 cq = crc_src<CRCMODE>(c, p);
                 ghash_step(lds, st[0].acc, gl, c);
                 if (CRCMODE) st[0].A = crc_piece<kLdsCrc>(lds, st[0].A, cq.x, cq.y, cq.z, cq.w);
@@ -400,7 +472,7 @@ __global__ __launch_bounds__(kThreads) void gcm_main_k(const Task *__restrict__ 
                 }
             }
         }
-        if (r0 < rf) nxt[0] = *reinterpret_cast<const uint4 *>(src + ld0[0] + 1024 * r0 + lo);
+        if (r0 < rf) nxt[0] = gld16(src + ld0[0] + 1024 * r0 + lo);
     }
 #endif
     for (uint64_t r = r0; r < rf; r++) {
@@ -410,7 +482,7 @@ __global__ __launch_bounds__(kThreads) void gcm_main_k(const Task *__restrict__ 
         for (int s = 0; s < NS; s++) {
             d[s] = nxt[s];
             const uint64_t o = ld0[s] + 1024 * r + lo;
-            if (r + 1 < rf) nxt[s] = *reinterpret_cast<const uint4 *>(src + o + 1024);
+            if (r + 1 < rf) nxt[s] = gld16(src + o + 1024);
             ctr[s] = (uint32_t)((o >> 4) + 2);
         }
         uint32_t ks[NS][4];
@@ -421,7 +493,7 @@ __global__ __launch_bounds__(kThreads) void gcm_main_k(const Task *__restrict__ 
             const uint64_t o = st[s].sub0 + 1024 * r + lo;
             const uint4 x = make_uint4(d[s].x ^ ks[s][0], d[s].y ^ ks[s][1], d[s].z ^ ks[s][2], d[s].w ^ ks[s][3]);
             const uint4 c = OPEN ? d[s] : x, p = OPEN ? x : d[s];
-            *reinterpret_cast<uint4 *>(dst + o) = OPEN ? p : c;
+            gst16(dst + o, OPEN ? p : c);
             const uint4 cq = crc_src<CRCMODE>(c, p);
             ghash_step(lds, st[s].acc, gl, c);
             if (CRCMODE) st[s].A = crc_piece<kLdsCrc>(lds, st[s].A, cq.x, cq.y, cq.z, cq.w);
@@ -476,6 +548,13 @@ __global__ __launch_bounds__(kThreads) void gcm_main_k(const Task *__restrict__ 
             partial[4 * slot + 2] = zm[2];
             partial[4 * slot + 3] = zm[3];
             pexp[slot] = (uint32_t)(nblk - wend);
+            // the 8-wave bitsliced shape leaves the upper half of the task's
+            // kSlotsPerTask slots unused: zero them for gcm_finalize
+            for (uint32_t u = task.slot0 + GcmShape<BS>::waves * NS + wave * NS + s; u < task.slot0 + kSlotsPerTask;
+                 u += GcmShape<BS>::waves * NS) {
+                partial[4 * u + 0] = partial[4 * u + 1] = partial[4 * u + 2] = partial[4 * u + 3] = 0;
+                pexp[u] = 0;
+            }
         }
     }
 }
@@ -530,6 +609,20 @@ __global__ __launch_bounds__(64) void gcm_keysetup_k(const KeyIn *__restrict__ k
         w[i] = w[i - 8] ^ t;
     }
     if (lane < 60) sc->rk[lane] = w[lane];
+    {
+        // bitsliced-AES masks: lane 4(r-1) + w computes dword w of u_r
+        const uint32_t my = lane < 56 ? jfsx_bs::round_mask_word(w, 1 + (int)(lane >> 2), (int)(lane & 3)) : 0u;
+        if (lane < 56) sc->bsu[1 + (lane >> 2)][lane & 3] = my;
+        // round-1 constants: S-boxes of the 12 nonce bytes (lanes 0..11), then
+        // MixColumns of each column's uniform part (lanes 0..3)
+        const uint32_t x0w[3] = {k.nonce[0] ^ w[0], k.nonce[1] ^ w[1], k.nonce[2] ^ w[2]};
+        const uint32_t sb = lane < 12 ? jfsx_bs::sbox_byte((x0w[lane >> 2] >> (8 * (lane & 3))) & 0xffu) : 0u;
+        uint32_t sbn[12];
+        for (int i = 0; i < 12; i++) sbn[i] = (uint32_t)__shfl(sb, i, 64);
+        const uint32_t u1[4] = {(uint32_t)__shfl(my, 0, 64), (uint32_t)__shfl(my, 1, 64), (uint32_t)__shfl(my, 2, 64),
+                                (uint32_t)__shfl(my, 3, 64)};
+        if (lane < 4) sc->r1c[lane] = jfsx_bs::round1_const(sbn, u1, (int)lane);
+    }
     // round-0 state of the counter blocks (nonce || ctr) and round-1 constants
     const uint32_t x0 = k.nonce[0] ^ w[0], x1 = k.nonce[1] ^ w[1], x2 = k.nonce[2] ^ w[2];
     if (lane == 0) {
@@ -641,11 +734,18 @@ void launch_gcm_keysetup(hipStream_t s, int n, const KeyIn *keys, const BlkDev *
     if (n > 0) hipLaunchKernelGGL(gcm_keysetup_k, dim3(n), dim3(64), 0, s, keys, blks, sched, t.aes);
 }
 
-void launch_gcm_main(hipStream_t s, int ntasks, bool open, int crc_mode, const Task *tasks, const BlkDev *blks,
-                     const GcmSched *sched, uint32_t *partial, uint32_t *pexp, DevTables t) {
+void launch_gcm_main(hipStream_t s, int ntasks, bool open, int crc_mode, bool bitslice, const Task *tasks,
+                     const BlkDev *blks, const GcmSched *sched, uint32_t *partial, uint32_t *pexp, DevTables t) {
     if (ntasks <= 0) return;
-    dim3 g(ntasks), bl(kThreads);
-#define L(O, C) hipLaunchKernelGGL((gcm_main_k<O, C, kStreams>), g, bl, 0, s, tasks, blks, sched, partial, pexp, t)
+#define L(O, C)                                                                                              \
+    do {                                                                                                     \
+        if (bitslice)                                                                                        \
+            hipLaunchKernelGGL((gcm_main_k<O, C, 1, 1>), dim3(ntasks), dim3(GcmShape<1>::threads), 0, s, tasks, \
+                               blks, sched, partial, pexp, t);                                               \
+        else                                                                                                 \
+            hipLaunchKernelGGL((gcm_main_k<O, C, kStreams, 0>), dim3(ntasks), dim3(GcmShape<0>::threads), 0, s, \
+                               tasks, blks, sched, partial, pexp, t);                                        \
+    } while (0)
     switch ((open ? 8 : 0) | crc_mode) {
         case 8: L(true, 0); break;
         case 9: L(true, 1); break;

@@ -25,14 +25,16 @@ constexpr int kThreads = kWaves * 64;
 #ifndef JFSX_STREAMS
 #define JFSX_STREAMS 1
 #endif
-// GHASH table walk issued as two halves of 8 lookups with a scheduling fence
-// between them (lower peak VGPRs; measured +3% on the GCM seal kernel).
+// GHASH table walk issued in groups of lookups with a scheduling fence between
+// them (lower peak VGPRs): 4 = four quarters of 4 (default), 1 = two halves of
+// 8, 0 = all 16 at once.
 #ifndef JFSX_GH8
-#define JFSX_GH8 1
+#define JFSX_GH8 4
 #endif
-// Two-row unrolled fast loop (spills at the 128-VGPR cap when combined with GH8).
+// Two-row unrolled T-table loop (two AES chains interleaved); with the GHASH
+// quarters it fits the 128-VGPR cap (+2% measured).
 #ifndef JFSX_U2
-#define JFSX_U2 0
+#define JFSX_U2 1
 #endif
 constexpr int kStreams = JFSX_STREAMS;         // independent segment streams per wave (ILP)
 constexpr int kSlotsPerTask = kWaves * kStreams;  // GHASH/Poly partial slots per task
@@ -79,6 +81,8 @@ struct GcmSched {
     uint32_t basis[128][4];  // x^i * H^64, memory order
     uint32_t hpow[68][4];    // H^k, memory order (k = 0..67)
     uint32_t h2k[32][4];     // H^(2^k), memory order
+    uint32_t bsu[16][4];     // bitsliced-AES S-box output masks of rounds 1..14 (jfsx_aes_bs.h)
+    uint32_t r1c[4];         // CTR round-1 constants of the 32-slot layout (round1_const)
 };
 
 // per-key ChaCha20-Poly1305 schedule (Poly1305 values in 26-bit limbs)
@@ -220,8 +224,8 @@ struct DevTables {
 };
 void launch_gcm_keysetup(hipStream_t s, int n, const KeyIn *keys, const BlkDev *blks, GcmSched *sched,
                          DevTables t);
-void launch_gcm_main(hipStream_t s, int ntasks, bool open, int crc_mode, const Task *tasks, const BlkDev *blks,
-                     const GcmSched *sched, uint32_t *partial, uint32_t *pexp, DevTables t);
+void launch_gcm_main(hipStream_t s, int ntasks, bool open, int crc_mode, bool bitslice, const Task *tasks,
+                     const BlkDev *blks, const GcmSched *sched, uint32_t *partial, uint32_t *pexp, DevTables t);
 void launch_gcm_finalize(hipStream_t s, int n, bool open, int crc_mode, const BlkDev *blks, const GcmSched *sched,
                          const uint32_t *partial, const uint32_t *pexp, BlkOut *out);
 void launch_cp_keysetup(hipStream_t s, int n, const KeyIn *keys, const BlkDev *blks, CpSched *sched);

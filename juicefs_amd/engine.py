@@ -17,6 +17,7 @@ AES256GCM = 0
 CHACHA20P1305 = 1
 CRC_NONE, CRC_GEN, CRC_VERIFY = 0, 1, 2
 CRC_CT = 4  # flag: segment CRCs over the ciphertext (object checksum)
+CTX_BITSLICE = 1  # context flag: AES-GCM keystream from the bitsliced AES (VALU)
 MEM_DEVICE, MEM_HOST = 0, 1
 OK, ETAG, ECRC = 0, 1, 2
 EINVAL, ENODEV, EIO, ENOMEM, EMISFORMED = -22, -19, -5, -12, -74
@@ -192,12 +193,13 @@ class DeviceBuffer:
 class Engine:
     """One GPU context (device ordinal + HIP stream + workspace)."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, flags=0):
+        """flags: 0 or CTX_BITSLICE (AES-GCM keystream from the bitsliced AES)."""
         self.L = load_library()
         if device_count() <= device:
             raise RuntimeError("jfsx: no HIP device %d visible (the engine has no CPU path)" % device)
         ctx = ctypes.c_void_p()
-        rc = self.L.jfsx_ctx_open(device, 0, ctypes.byref(ctx))
+        rc = self.L.jfsx_ctx_open(device, flags, ctypes.byref(ctx))
         if rc:
             raise EngineError(rc, "jfsx_ctx_open(%d)" % device)
         self.ctx = ctx.value

@@ -16,9 +16,11 @@ ALGOS = {"aes256gcm": E.AES256GCM, "chacha20poly1305": E.CHACHA20P1305}
 ORC = {E.AES256GCM: orc.AES256GCM, E.CHACHA20P1305: orc.CHACHA20P1305}
 
 
-@pytest.fixture(scope="module")
-def eng():
-    e = E.Engine(0)
+@pytest.fixture(scope="module", params=["ttable", "bitslice"])
+def eng(request):
+    """Every parity case runs on both AES-GCM keystream kernels (T-table in LDS
+    and the bitsliced VALU AES; the ChaCha path ignores the flag)."""
+    e = E.Engine(0, E.CTX_BITSLICE if request.param == "bitslice" else 0)
     yield e
     e.close()
 
