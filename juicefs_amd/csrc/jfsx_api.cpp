@@ -127,6 +127,7 @@ struct Workspace {
     size_t scap = 0;
     int n = 0;              // blocks of the batch in flight
     uint64_t nt = 0;        // tasks of the batch in flight
+    const void *dout = nullptr;  // device BlkOut[n] of the batch in flight
 };
 
 constexpr int kRing = 3;  // host-ingest pipeline depth (H2D | transform | D2H)
@@ -233,8 +234,14 @@ int check_aead_args(int algo, int n, const jfsx_blk *blks, int crc_mode, bool de
 // Enqueue keysetup -> transform -> finalize -> result copy for n device-resident
 // blocks on stream s, using workspace w.  Results land in w.h (BlkOut[n]) once
 // the stream reaches that point; finish_aead() copies them into blks.
+// Stages the batch's metadata and enqueues keysetup / main / finalize on s.
+// Host ingest passes up = (s_in, ev): the metadata upload then rides the
+// upload stream behind the data, ev is recorded there and s waits on it; with
+// collect = false the caller downloads the BlkOut results on its own stream.
+// The compute stream then carries kernels only, so the H2D and D2H DMA of
+// neighbouring slots run concurrently (full duplex).
 int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, int k, int algo, bool open, int n, const jfsx_blk *blks,
-                 int crc_mode) {
+                 int crc_mode, hipStream_t up = nullptr, hipEvent_t up_ev = nullptr, bool collect = true) {
     const bool gcm = algo == JFSX_AES256GCM;
     std::vector<uint64_t> lens(n);
     uint64_t crc_calc_words = 0;
@@ -290,7 +297,13 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, int k, int algo, bool
         bd.nslots += slots;
     }
     if (nt) memcpy(h + o_task, plan.tasks.data(), sizeof(Task) * nt);
-    HIP_OK(hipMemcpyAsync(d, h, h_bytes, hipMemcpyHostToDevice, s));
+    if (up) {
+        HIP_OK(hipMemcpyAsync(d, h, h_bytes, hipMemcpyHostToDevice, up));
+        HIP_OK(hipEventRecord(up_ev, up));
+        HIP_OK(hipStreamWaitEvent(s, up_ev, 0));
+    } else {
+        HIP_OK(hipMemcpyAsync(d, h, h_bytes, hipMemcpyHostToDevice, s));
+    }
     if ((crc_mode & 3) == JFSX_CRC_GEN)
         for (int i = 0; i < n; i++)
             if (blks[i].len == 0) HIP_OK(hipMemsetAsync(blks[i].crc, 0, 4, s));
@@ -316,7 +329,8 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, int k, int algo, bool
         launch_cp_finalize(s, n, open, crc_mode, db, dsch, dpart, dpexp, dout);
     }
     HIP_OK(hipGetLastError());
-    HIP_OK(hipMemcpyAsync(h, dout, sizeof(BlkOut) * n, hipMemcpyDeviceToHost, s));
+    w.dout = dout;
+    if (collect) HIP_OK(hipMemcpyAsync(h, dout, sizeof(BlkOut) * n, hipMemcpyDeviceToHost, s));
     w.n = n;
     w.nt = nt;
     return 0;
@@ -433,9 +447,9 @@ int run_aead_host(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int c
             }
         }
         if ((rc = flush_in())) return rc;
-        HIP_OK(hipEventRecord(c->ev_in[k], c->s_in));
-        HIP_OK(hipStreamWaitEvent(c->stream, c->ev_in[k], 0));
-        if ((rc = enqueue_aead(c, w, c->stream, k, algo, open, b1 - b0, dv.data() + b0, crc_mode))) return rc;
+        if ((rc = enqueue_aead(c, w, c->stream, k, algo, open, b1 - b0, dv.data() + b0, crc_mode, c->s_in, c->ev_in[k],
+                               false)))
+            return rc;
         HIP_OK(hipEventRecord(c->ev_comp[k], c->stream));
         HIP_OK(hipStreamWaitEvent(c->s_out, c->ev_comp[k], 0));
         {
@@ -460,10 +474,23 @@ int run_aead_host(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int c
                 if (align256(blks[i].len) != blks[i].len && (rc = flush_out())) return rc;
             }
             if ((rc = flush_out())) return rc;
-            if ((crc_mode & 3) == JFSX_CRC_GEN)
-                for (int i = b0; i < b1; i++)
-                    HIP_OK(hipMemcpyAsync(blks[i].crc, dv[i].crc, 4 * nseg_of(blks[i].len), hipMemcpyDeviceToHost,
-                                          c->s_out));
+            if ((crc_mode & 3) == JFSX_CRC_GEN) {
+                // CRC arrays: one copy per run that is contiguous on both sides
+                for (int i = b0; i < b1; i++) {
+                    const size_t cn = 4 * nseg_of(blks[i].len);
+                    char *hd = (char *)blks[i].crc;
+                    const char *dd = (const char *)dv[i].crc;
+                    if (!(on && oh + on == hd && od + on == dd) && (rc = flush_out())) return rc;
+                    if (!on) {
+                        oh = hd;
+                        od = dd;
+                    }
+                    on += cn;
+                    if (align256(cn) != cn && (rc = flush_out())) return rc;
+                }
+                if ((rc = flush_out())) return rc;
+            }
+            HIP_OK(hipMemcpyAsync(w.h, w.dout, sizeof(BlkOut) * (b1 - b0), hipMemcpyDeviceToHost, c->s_out));
         }
         HIP_OK(hipEventRecord(c->ev_out[k], c->s_out));
         busy[k] = (int)g;
