@@ -180,6 +180,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and args.mode == "seal":
         cpu = cpu_baseline(args)
+    traffic, traffic_src = pmc_traffic(args, nb * L)
     if rank == 0:
         line = {
             "metric": "sealed+checksummed GB/s, 4 MiB blocks" if args.mode == "seal" else
@@ -195,7 +196,8 @@ def main():
                 "parallelism": "block-sharded x%d, no collective" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": ("crc_segments_k" if args.mode == "crc" else
                                     ("gcm_main_k" if args.algo == "aes256gcm" else "cp_main_k")),
                          "kernel_avg_ms": round(k_avg_ms, 3), "algorithmic_bytes_per_launch": algo_bytes},
@@ -206,6 +208,25 @@ def main():
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r1", "pmc_traffic.json")
+
+
+def pmc_traffic(args, plain_per_launch):
+    """HBM bytes per launch of the dominant kernel from the committed PMC passes
+    (FETCH_SIZE/WRITE_SIZE of the same kernel on a 4 GiB batch, corrected as the
+    MI355X guide prescribes, scaled per plaintext byte); None when no pass
+    covers this variant."""
+    key = {("seal", "aes256gcm"): "gcm_" + args.aes, ("seal", "chacha20poly1305"): "chacha"}.get(
+        (args.mode, args.algo), "crc_verify" if args.mode == "crc" else None)
+    try:
+        k = json.load(open(PMC_TRAFFIC))["kernels"][key]
+    except (OSError, KeyError, ValueError):
+        return None, None
+    if args.crc != "full":
+        return None, None
+    return int(k["bytes_per_plain_byte"] * plain_per_launch), "profiles/r1/pmc_traffic.json (%s)" % k["kernel"]
 
 
 def pcie_probe(eng, nbytes=1 << 30):
