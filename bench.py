@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--mem", choices=["device", "host"], default="device",
                     help="device: inputs resident in HBM (configs[1]); host: pinned host buffers streamed over PCIe "
                          "(configs[2], host ingest)")
+    ap.add_argument("--ragged", action="store_true",
+                    help="configs[4]: block lengths uniform in [64 KiB, 4 MiB] (seeded), non-multiples of 16/64/32768")
     ap.add_argument("--aes", choices=["ttable", "bitslice"], default="ttable",
                     help="AES-GCM keystream kernel: T-table AES in LDS, or bitsliced AES on the VALU")
     return ap.parse_args()
@@ -62,6 +64,16 @@ def barrier(dist):
 def max_over_ranks(dist, x, local):
     from juicefs_amd import shard
     return shard.max_over_ranks(dist, x, local)
+
+
+def ragged_len(seed, block, cap):
+    """configs[4]: a length uniform in [64 KiB, cap], SplitMix64 of (seed, block)."""
+    z = (seed * 0x9E3779B97F4A7C15 + block * 0xBF58476D1CE4E5B9 + 0x52616767) & (2**64 - 1)
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & (2**64 - 1)
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & (2**64 - 1)
+    z ^= z >> 31
+    lo = min(65536, cap)
+    return lo + z % (cap - lo + 1)
 
 
 def cpu_baseline(args):
@@ -106,24 +118,27 @@ def main():
     dst = eng.alloc(nb * L) if args.mode != "crc" else None
     crc = eng.alloc(nb * 4 * nseg)
     base = rank * nb  # global block index: blocks shard across ranks (juicefs_amd.shard.shard)
+    # block b occupies slot [b*L, b*L + lens[b]); ragged lengths are a seeded
+    # draw per global block index, so every rank and rerun sees the same batch
+    lens = [ragged_len(SEED, base + b, L) if args.ragged else L for b in range(nb)]
     for b in range(nb):
-        eng.gen_synthetic(src, L, SEED, base + b, offset=b * L)
+        eng.gen_synthetic(src, lens[b], SEED, base + b, offset=b * L)
     eng.sync()
 
     if args.mode == "crc":
         ranges = (E.jfsx_range * nb)()
         for b in range(nb):
-            ranges[b].data, ranges[b].len, ranges[b].crc = src.ptr + b * L, L, crc.ptr + 4 * nseg * b
+            ranges[b].data, ranges[b].len, ranges[b].crc = src.ptr + b * L, lens[b], crc.ptr + 4 * nseg * b
         eng.crc32c_segments(ranges, nb, E.CRC_GEN, E.MEM_DEVICE)
 
         def step():
             eng.crc32c_segments(ranges, nb, E.CRC_VERIFY, E.MEM_DEVICE)
-        algo_bytes = nb * (L + 4 * nseg)
+        algo_bytes = sum(lb + 4 * -(-lb // E.SEG) for lb in lens)
     else:
         specs = []
         for b in range(nb):
             key, nonce = E.gen_key(SEED, base + b)
-            specs.append({"key": key, "nonce": nonce, "src": src.ptr + b * L, "dst": dst.ptr + b * L, "len": L,
+            specs.append({"key": key, "nonce": nonce, "src": src.ptr + b * L, "dst": dst.ptr + b * L, "len": lens[b],
                           "crc": crc.ptr + 4 * nseg * b})
         blks, n = eng.make_blocks(specs)
         if args.mode == "seal":
@@ -137,7 +152,7 @@ def main():
 
             def step():
                 eng.open_batch(algo, oblks, n, E.CRC_VERIFY, E.MEM_DEVICE)
-        algo_bytes = nb * (2 * L + 16 + 4 * nseg + 44)
+        algo_bytes = sum(2 * lb + 16 + 4 * -(-lb // E.SEG) + 44 for lb in lens)
 
     for _ in range(args.warmup):
         step()
@@ -163,36 +178,39 @@ def main():
         from oracle import oracle as orc
         cs = None
         for b in range(0, nb, max(1, nb // args.verify))[:args.verify]:
-            p = orc.gen_block(SEED, base + b, L)
+            p = orc.gen_block(SEED, base + b, lens[b])
             key, nonce = orc.gen_key(SEED, base + b)
             c, tag = orc.seal(orc.AES256GCM if algo == E.AES256GCM else orc.CHACHA20P1305, key, nonce, p,
                               fast=algo == E.AES256GCM)
-            ok = bytes(blks[b].tag) == tag and dst.download(L, offset=b * L).tobytes() == c
+            ok = bytes(blks[b].tag) == tag and dst.download(lens[b], offset=b * L).tobytes() == c
             if args.crc == "full":
-                ok = ok and crc.download(4 * nseg, offset=4 * nseg * b).tobytes() == orc.checksum(p, hw=True)
+                cs = orc.checksum(p, hw=True)
+                ok = ok and crc.download(len(cs), offset=4 * nseg * b).tobytes() == cs
             if not ok:
                 raise SystemExit("bench: block %d differs from the oracle" % b)
             verified += 1
 
-    total_plain = world * nb * L * args.steps
+    total_plain = world * sum(lens) * args.steps
     value = total_plain / el / 1e9
     achieved = algo_bytes / (k_avg_ms / 1e3) / 1e9 if k_n else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and args.mode == "seal":
         cpu = cpu_baseline(args)
-    traffic, traffic_src = pmc_traffic(args, nb * L)
+    traffic, traffic_src = pmc_traffic(args, sum(lens)) if not args.ragged else (None, None)
     if rank == 0:
         line = {
-            "metric": "sealed+checksummed GB/s, 4 MiB blocks" if args.mode == "seal" else
-                      ("opened+verified GB/s, 4 MiB blocks" if args.mode == "open" else "CRC32C-verified GB/s"),
+            "metric": ("sealed+checksummed GB/s, %s" if args.mode == "seal" else
+                       ("opened+verified GB/s, %s" if args.mode == "open" else "CRC32C-verified GB/s, %s")) % (
+                          "ragged 64 KiB-4 MiB blocks" if args.ragged else "4 MiB blocks"),
             "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic (SplitMix64 blocks, "
             "per-block SplitMix64 keys/nonces), device-resident",
-            "config": {"workload": "%s GiB device-resident batch of 4 MiB blocks per GPU, %s %s + CRC32C %s" % (
-                nb * L / 2**30, args.algo, args.mode, "full" if args.mode == "seal" else "verify"),
-                "blocks_per_gpu": nb, "block_bytes": L, "algo": args.algo, "mode": args.mode,
-                "aes_kernel": args.aes if args.algo == "aes256gcm" and args.mode != "crc" else None,
+            "config": {"workload": "%s GiB device-resident batch of %s blocks per GPU, %s %s + CRC32C %s" % (
+                round(sum(lens) / 2**30, 3), "ragged 64 KiB-4 MiB" if args.ragged else "4 MiB", args.algo, args.mode,
+                "full" if args.mode == "seal" else "verify"),
+                "blocks_per_gpu": nb, "block_bytes": "ragged" if args.ragged else L, "algo": args.algo,
+                "mode": args.mode, "aes_kernel": args.aes if args.algo == "aes256gcm" and args.mode != "crc" else None,
                 "parallelism": "block-sharded x%d, no collective" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
