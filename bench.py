@@ -34,7 +34,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--blocks", type=int, default=16384, help="4 MiB blocks per GPU (16384 = 64 GiB)")
     ap.add_argument("--block-bytes", type=int, default=BLOCK)
-    ap.add_argument("--mode", choices=["seal", "open", "crc"], default="seal")
+    ap.add_argument("--mode", choices=["seal", "open", "crc", "decrypt"], default="seal",
+                    help="decrypt = dataEncryptor.Decrypt end to end: batched RSA-OAEP key unwrap + Open + CRC verify")
     ap.add_argument("--algo", choices=["aes256gcm", "chacha20poly1305"], default="aes256gcm")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
@@ -149,9 +150,30 @@ def main():
             eng.seal_batch(algo, blks, n, E.CRC_GEN, E.MEM_DEVICE)
             oblks, _ = eng.make_blocks([dict(s, src=s["dst"], dst=s["src"], tag=bytes(blks[i].tag))
                                         for i, s in enumerate(specs)])
+            if args.mode == "open":
+                def step():
+                    eng.open_batch(algo, oblks, n, E.CRC_VERIFY, E.MEM_DEVICE)
+            else:
+                # Decrypt end to end: every object's key arrives RSA-OAEP
+                # wrapped (encrypt.go:196-216); each step unwraps all n keys on
+                # the GPU straight into the descriptors, then opens
+                import ctypes
+                import numpy as np
+                from juicefs_amd import encrypt as enc
+                rsae = enc.NewRSAEncryptor(enc.GenerateRsaKey(2048))
+                dkey = eng.rsa_key(*enc.rsa_crt_components(rsae.privKey))
+                wrapped = np.frombuffer(b"".join(rsae.Encrypt(bytes(specs[i]["key"])) for i in range(n)), np.uint8)
+                wlen = np.full(n, 256, np.uint32)
+                mlen = np.zeros(n, np.int32)
+                for i in range(n):
+                    ctypes.memset(ctypes.addressof(oblks[i]) + E.jfsx_blk.key.offset, 0, 32)
 
-            def step():
-                eng.open_batch(algo, oblks, n, E.CRC_VERIFY, E.MEM_DEVICE)
+                def step():
+                    eng._check(eng.L.jfsx_rsa_oaep_decrypt_batch(
+                        eng.ctx, dkey, n, wrapped.ctypes.data, 256, wlen.ctypes.data,
+                        ctypes.addressof(oblks[0]) + E.jfsx_blk.key.offset, ctypes.sizeof(E.jfsx_blk),
+                        mlen.ctypes.data), "unwrap")
+                    eng.open_batch(algo, oblks, n, E.CRC_VERIFY, E.MEM_DEVICE)
         algo_bytes = sum(2 * lb + 16 + 4 * -(-lb // E.SEG) + 44 for lb in lens)
 
     for _ in range(args.warmup):
@@ -174,6 +196,30 @@ def main():
 
     # post-timing spot check of a few blocks against the oracle (checker only)
     verified = 0
+    if args.mode in ("open", "decrypt"):
+        bad = [i for i in range(nb) if oblks[i].status != E.OK]
+        if args.mode == "decrypt":
+            bad += [i for i in range(nb) if mlen[i] != 32 or bytes(oblks[i].key) != bytes(specs[i]["key"])]
+        if bad:
+            raise SystemExit("bench: %d blocks failed to open (first %d)" % (len(bad), bad[0]))
+        verified = nb
+    rsa = None
+    if args.mode == "decrypt":
+        # the unwrap alone (GPU batch) beside the reference's host path
+        # (libcrypto RSA-OAEP, one thread) on a bounded sample
+        t = time.perf_counter()
+        eng._check(eng.L.jfsx_rsa_oaep_decrypt_batch(eng.ctx, dkey, n, wrapped.ctypes.data, 256, wlen.ctypes.data,
+                                                     None, 0, mlen.ctypes.data), "unwrap")
+        gpu_s = time.perf_counter() - t
+        sample = [bytes(wrapped[256 * i:256 * i + 256]) for i in range(min(n, 200))]
+        t = time.perf_counter()
+        for w in sample:
+            rsae.Decrypt(w)
+        host_s = (time.perf_counter() - t) / len(sample)
+        rsa = {"unwraps": n, "gpu_ms_per_batch": round(gpu_s * 1e3, 3), "gpu_unwraps_per_s": round(n / gpu_s),
+               "host_us_per_unwrap_1thread": round(host_s * 1e6, 1),
+               "host_sample": "%d libcrypto RSA-OAEP decrypts, 1 thread" % len(sample)}
+        eng.rsa_key_free(dkey)
     if args.verify and args.mode == "seal":
         from oracle import oracle as orc
         cs = None
@@ -200,7 +246,9 @@ def main():
     if rank == 0:
         line = {
             "metric": ("sealed+checksummed GB/s, %s" if args.mode == "seal" else
-                       ("opened+verified GB/s, %s" if args.mode == "open" else "CRC32C-verified GB/s, %s")) % (
+                       ("opened+verified GB/s, %s" if args.mode == "open" else
+                        ("decrypted (RSA unwrap + open + verify) GB/s, %s" if args.mode == "decrypt" else
+                         "CRC32C-verified GB/s, %s"))) % (
                           "ragged 64 KiB-4 MiB blocks" if args.ragged else "4 MiB blocks"),
             "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
@@ -221,6 +269,7 @@ def main():
                          "kernel_avg_ms": round(k_avg_ms, 3), "algorithmic_bytes_per_launch": algo_bytes},
             "cpu_baseline": cpu,
             "verified_blocks": verified,
+            **({"rsa_unwrap": rsa} if rsa else {}),
         }
         print(json.dumps(line), flush=True)
     eng.close()

@@ -191,6 +191,22 @@ uint32_t jfsx_crc32c_update(uint32_t crc, const void *data, uint64_t n);
 uint32_t jfsx_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
 /* object-store checksum of header || C || tag (checksum.go:31-53) from the
  * big-endian 32 KiB segment CRCs of C that a GEN|CT batch returned */
+/* Batched RSA-OAEP key unwrap: replaces, per object,
+ * rsaEncryptor.Decrypt = rsa.DecryptOAEP(sha256, rand, priv, wrapped,
+ * label) (pkg/object/encrypt.go:124-134, called at :207-210) for every object
+ * of a batch at once, on the GPU.  The key is given by its CRT components
+ * (Go's Primes[0], Primes[1], Precomputed.Dp, Dq, Qinv), big-endian,
+ * prime_bytes each; RSA-2048 (prime_bytes = 128) only.  ct: host memory, item
+ * i at ct + i*ct_stride, ct_len[i] bytes.  msg_len[i] = message length, or -1
+ * for the decryption error (Go's "crypto/rsa: decryption error"); up to
+ * msg_stride bytes of each message are copied to msg + i*msg_stride. */
+typedef struct jfsx_rsa_key jfsx_rsa_key;
+int jfsx_rsa_key_new(jfsx_ctx *ctx, const uint8_t *p, const uint8_t *q, const uint8_t *dp, const uint8_t *dq,
+                     const uint8_t *qinv, int prime_bytes, const uint8_t *label, int label_len, jfsx_rsa_key **out);
+int jfsx_rsa_key_free(jfsx_rsa_key *key);
+int jfsx_rsa_oaep_decrypt_batch(jfsx_ctx *ctx, const jfsx_rsa_key *key, int n, const uint8_t *ct, uint64_t ct_stride,
+                                const uint32_t *ct_len, uint8_t *msg, uint64_t msg_stride, int32_t *msg_len);
+
 int jfsx_object_crc32c(const void *hdr, uint64_t hlen, const uint8_t *seg_crcs, uint64_t clen,
                        const uint8_t *tag, uint32_t *out);
 

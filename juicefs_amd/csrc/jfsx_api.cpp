@@ -13,6 +13,9 @@
 
 #include "jfsx_internal.h"
 
+#define JFSX_HD static inline
+#include "jfsx_rsa.h"
+
 using namespace jfsx;
 
 #define HIP_OK(x)                                      \
@@ -148,6 +151,10 @@ struct jfsx_ctx {
     size_t slot_bytes = (size_t)256 << 20;
     bool timing = false;
     bool bitslice = false;  // JFSX_CTX_BITSLICE
+    char *rsa_d = nullptr;  // batched RSA unwrap: ct | halves | em | len (device, grow-only)
+    size_t rsa_dcap = 0;
+    char *rsa_h = nullptr;  // pinned mirror of ct in / em + len out
+    size_t rsa_hcap = 0;
     double ms_total = 0;
     uint64_t launches = 0;
 };
@@ -672,6 +679,8 @@ int jfsx_ctx_close(jfsx_ctx *c) {
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
     if (c->d_tab) (void)hipFree(c->d_tab);
+    if (c->rsa_d) (void)hipFree(c->rsa_d);
+    if (c->rsa_h) (void)hipHostFree(c->rsa_h);
     for (int k = 0; k < kRing; k++) {
         Workspace &w = c->ws[k];
         if (w.d) (void)hipFree(w.d);
@@ -1078,6 +1087,88 @@ int jfsx_debug_tables(uint32_t *aes, uint32_t *crc, uint32_t *crcx) {
     if (aes) memcpy(aes, a.data(), 4 * a.size());
     if (crc) memcpy(crc, c.data(), 4 * c.size());
     if (crcx) memcpy(crcx, x.data(), 4 * x.size());
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// batched RSA-OAEP key unwrap (rsaEncryptor.Decrypt,
+// pkg/object/encrypt.go:124-134 and :207-210)
+// ---------------------------------------------------------------------------
+struct jfsx_rsa_key {
+    int device = 0;
+    jfsx_rsa::Key *d_key = nullptr;
+};
+
+int jfsx_rsa_key_new(jfsx_ctx *c, const uint8_t *p, const uint8_t *q, const uint8_t *dp, const uint8_t *dq,
+                     const uint8_t *qinv, int prime_bytes, const uint8_t *label, int label_len, jfsx_rsa_key **out) {
+    if (!c || !out || !p || !q || !dp || !dq || !qinv || label_len < 0 || (label_len && !label)) return JFSX_EINVAL;
+    *out = nullptr;
+    if (prime_bytes != 4 * jfsx_rsa::kLimbs) return JFSX_EINVAL;  // RSA-2048 (1024-bit primes)
+    jfsx_rsa::Key k;
+    const uint8_t empty = 0;
+    if (!jfsx_rsa::key_setup(k, p, q, dp, dq, qinv, label_len ? label : &empty, label_len)) return JFSX_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    jfsx_rsa_key *rk = new jfsx_rsa_key();
+    rk->device = c->device;
+    if (hipMalloc((void **)&rk->d_key, sizeof(k)) != hipSuccess) {
+        delete rk;
+        return JFSX_ENOMEM;
+    }
+    if (hipMemcpy(rk->d_key, &k, sizeof(k), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(rk->d_key);
+        delete rk;
+        return JFSX_EIO;
+    }
+    *out = rk;
+    return 0;
+}
+
+int jfsx_rsa_key_free(jfsx_rsa_key *k) {
+    if (!k) return JFSX_EINVAL;
+    (void)hipSetDevice(k->device);
+    if (k->d_key) (void)hipFree(k->d_key);
+    delete k;
+    return 0;
+}
+
+int jfsx_rsa_oaep_decrypt_batch(jfsx_ctx *c, const jfsx_rsa_key *k, int n, const uint8_t *ct, uint64_t ct_stride,
+                                const uint32_t *ct_len, uint8_t *msg, uint64_t msg_stride, int32_t *msg_len) {
+    if (!c || !k || n < 0 || (n && (!ct || !ct_len || !msg_len || (msg_stride && !msg)))) return JFSX_EINVAL;
+    if (n == 0) return 0;
+    if (k->device != c->device) return JFSX_EINVAL;
+    constexpr size_t K = jfsx_rsa::kModBytes;
+    const size_t o_ct = 0, o_mh = align256(K * n), o_em = o_mh + align256(2 * 4 * jfsx_rsa::kLimbs * (size_t)n),
+                 o_len = o_em + align256(K * n), dbytes = o_len + align256(4 * (size_t)n);
+    const size_t hbytes = align256(K * n) + align256(4 * (size_t)n);
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    int rc;
+    if ((rc = ensure_dev(c, &c->rsa_d, &c->rsa_dcap, dbytes))) return rc;
+    if ((rc = ensure_host(&c->rsa_h, &c->rsa_hcap, hbytes))) return rc;
+    // Go's decrypt rejects a ciphertext longer than the modulus; shorter ones
+    // are big-endian integers (left-padded here)
+    for (int i = 0; i < n; i++) {
+        uint8_t *d = (uint8_t *)c->rsa_h + K * i;
+        const uint32_t l = ct_len[i] <= K ? ct_len[i] : 0;
+        memset(d, 0, K - l);
+        if (l) memcpy(d + K - l, ct + ct_stride * i, l);
+    }
+    char *d = c->rsa_d;
+    HIP_OK(hipMemcpyAsync(d + o_ct, c->rsa_h, K * n, hipMemcpyHostToDevice, c->stream));
+    launch_rsa_unwrap(c->stream, k->d_key, n, (const uint8_t *)(d + o_ct), (uint32_t *)(d + o_mh),
+                      (uint8_t *)(d + o_em), (int32_t *)(d + o_len));
+    HIP_OK(hipGetLastError());
+    char *hl = c->rsa_h + align256(K * n);
+    HIP_OK(hipMemcpyAsync(c->rsa_h, d + o_em, K * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipMemcpyAsync(hl, d + o_len, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < n; i++) {
+        int32_t l = ((const int32_t *)hl)[i];
+        if (ct_len[i] > K) l = -1;
+        msg_len[i] = l;
+        if (l > 0 && msg_stride) memcpy(msg + msg_stride * i, c->rsa_h + K * i, std::min<uint64_t>(l, msg_stride));
+    }
     return 0;
 }
 

@@ -463,7 +463,9 @@ __global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *
                 const uint4 c = OPEN ? dd[u] : x, p = OPEN ? x : dd[u];
                 gst16(dst + o, OPEN ? p : c);
                 const uint4 cq = crc_src<CRCMODE>(c, p);
+#ifndef JFSX_ABLATE_GHASH
                 ghash_step(lds, st[0].acc, gl, c);
+#endif
                 if (CRCMODE) st[0].A = crc_piece<kLdsCrc>(lds, st[0].A, cq.x, cq.y, cq.z, cq.w);
                 if (CRCMODE && ((r0 + u) & 31) == 31) {
                     crc_segment_end<CRCMODE>(blk, tab, lane, xl, st[0].seg0, st[0].seg0 + kSeg, st[0].A, 0);

@@ -1,0 +1,355 @@
+// jfsx_rsa.h -- RSA-OAEP (SHA-256) private-key decryption arithmetic for the
+// batched key unwrap.
+//
+// Replaces, per object, rsaEncryptor.Decrypt = rsa.DecryptOAEP(sha256.New(),
+// rand, privKey, wrapped, []byte("keys")) (pkg/object/encrypt.go:124-134,
+// :207-210), which the reference runs on the host for every block it opens.
+// The arithmetic is RSA with the CRT (RFC 8017 5.1.2 / Go's precomputed
+// Dp, Dq, Qinv): m1 = c^dp mod p, m2 = c^dq mod q, h = qinv (m1 - m2) mod p,
+// m = m2 + h q; then EME-OAEP decoding (RFC 8017 7.1.2) with SHA-256 as hash
+// and MGF1 hash.  Primes are 1024-bit (RSA-2048, the size the reference docs
+// use), in 32 little-endian 32-bit limbs; products use Montgomery CIOS.
+//
+// Host/device portable: the includer defines JFSX_HD.  Every function is
+// pinned on the CPU by tests/test_rsa.py against libcrypto's RSA-OAEP.
+#pragma once
+#include <stdint.h>
+
+namespace jfsx_rsa {
+
+constexpr int kLimbs = 32;        // 1024-bit prime
+constexpr int kModBytes = 256;    // RSA-2048 modulus
+constexpr int kHash = 32;         // SHA-256
+
+// ---------------------------------------------------------------------------
+// multi-precision helpers (little-endian limbs)
+// ---------------------------------------------------------------------------
+// -m^-1 mod 2^32 (m odd), Newton iteration
+JFSX_HD uint32_t mont_inv32(uint32_t m0) {
+    uint32_t x = m0;  // correct to 3 bits
+    for (int i = 0; i < 5; i++) x *= 2u - m0 * x;
+    return 0u - x;
+}
+
+// a >= b ?
+JFSX_HD bool geq(const uint32_t *a, const uint32_t *b, int n) {
+    for (int i = n - 1; i >= 0; i--)
+        if (a[i] != b[i]) return a[i] > b[i];
+    return true;
+}
+
+// a -= b, returns borrow
+JFSX_HD uint32_t sub_in(uint32_t *a, const uint32_t *b, int n) {
+    uint64_t br = 0;
+    for (int i = 0; i < n; i++) {
+        const uint64_t d = (uint64_t)a[i] - b[i] - br;
+        a[i] = (uint32_t)d;
+        br = (d >> 32) & 1u;
+    }
+    return (uint32_t)br;
+}
+
+// a += b, returns carry
+JFSX_HD uint32_t add_in(uint32_t *a, const uint32_t *b, int n) {
+    uint64_t c = 0;
+    for (int i = 0; i < n; i++) {
+        c += (uint64_t)a[i] + b[i];
+        a[i] = (uint32_t)c;
+        c >>= 32;
+    }
+    return (uint32_t)c;
+}
+
+// out = a b R^-1 mod m (R = 2^1024), a, b < m; CIOS with one final subtract
+JFSX_HD void mont_mul(const uint32_t *a, const uint32_t *b, const uint32_t *m, uint32_t minv, uint32_t *out) {
+    uint32_t t[kLimbs + 2];
+#pragma unroll
+    for (int j = 0; j < kLimbs + 2; j++) t[j] = 0;
+#pragma unroll
+    for (int i = 0; i < kLimbs; i++) {
+        const uint32_t ai = a[i];
+        uint64_t c = 0;
+#pragma unroll
+        for (int j = 0; j < kLimbs; j++) {
+            c = (uint64_t)ai * b[j] + (c + t[j]);
+            t[j] = (uint32_t)c;
+            c >>= 32;
+        }
+        c += t[kLimbs];
+        t[kLimbs] = (uint32_t)c;
+        t[kLimbs + 1] = (uint32_t)(c >> 32);
+        const uint32_t mi = t[0] * minv;
+        c = ((uint64_t)mi * m[0] + t[0]) >> 32;
+#pragma unroll
+        for (int j = 1; j < kLimbs; j++) {
+            c = (uint64_t)mi * m[j] + (c + t[j]);
+            t[j - 1] = (uint32_t)c;
+            c >>= 32;
+        }
+        c += t[kLimbs];
+        t[kLimbs - 1] = (uint32_t)c;
+        t[kLimbs] = t[kLimbs + 1] + (uint32_t)(c >> 32);
+    }
+    // t < 2m: subtract m once if t >= m
+    uint32_t d[kLimbs];
+    uint64_t br = 0;
+#pragma unroll
+    for (int j = 0; j < kLimbs; j++) {
+        const uint64_t x = (uint64_t)t[j] - m[j] - br;
+        d[j] = (uint32_t)x;
+        br = (x >> 32) & 1u;
+    }
+    const bool keep = t[kLimbs] == 0 && br;  // t < m
+#pragma unroll
+    for (int j = 0; j < kLimbs; j++) out[j] = keep ? t[j] : d[j];
+}
+
+// R^2 mod m by doubling (host side, once per key)
+JFSX_HD void mont_r2(const uint32_t *m, uint32_t *r2) {
+    uint32_t x[kLimbs + 1];
+    for (int j = 0; j <= kLimbs; j++) x[j] = 0;
+    x[0] = 1;
+    for (int k = 0; k < 2 * 32 * kLimbs; k++) {  // x = 2^k mod m
+        uint32_t c = 0;
+        for (int j = 0; j <= kLimbs; j++) {
+            const uint32_t nc = x[j] >> 31;
+            x[j] = (x[j] << 1) | c;
+            c = nc;
+        }
+        if (x[kLimbs] || geq(x, m, kLimbs)) {
+            const uint32_t b = sub_in(x, m, kLimbs);
+            x[kLimbs] -= b;
+        }
+    }
+    for (int j = 0; j < kLimbs; j++) r2[j] = x[j];
+}
+
+// big-endian bytes <-> limbs
+JFSX_HD void from_be(const uint8_t *b, int nbytes, uint32_t *x, int nlimbs) {
+    for (int j = 0; j < nlimbs; j++) x[j] = 0;
+    for (int i = 0; i < nbytes; i++) {
+        const int bit = 8 * (nbytes - 1 - i);
+        x[bit >> 5] |= (uint32_t)b[i] << (bit & 31);
+    }
+}
+JFSX_HD void to_be(const uint32_t *x, int nlimbs, uint8_t *b, int nbytes) {
+    for (int i = 0; i < nbytes; i++) {
+        const int bit = 8 * (nbytes - 1 - i);
+        b[i] = (bit >> 5) < nlimbs ? (uint8_t)(x[bit >> 5] >> (bit & 31)) : 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// SHA-256 (FIPS 180-4) and MGF1
+// ---------------------------------------------------------------------------
+JFSX_HD uint32_t ror(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+JFSX_HD void sha256_block(uint32_t h[8], const uint8_t *p) {
+    const uint32_t K[64] = {
+        0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5, 0xd807aa98,
+        0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174, 0xe49b69c1, 0xefbe4786,
+        0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da, 0x983e5152, 0xa831c66d, 0xb00327c8,
+        0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967, 0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13,
+        0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85, 0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819,
+        0xd6990624, 0xf40e3585, 0x106aa070, 0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a,
+        0x5b9cca4f, 0x682e6ff3, 0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7,
+        0xc67178f2};
+    uint32_t w[64];
+    for (int i = 0; i < 16; i++)
+        w[i] = ((uint32_t)p[4 * i] << 24) | ((uint32_t)p[4 * i + 1] << 16) | ((uint32_t)p[4 * i + 2] << 8) | p[4 * i + 3];
+    for (int i = 16; i < 64; i++) {
+        const uint32_t s0 = ror(w[i - 15], 7) ^ ror(w[i - 15], 18) ^ (w[i - 15] >> 3);
+        const uint32_t s1 = ror(w[i - 2], 17) ^ ror(w[i - 2], 19) ^ (w[i - 2] >> 10);
+        w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+    }
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+    for (int i = 0; i < 64; i++) {
+        const uint32_t t1 = hh + (ror(e, 6) ^ ror(e, 11) ^ ror(e, 25)) + ((e & f) ^ (~e & g)) + K[i] + w[i];
+        const uint32_t t2 = (ror(a, 2) ^ ror(a, 13) ^ ror(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+        hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
+// SHA-256 of a ‖ b (b may be empty), len(a) + len(b) < 2^29
+JFSX_HD void sha256_2(const uint8_t *a, int la, const uint8_t *b, int lb, uint8_t out[32]) {
+    uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    uint8_t blk[64];
+    const int total = la + lb;
+    int pos = 0, fill = 0;
+    // stream the message bytes, then 0x80, zeros, BE64 bit length
+    const int padded = ((total + 9 + 63) / 64) * 64;
+    for (int i = 0; i < padded; i++) {
+        uint8_t v;
+        if (i < la) v = a[i];
+        else if (i < total) v = b[i - la];
+        else if (i == total) v = 0x80;
+        else if (i >= padded - 8) v = (uint8_t)(((uint64_t)total * 8) >> (8 * (padded - 1 - i)));
+        else v = 0;
+        blk[fill++] = v;
+        if (fill == 64) {
+            sha256_block(h, blk);
+            fill = 0;
+        }
+        pos++;
+    }
+    (void)pos;
+    for (int i = 0; i < 8; i++) {
+        out[4 * i] = (uint8_t)(h[i] >> 24);
+        out[4 * i + 1] = (uint8_t)(h[i] >> 16);
+        out[4 * i + 2] = (uint8_t)(h[i] >> 8);
+        out[4 * i + 3] = (uint8_t)h[i];
+    }
+}
+
+// dst[0..len) ^= MGF1-SHA256(seed, len)
+JFSX_HD void mgf1_xor(const uint8_t *seed, int slen, uint8_t *dst, int len) {
+    uint8_t ctr[4], hsh[32];
+    for (int c = 0, done = 0; done < len; c++) {
+        ctr[0] = (uint8_t)(c >> 24); ctr[1] = (uint8_t)(c >> 16); ctr[2] = (uint8_t)(c >> 8); ctr[3] = (uint8_t)c;
+        sha256_2(seed, slen, ctr, 4, hsh);
+        for (int i = 0; i < 32 && done < len; i++, done++) dst[done] ^= hsh[i];
+    }
+}
+
+// EME-OAEP decode (RFC 8017 7.1.2 step 3) of em[0..k), lhash = SHA-256(label).
+// Returns the message length and moves the message to em[0..len), or -1
+// ("crypto/rsa: decryption error").  Branches depend on the data; the GPU
+// batch is not a constant-time implementation (documented in DESIGN.md).
+JFSX_HD int oaep_decode(uint8_t *em, int k, const uint8_t lhash[32]) {
+    uint8_t *seed = em + 1, *db = em + 1 + kHash;
+    const int dblen = k - kHash - 1;
+    mgf1_xor(db, dblen, seed, kHash);
+    mgf1_xor(seed, kHash, db, dblen);
+    int bad = em[0] != 0;
+    for (int i = 0; i < kHash; i++) bad |= db[i] != lhash[i];
+    int i = kHash;
+    while (i < dblen && db[i] == 0) i++;
+    if (i >= dblen || db[i] != 1) bad = 1;
+    if (bad) return -1;
+    const int mlen = dblen - i - 1;
+    for (int j = 0; j < mlen; j++) em[j] = db[i + 1 + j];
+    return mlen;
+}
+
+// ---------------------------------------------------------------------------
+// key material in device memory (written by the host once per key)
+// ---------------------------------------------------------------------------
+struct Key {
+    uint32_t n[2 * kLimbs];             // modulus p q (ciphertexts must be < n)
+    uint32_t p[kLimbs], q[kLimbs];      // primes
+    uint32_t dp[kLimbs], dq[kLimbs];    // CRT exponents
+    uint32_t qinv[kLimbs];              // q^-1 mod p
+    uint32_t r2p[kLimbs], r2q[kLimbs];  // R^2 mod p, R^2 mod q
+    uint32_t pinv, qinv32;              // -p^-1, -q^-1 mod 2^32
+    int32_t dp_bits, dq_bits;           // exponent bit lengths
+    uint8_t lhash[32];                  // SHA-256(label)
+};
+
+JFSX_HD int bit_length(const uint32_t *x, int nlimbs) {
+    for (int i = nlimbs - 1; i >= 0; i--)
+        if (x[i]) return 32 * i + 32 - __builtin_clz(x[i]);
+    return 0;
+}
+
+// Key from the CRT components (big-endian, 128 bytes each) and the OAEP
+// label.  Returns false unless p, q are odd 1024-bit primes' shape.
+JFSX_HD bool key_setup(Key &k, const uint8_t *p, const uint8_t *q, const uint8_t *dp, const uint8_t *dq,
+                       const uint8_t *qinv, const uint8_t *label, int label_len) {
+    const int nb = 4 * kLimbs;
+    from_be(p, nb, k.p, kLimbs);
+    from_be(q, nb, k.q, kLimbs);
+    from_be(dp, nb, k.dp, kLimbs);
+    from_be(dq, nb, k.dq, kLimbs);
+    from_be(qinv, nb, k.qinv, kLimbs);
+    if (!(k.p[0] & 1u) || !(k.q[0] & 1u) || bit_length(k.p, kLimbs) != 32 * kLimbs ||
+        bit_length(k.q, kLimbs) != 32 * kLimbs)
+        return false;
+    k.pinv = mont_inv32(k.p[0]);
+    k.qinv32 = mont_inv32(k.q[0]);
+    mont_r2(k.p, k.r2p);
+    mont_r2(k.q, k.r2q);
+    k.dp_bits = bit_length(k.dp, kLimbs);
+    k.dq_bits = bit_length(k.dq, kLimbs);
+    if (k.dp_bits < 2 || k.dq_bits < 2) return false;
+    for (int j = 0; j < 2 * kLimbs; j++) k.n[j] = 0;
+    for (int i = 0; i < kLimbs; i++) {
+        uint64_t c = 0;
+        for (int j = 0; j < kLimbs; j++) {
+            c = (uint64_t)k.p[i] * k.q[j] + (c + k.n[i + j]);
+            k.n[i + j] = (uint32_t)c;
+            c >>= 32;
+        }
+        k.n[i + kLimbs] = (uint32_t)c;
+    }
+    sha256_2(label, label_len, label, 0, k.lhash);
+    return true;
+}
+
+// c mod m for a 2048-bit c = hi R + lo (hi, lo < R): (hi R mod m) + lo, reduced
+JFSX_HD void reduce_2048(const uint32_t *c, const uint32_t *m, uint32_t minv, const uint32_t *r2, uint32_t *out) {
+    uint32_t t[kLimbs + 1];
+    mont_mul(c + kLimbs, r2, m, minv, t);  // hi R mod m (hi < R, r2 < m: CIOS bound holds)
+    t[kLimbs] = add_in(t, c, kLimbs);      // + lo: < 3m since lo < R < 2m
+    for (int rep = 0; rep < 2; rep++)
+        if (t[kLimbs] || geq(t, m, kLimbs)) t[kLimbs] -= sub_in(t, m, kLimbs);
+    for (int j = 0; j < kLimbs; j++) out[j] = t[j];
+}
+
+// x^e mod m, left to right over the e_bits bits of e (x < m)
+JFSX_HD void mod_exp(const uint32_t *x, const uint32_t *e, int e_bits, const uint32_t *m, uint32_t minv,
+                     const uint32_t *r2, uint32_t *out) {
+    uint32_t xm[kLimbs], acc[kLimbs], one[kLimbs];
+    mont_mul(x, r2, m, minv, xm);  // x R mod m
+    for (int j = 0; j < kLimbs; j++) acc[j] = xm[j];
+    for (int b = e_bits - 2; b >= 0; b--) {
+        mont_mul(acc, acc, m, minv, acc);
+        if ((e[b >> 5] >> (b & 31)) & 1u) mont_mul(acc, xm, m, minv, acc);
+    }
+    for (int j = 0; j < kLimbs; j++) one[j] = j == 0;
+    mont_mul(acc, one, m, minv, out);  // leave the Montgomery domain
+}
+
+// m = m2 + q (qinv (m1 - m2) mod p), the 2048-bit CRT recombination
+JFSX_HD void crt(const Key &k, const uint32_t *m1, const uint32_t *m2, uint32_t *m) {
+    uint32_t t[kLimbs + 1], h[kLimbs], u[kLimbs];
+    for (int j = 0; j < kLimbs; j++) t[j] = m2[j];
+    t[kLimbs] = 0;
+    if (geq(t, k.p, kLimbs)) sub_in(t, k.p, kLimbs);  // m2 < q < 2p
+    for (int j = 0; j < kLimbs; j++) u[j] = m1[j];
+    if (sub_in(u, t, kLimbs)) add_in(u, k.p, kLimbs);  // (m1 - m2) mod p
+    mont_mul(u, k.qinv, k.p, k.pinv, h);               // u qinv R^-1
+    mont_mul(h, k.r2p, k.p, k.pinv, h);                // u qinv
+    for (int j = 0; j < 2 * kLimbs; j++) m[j] = j < kLimbs ? m2[j] : 0;
+    for (int i = 0; i < kLimbs; i++) {  // m += h q
+        uint64_t c = 0;
+        for (int j = 0; j < kLimbs; j++) {
+            c = (uint64_t)h[i] * k.q[j] + (c + m[i + j]);
+            m[i + j] = (uint32_t)c;
+            c >>= 32;
+        }
+        for (int j = i + kLimbs; j < 2 * kLimbs && c; j++) {
+            c += m[j];
+            m[j] = (uint32_t)c;
+            c >>= 32;
+        }
+    }
+}
+
+// One whole unwrap on one thread (the CPU pin; the GPU splits it into the
+// two half exponentiations and a finish kernel): ct = k bytes, big-endian.
+// Returns the message length (msg in em[0..len)) or -1.
+JFSX_HD int decrypt(const Key &k, const uint8_t *ct, uint8_t em[kModBytes]) {
+    uint32_t c[2 * kLimbs], m1[kLimbs], m2[kLimbs], m[2 * kLimbs], x[kLimbs];
+    from_be(ct, kModBytes, c, 2 * kLimbs);
+    if (geq(c, k.n, 2 * kLimbs)) return -1;
+    reduce_2048(c, k.p, k.pinv, k.r2p, x);
+    mod_exp(x, k.dp, k.dp_bits, k.p, k.pinv, k.r2p, m1);
+    reduce_2048(c, k.q, k.qinv32, k.r2q, x);
+    mod_exp(x, k.dq, k.dq_bits, k.q, k.qinv32, k.r2q, m2);
+    crt(k, m1, m2, m);
+    to_be(m, 2 * kLimbs, em, kModBytes);
+    return oaep_decode(em, kModBytes, k.lhash);
+}
+
+}  // namespace jfsx_rsa

@@ -74,6 +74,8 @@ class _Crypto:
             ("PEM_write_bio_PrivateKey", I, [P, P, P, P, I, P, P]), ("BIO_new", P, [P]),
             ("BIO_s_mem", P, []), ("BIO_ctrl", ctypes.c_long, [P, I, ctypes.c_long, P]),
             ("ERR_clear_error", None, []),
+            ("EVP_PKEY_get_bn_param", I, [P, ctypes.c_char_p, ctypes.POINTER(P)]),
+            ("BN_bn2binpad", I, [P, P, I]), ("BN_free", None, [P]),
         ]:
             f = getattr(L, name)
             f.restype = res
@@ -154,6 +156,27 @@ def ParseRsaPrivateKeyFromPath(path, passphrase=""):
     return ParseRsaPrivateKeyFromPem(b, passphrase.encode() if isinstance(passphrase, str) else passphrase)
 
 
+def rsa_crt_components(priv, nbytes=128):
+    """(p, q, dp, dq, qinv) of an RSA private key, big-endian, nbytes each --
+    the precomputed CRT values Go's rsa.PrivateKey carries (Primes, Dp, Dq,
+    Qinv), which the engine's batched unwrap consumes."""
+    L = _Crypto.get().L
+    out = []
+    for name in (b"rsa-factor1", b"rsa-factor2", b"rsa-exponent1", b"rsa-exponent2", b"rsa-coefficient1"):
+        bn = ctypes.c_void_p()
+        if L.EVP_PKEY_get_bn_param(priv._pkey, name, ctypes.byref(bn)) != 1:
+            L.ERR_clear_error()
+            raise EncryptError("not an RSA private key with CRT parameters")
+        try:
+            buf = ctypes.create_string_buffer(nbytes)
+            if L.BN_bn2binpad(bn, buf, nbytes) != nbytes:
+                raise EncryptError("RSA CRT parameter %s does not fit %d bytes" % (name.decode(), nbytes))
+            out.append(buf.raw)
+        finally:
+            L.BN_free(bn)
+    return tuple(out)
+
+
 class RsaEncryptor:
     """rsaEncryptor: RSA-OAEP with SHA-256 (OAEP and MGF1) and label "keys"."""
 
@@ -197,6 +220,34 @@ class RsaEncryptor:
 
     def Decrypt(self, ciphertext):
         return self._run(bytes(ciphertext), True)
+
+    def DecryptBatch(self, ciphertexts, eng=None):
+        """Decrypt for a whole read window at once: the engine's batched
+        RSA-OAEP unwrap on the GPU, bit-exact to
+        rsa.DecryptOAEP.  Returns, per item, the plaintext or the EncryptError
+        Decrypt would raise.  Keys the engine does not take (not RSA-2048)
+        unwrap on the host as the reference does (encrypt.go:132-134)."""
+        eng = eng or default_engine()
+        dk = self._device_key(eng)
+        if dk is None:
+            out = []
+            for c in ciphertexts:
+                try:
+                    out.append(self.Decrypt(c))
+                except EncryptError as e:
+                    out.append(e)
+            return out
+        res = eng.oaep_decrypt_batch(dk, ciphertexts)
+        return [EncryptError("crypto/rsa: decryption error") if r is None else r for r in res]
+
+    def _device_key(self, eng):
+        keys = self.__dict__.setdefault("_dev_keys", {})
+        if eng.ctx not in keys:
+            try:
+                keys[eng.ctx] = eng.rsa_key(*rsa_crt_components(self.privKey), label=self.label)
+            except Exception:  # not RSA-2048 with CRT parameters
+                keys[eng.ctx] = None
+        return keys[eng.ctx]
 
 
 def NewRSAEncryptor(privKey):
@@ -274,6 +325,7 @@ class DataEncryptor:
         from .checksum import ChecksumVerifyError
         res = [None] * len(ciphertexts)
         specs, idx, bufs, segs = [], [], [], []
+        parsed = []
         for i, c in enumerate(ciphertexts):
             c = bytes(c)
             if len(c) < 3:
@@ -284,14 +336,25 @@ class DataEncryptor:
             if 3 + keyLen + nonceLen >= len(c):
                 res[i] = EncryptError("misformed ciphertext: %d %d" % (keyLen, nonceLen))
                 continue
+            parsed.append((i, c, keyLen, nonceLen))
+        # unwrap every object key of the window at once when the key encryptor
+        # batches (the GPU RSA-OAEP unwrap), else one by one (encrypt.go:207)
+        wrapped = [c[3:3 + kl] for _, c, kl, _ in parsed]
+        if hasattr(self.keyEncryptor, "DecryptBatch"):
+            keys = self.keyEncryptor.DecryptBatch(wrapped, self.eng)
+        else:
+            keys = []
+            for w in wrapped:
+                try:
+                    keys.append(self.keyEncryptor.Decrypt(w))
+                except Exception as e:
+                    keys.append(e)
+        for (i, c, keyLen, nonceLen), key in zip(parsed, keys):
             body = c[3:]
-            cipherkey = body[:keyLen]
             nonce = body[keyLen:keyLen + nonceLen]
             ct = body[keyLen + nonceLen:]
-            try:
-                key = self.keyEncryptor.Decrypt(cipherkey)
-            except Exception as e:  # encrypt.go:207-210
-                res[i] = EncryptError("decryt key: " + str(e))
+            if isinstance(key, Exception):  # encrypt.go:207-210
+                res[i] = EncryptError("decryt key: " + str(key))
                 continue
             if len(key) != self.keyLen:
                 res[i] = EncryptError("crypto/aes: invalid key size %d" % len(key))

@@ -31,6 +31,7 @@ EXPORTS = [
     "jfsx_seal_batch", "jfsx_open_batch", "jfsx_crc32c_segments", "jfsx_checksum", "jfsx_cache_verify",
     "jfsx_data_encrypt", "jfsx_data_decrypt", "jfsx_parse_header", "jfsx_gen_synthetic", "jfsx_gen_key",
     "jfsx_debug_tables", "jfsx_crc32c_update", "jfsx_crc32c_combine", "jfsx_object_crc32c",
+    "jfsx_rsa_key_new", "jfsx_rsa_key_free", "jfsx_rsa_oaep_decrypt_batch",
 ]
 
 
@@ -103,6 +104,9 @@ def load_library(path=LIB_PATH):
             "jfsx_gen_synthetic": (I, [P, P, U64, U64, U64]),
             "jfsx_gen_key": (None, [U64, U64, P, P]),
             "jfsx_debug_tables": (I, [P, P, P]),
+            "jfsx_rsa_key_new": (I, [P, P, P, P, P, P, I, P, I, PP]),
+            "jfsx_rsa_key_free": (I, [P]),
+            "jfsx_rsa_oaep_decrypt_batch": (I, [P, P, I, P, U64, P, P, U64, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -359,6 +363,39 @@ class Engine:
                                       ctypes.byref(got) if expect_crc is not None else None)
         self.last_got_crc = got.value
         return rc, out[:olen.value].tobytes() if rc == 0 else b""
+
+    def rsa_key(self, p, q, dp, dq, qinv, label=b"keys"):
+        """Device copy of an RSA-2048 private key from its CRT components
+        (big-endian, 128 bytes each) for oaep_decrypt_batch."""
+        k = ctypes.c_void_p()
+        lab = bytes(label)
+        self._check(self.L.jfsx_rsa_key_new(self.ctx, bytes(p), bytes(q), bytes(dp), bytes(dq), bytes(qinv), len(p),
+                                            lab if lab else None, len(lab), ctypes.byref(k)), "jfsx_rsa_key_new")
+        return k.value
+
+    def rsa_key_free(self, key):
+        if key:
+            self.L.jfsx_rsa_key_free(key)
+
+    def oaep_decrypt_batch(self, key, ciphertexts):
+        """rsa.DecryptOAEP(sha256, priv, c, label) for every c at once: a list
+        of plaintexts, None where Go returns the decryption error."""
+        n = len(ciphertexts)
+        if n == 0:
+            return []
+        stride = max(1, max(len(c) for c in ciphertexts))
+        buf = np.zeros(n * stride, np.uint8)
+        lens = np.zeros(n, np.uint32)
+        for i, c in enumerate(ciphertexts):
+            c = bytes(c)
+            buf[i * stride:i * stride + len(c)] = np.frombuffer(c, np.uint8)
+            lens[i] = len(c)
+        msg = np.zeros(n * 256, np.uint8)
+        mlen = np.zeros(n, np.int32)
+        self._check(self.L.jfsx_rsa_oaep_decrypt_batch(self.ctx, key, n, buf.ctypes.data, stride, lens.ctypes.data,
+                                                       msg.ctypes.data, 256, mlen.ctypes.data),
+                    "jfsx_rsa_oaep_decrypt_batch")
+        return [None if mlen[i] < 0 else msg[256 * i:256 * i + mlen[i]].tobytes() for i in range(n)]
 
     def crc32c_update(self, crc, data):
         return crc32c_update(crc, data)

@@ -1,5 +1,7 @@
 // VALU issue-rate probe for the bitsliced AES (measurement tool, not product code):
-// independent v_bitop3_b32 / v_xor_b32 streams at 1..8 waves per SIMD.
+// independent v_bitop3_b32 / v_xor_b32 / add+alignbit / v_mad_u64_u32 streams
+// at 2 and 4 waves per SIMD (rates in wave-instructions of the loop body; mode
+// 3 is two instructions per element, mode 4 is one mad plus one xor).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>
@@ -16,7 +18,11 @@ __global__ __launch_bounds__(1024) void probe(uint32_t *out, uint32_t seed, int 
             if (MODE == 0) r[i] = __builtin_amdgcn_bitop3_b32(r[i], a, b, 0x96);       // 3 VGPR sources
             else if (MODE == 1) r[i] = r[i] ^ a;                                        // v_xor_b32
             else if (MODE == 2) r[i] = __builtin_amdgcn_bitop3_b32(r[i], a, seed, 0x96); // 2 VGPR + SGPR
-            else r[i] = __builtin_amdgcn_bitop3_b32(r[i], a, b, 0x6a);
+            else if (MODE == 3) r[i] = __builtin_amdgcn_alignbit(r[i] + a, r[i] + a, 16);  // v_add + v_alignbit
+            else {  // v_mad_u64_u32 (Poly1305 limb products)
+                const uint64_t m = (uint64_t)r[i] * a + b;
+                r[i] = (uint32_t)m ^ (uint32_t)(m >> 32);
+            }
         }
     }
     uint32_t x = 0;
@@ -32,8 +38,8 @@ int main() {
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     const int iters = 4000;
-    for (int mode = 0; mode < 3; mode++) {
-        for (int wps : {1, 2, 4, 8}) {  // waves per SIMD: 256 CUs x 4 SIMDs
+    for (int mode = 0; mode < 5; mode++) {
+        for (int wps : {2, 4}) {  // waves per SIMD: 256 CUs x 4 SIMDs
             const int threads = 256 * wps;  // per workgroup: 4*wps waves -> one WG per CU
             const int blocks = 256;
             float best = 1e9;
@@ -42,6 +48,8 @@ int main() {
                 if (mode == 0) hipLaunchKernelGGL(probe<0>, dim3(blocks), dim3(threads), 0, 0, out, 7u, iters);
                 if (mode == 1) hipLaunchKernelGGL(probe<1>, dim3(blocks), dim3(threads), 0, 0, out, 7u, iters);
                 if (mode == 2) hipLaunchKernelGGL(probe<2>, dim3(blocks), dim3(threads), 0, 0, out, 7u, iters);
+                if (mode == 3) hipLaunchKernelGGL(probe<3>, dim3(blocks), dim3(threads), 0, 0, out, 7u, iters);
+                if (mode == 4) hipLaunchKernelGGL(probe<4>, dim3(blocks), dim3(threads), 0, 0, out, 7u, iters);
                 hipEventRecord(e1);
                 hipEventSynchronize(e1);
                 float ms;
