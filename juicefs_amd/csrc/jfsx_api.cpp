@@ -93,18 +93,20 @@ void make_crc_tables(std::vector<uint32_t> &crc, std::vector<uint32_t> &crcx) {
             if (n & 1) r = crc_mulmod_h(x8[k], r);
         return r;
     };
-    crc.assign(24 * 256, 0);
+    crc.assign(28 * 256, 0);
     for (int j = 0; j < 16; j++) {
         const uint32_t xp = xpow8(15 - j);
         for (int b = 0; b < 256; b++) crc[j * 256 + b] = crc_mulmod_h(xp, T[b]);
     }
     // S tables: shift a lane CRC across the gap to its next piece -- 1008 B for
     // 16-B pieces at 1 KiB row stride (GCM), 4032 B for 64-B chunks at 4 KiB (ChaCha)
-    const uint32_t x1008 = xpow8(1008), x4032 = xpow8(4032);
+    // (and 1024 B: a whole row, for the CRC-only kernel's A' = S(A) ^ U(piece))
+    const uint32_t x1008 = xpow8(1008), x4032 = xpow8(4032), x1024 = xpow8(1024);
     for (int k = 0; k < 4; k++)
         for (uint32_t v = 0; v < 256; v++) {
             crc[(16 + k) * 256 + v] = crc_mulmod_h(x1008, v << (8 * k));
             crc[(20 + k) * 256 + v] = crc_mulmod_h(x4032, v << (8 * k));
+            crc[(24 + k) * 256 + v] = crc_mulmod_h(x1024, v << (8 * k));
         }
     crcx.assign(192, 0);
     for (int l = 0; l < 64; l++) crcx[l] = xpow8(16 * (63 - l));
@@ -520,7 +522,13 @@ int run_crc(jfsx_ctx *c, int n, jfsx_range *r, int mode) {
     if (n == 0) return 0;
     uint64_t calc_words = 0;
     std::vector<Task> tasks;
-    const uint64_t per = 4 * (uint64_t)kSeg;
+    // one 16-wave workgroup per task (jfsx_crc.hip): up to kCrcTaskBytes, but
+    // small enough that a small batch still spreads over every CU (~2 tasks
+    // per CU), and a whole number of 16-segment rounds
+    uint64_t total = 0;
+    for (int i = 0; i < n; i++) total += r[i].len;
+    const uint64_t round = 16 * (uint64_t)kSeg;
+    const uint64_t per = std::min<uint64_t>(kCrcTaskBytes, std::max<uint64_t>(round, (total / 512 + round - 1) / round * round));
     for (int i = 0; i < n; i++) {
         if (r[i].len && (!r[i].data || !aligned16(r[i].data))) return JFSX_EINVAL;
         if (!r[i].crc) return JFSX_EINVAL;
@@ -1082,7 +1090,7 @@ void jfsx_gen_key(uint64_t seed, uint64_t b, uint8_t key[32], uint8_t nonce[12])
 
 int jfsx_debug_tables(uint32_t *aes, uint32_t *crc, uint32_t *crcx) {
     std::vector<uint32_t> a, c, x;
-    make_aes_table(a);  // 16384 / 6144 / 192 dwords
+    make_aes_table(a);  // 16384 / 7168 / 192 dwords
     make_crc_tables(c, x);
     if (aes) memcpy(aes, a.data(), 4 * a.size());
     if (crc) memcpy(crc, c.data(), 4 * c.size());

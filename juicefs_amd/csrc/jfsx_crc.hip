@@ -11,59 +11,131 @@
 
 namespace jfsx {
 
-constexpr uint32_t kCrcWaves = 4;  // 256-thread workgroups, one segment per wave
-constexpr uint32_t kLdsCrcOnly = 0;
+// Slice-by-16 reads 20 random table dwords per 16 B; with one copy of each
+// table, 32 lanes of random bytes land on the 32 LDS banks with ~3.5-way
+// conflicts and the kernel is LDS-bound near 4.2 TB/s.  Here every byte lookup
+// is split into its two nibble lookups (the tables are linear: T[b] =
+// T[b & 15] ^ T[b & 240]) and each 16-entry nibble table is replicated 32x,
+// one replica per bank, so lane l always reads bank l mod 32: conflict-free at
+// twice the lookups.  A v_perm builds each address in one VALU op:
+//   perm(x & 0x0f0f0f0f, lb) = (lo nibble of byte k) << 8 | lb
+//   perm((x >> 4) & 0x0f0f0f0f, lb) = (hi nibble of byte k) << 8 | lb
+// with lb = 4 * (lane mod 32) | 0x10000 (byte 2 of lb is selected for the
+// tables above 64 KiB, past the ds_read offset field) and the table in the
+// ds_read immediate: table t (lo) / t + 0.5 (hi) at t * 4096 + hi * 128, nibble
+// stride 256 B -- 20 x 4 KiB = 80 KiB, two 16-wave workgroups per CU.
+// Tables t = 0..15 are U0..U15 (slice-by-16); t = 16..19 shift a lane CRC by
+// one 1 KiB row, so A' = S1024(A) ^ U(piece) and the 32 data lookups of a row
+// do not wait for A.  Each workgroup stages the tables once per task (0.5 to
+// 4 MiB) and every wave loops over segments.
+constexpr uint32_t kCrcWaves = 16;
+#ifndef JFSX_CRC_PF
+#define JFSX_CRC_PF 4
+#endif
+constexpr int kCrcPf = JFSX_CRC_PF;  // rows of 16 B per lane in flight
+constexpr uint32_t kCrcLds = 20 * 4096;  // 81920 B
 
-__global__ __launch_bounds__(kCrcWaves * 64) void crc_segments_k(const Task *__restrict__ tasks,
+#define NIB(t, h, xm, k)                                                                                          \
+    lds_u32(lds, __builtin_amdgcn_perm((xm), lb, ((t) >= 16 ? 0x0c020000u : 0x0c0c0000u) | ((4u + (k)) << 8)) + \
+                     (((t)&15) * 4096u + (h)*128u))
+#define X3(a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), 0x96)
+
+// the 8 nibble lookups of word x through tables t..t+3
+__device__ __forceinline__ uint32_t crc_word_nib(const char *lds, uint32_t lb, uint32_t t, uint32_t x) {
+    const uint32_t xl = x & 0x0f0f0f0fu, xh = (x >> 4) & 0x0f0f0f0fu;
+    return X3(X3(NIB(t, 0, xl, 0), NIB(t, 1, xh, 0), NIB(t + 1, 0, xl, 1)),
+              X3(NIB(t + 1, 1, xh, 1), NIB(t + 2, 0, xl, 2), NIB(t + 2, 1, xh, 2)),
+              NIB(t + 3, 0, xl, 3) ^ NIB(t + 3, 1, xh, 3));
+}
+
+// A advanced over one 1 KiB row whose lane piece is p:
+// crc_raw(shift(A, 1008 B), p) = shift(A, 1024 B) ^ crc_raw(0, p)
+__device__ __forceinline__ uint32_t crc_row_nib(const char *lds, uint32_t lb, uint32_t A, uint4 p) {
+    const uint32_t d = X3(crc_word_nib(lds, lb, 0, p.x), crc_word_nib(lds, lb, 4, p.y), crc_word_nib(lds, lb, 8, p.z)) ^
+                       crc_word_nib(lds, lb, 12, p.w);
+    return crc_word_nib(lds, lb, 16, A) ^ d;
+}
+#undef X3
+
+// ragged tails (segment length not a multiple of 16 B: the last segment of an
+// odd-sized block only) read the byte tables from global memory:
+// crc_raw(shift(A, 1008 B), first n bytes of p)
+__device__ __noinline__ uint32_t crc_partial_g(const uint32_t *__restrict__ T, uint32_t A, const uint32_t p[4], int n) {
+    uint32_t c = T[16 * 256 + (A & 0xffu)] ^ T[17 * 256 + ((A >> 8) & 0xffu)] ^ T[18 * 256 + ((A >> 16) & 0xffu)] ^
+                 T[19 * 256 + (A >> 24)];
+    for (int i = 0; i < n; i++) {
+        const uint32_t byte = (p[i >> 2] >> (8 * (i & 3))) & 0xffu;
+        c = T[15 * 256 + ((c ^ byte) & 0xffu)] ^ (c >> 8);
+    }
+    return c;
+}
+
+__global__ __launch_bounds__(kCrcWaves * 64) __attribute__((amdgpu_waves_per_eu(8))) void crc_segments_k(const Task *__restrict__ tasks,
                                                                 const BlkDev *__restrict__ blks, DevTables tab) {
-    __shared__ __attribute__((aligned(16))) char lds[20480];
+    __shared__ __attribute__((aligned(16))) char lds[kCrcLds];
     const Task task = tasks[blockIdx.x];
     const BlkDev blk = blks[task.blk];
     const uint32_t tid = threadIdx.x;
-    {
-        const uint4 *gc = reinterpret_cast<const uint4 *>(tab.crc);
-        uint4 *lc = reinterpret_cast<uint4 *>(lds);
-        for (uint32_t i = tid; i < 1280; i += kCrcWaves * 64) lc[i] = gc[i];
+    // stage: i = (table t, hi, nibble, replica quad rq)
+    for (uint32_t i = tid; i < 640 * 8; i += kCrcWaves * 64) {
+        const uint32_t rq = i & 7, nib = (i >> 3) & 15, hi = (i >> 7) & 1, t = i >> 8;
+        const uint32_t v = tab.crc[(t < 16 ? t : t + 8) * 256 + (hi ? nib << 4 : nib)];
+        *reinterpret_cast<uint4 *>(lds + t * 4096 + nib * 256 + hi * 128 + 16 * rq) = make_uint4(v, v, v, v);
     }
     __syncthreads();
-    const uint32_t wave = tid >> 6, lane = tid & 63;
-    const uint64_t seg0 = task.c0 + (uint64_t)wave * kSeg;
-    if (seg0 >= task.c1) return;
-    const uint64_t seg1 = seg0 + kSeg < task.c1 ? seg0 + kSeg : task.c1;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const uint32_t lb = ((lane & 31) << 2) | 0x10000u;
     const uint8_t *src = blk.src;
-    uint32_t A = 0, lend = 0;
-    const uint64_t nrows = (seg1 - seg0 + 1023) / 1024;
-    uint4 nxt = load_piece(src, seg0 + 16 * lane, seg1);
-    for (uint64_t r = 0; r < nrows; r++) {
-        const uint64_t o = seg0 + 1024 * r + 16 * lane;
-        uint4 p = nxt;
-        if (r + 1 < nrows) nxt = load_piece(src, o + 1024, seg1);
-        if (o + 16 <= seg1) {
-            A = crc_piece<kLdsCrcOnly>(lds, A, p.x, p.y, p.z, p.w);
-            lend = (uint32_t)(o + 16 - seg0);
-        } else if (o < seg1) {
-            const uint32_t pw[4] = {p.x, p.y, p.z, p.w};
-            A = crc_partial<kLdsCrcOnly>(lds, A, pw, (int)(seg1 - o));
-            lend = (uint32_t)(seg1 - seg0);
+    for (uint64_t seg0 = task.c0 + (uint64_t)wave * kSeg; seg0 < task.c1; seg0 += (uint64_t)kCrcWaves * kSeg) {
+        const uint64_t seg1 = seg0 + kSeg < task.c1 ? seg0 + kSeg : task.c1;
+        uint32_t A = 0, lend = 0;
+        const uint64_t nrows = (seg1 - seg0 + 1023) / 1024;
+        if (seg1 - seg0 == (uint64_t)kSeg) {
+            // full segment: 32 rows, kCrcPf loads in flight per wave (HBM
+            // latency x 8 TB/s needs ~64 KiB in flight per CU)
+            const uint8_t *q = src + seg0 + 16 * lane;
+            uint4 buf[kCrcPf];
+#pragma unroll
+            for (int r = 0; r < kCrcPf; r++) buf[r] = gld16(q + 1024 * r);
+#pragma unroll
+            for (int r = 0; r < 32; r++) {
+                const uint4 p = buf[r % kCrcPf];
+                if (r + kCrcPf < 32) buf[r % kCrcPf] = gld16(q + 1024 * (r + kCrcPf));
+                A = crc_row_nib(lds, lb, A, p);
+            }
+            lend = kSeg - 1024 + 16 * lane + 16;
+        } else {
+            for (uint64_t r = 0; r < nrows; r++) {
+                const uint64_t o = seg0 + 1024 * r + 16 * lane;
+                const uint4 p = load_piece(src, o, seg1);
+                if (o + 16 <= seg1) {
+                    A = crc_row_nib(lds, lb, A, p);
+                    lend = (uint32_t)(o + 16 - seg0);
+                } else if (o < seg1) {
+                    const uint32_t pw[4] = {p.x, p.y, p.z, p.w};
+                    A = crc_partial_g(tab.crc, A, pw, (int)(seg1 - o));
+                    lend = (uint32_t)(seg1 - seg0);
+                }
+            }
         }
-    }
-    const uint32_t Lseg = (uint32_t)(seg1 - seg0);
-    uint32_t v, K;
-    if (Lseg == (uint32_t)kSeg) {
-        v = crc_mulmod(tab.crcx[lane], A);
-        K = tab.crcx[96];
-    } else {
-        v = crc_mulmod(crc_xpow8(Lseg - lend, tab.crcx + 64), A);
-        K = crc_mulmod(crc_xpow8(Lseg, tab.crcx + 64), 0xffffffffu);
-    }
-    const uint32_t raw = wave_xor(v);
-    if (lane == 0) {
-        const uint32_t crc = ~(K ^ raw);
-        const uint64_t si = seg0 / kSeg;
-        if (blk.crc_calc)
-            blk.crc_calc[si] = crc;
-        else
-            *reinterpret_cast<uint32_t *>(blk.crc + 4 * si) = __builtin_bswap32(crc);
+        const uint32_t Lseg = (uint32_t)(seg1 - seg0);
+        uint32_t v, K;
+        if (Lseg == (uint32_t)kSeg) {
+            v = crc_mulmod(tab.crcx[lane], A);
+            K = tab.crcx[96];
+        } else {
+            v = crc_mulmod(crc_xpow8(Lseg - lend, tab.crcx + 64), A);
+            K = crc_mulmod(crc_xpow8(Lseg, tab.crcx + 64), 0xffffffffu);
+        }
+        const uint32_t raw = wave_xor(v);
+        if (lane == 0) {
+            const uint32_t crc = ~(K ^ raw);
+            const uint64_t si = seg0 / kSeg;
+            if (blk.crc_calc)
+                blk.crc_calc[si] = crc;
+            else
+                *reinterpret_cast<uint32_t *>(blk.crc + 4 * si) = __builtin_bswap32(crc);
+        }
     }
 }
 

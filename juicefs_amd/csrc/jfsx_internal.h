@@ -98,6 +98,7 @@ struct CpSched {
     uint32_t r2k[32][5];    // r^(2^k)
 };
 
+constexpr uint64_t kCrcTaskBytes = 4 << 20;  // bytes per CRC-only task (crc_segments_k)
 constexpr int kCpWaves = 4;                 // waves per ChaCha20-Poly1305 workgroup
 constexpr int kCpTaskBytes = 1 << 20;       // bytes per ChaCha task (<= kCpWaves * segments)
 
@@ -219,7 +220,7 @@ struct JfsxTables;
 namespace jfsx {
 struct DevTables {
     const uint32_t *aes;    // 16384 dwords: T0|T2 replicated x32 per index
-    const uint32_t *crc;    // 20 x 256 dwords: U0..U15 (slice-by-16), S0..S3 (shift 1008 B)
+    const uint32_t *crc;    // 28 x 256 dwords: U0..U15 (slice-by-16), shift 1008 B, 4032 B, 1024 B
     const uint32_t *crcx;   // 64 lane shift constants, 32 x8pow, K_full
 };
 void launch_gcm_keysetup(hipStream_t s, int n, const KeyIn *keys, const BlkDev *blks, GcmSched *sched,

@@ -172,6 +172,31 @@ def test_crc_segments_device_gen_verify(eng):
             assert arr[i].status == E.OK
 
 
+def test_crc_segments_ragged_many_tasks(eng):
+    """crc_segments_k: ragged tails (byte-serial path), short segments, and
+    ranges split over several 16-wave tasks (0.5-4 MiB each)."""
+    rng = np.random.default_rng(5)
+    lens = [0, 15, 16, 17, 1023, 1024, 1025, 32767, 32769, (512 << 10) + 3, (3 << 20) + 1, (9 << 20) + 13,
+            (16 << 20)] + [int(x) for x in rng.integers(1, 1 << 21, 20)]
+    bufs = []
+    for i, n in enumerate(lens):
+        d = orc.gen_block(21, i, n)
+        db = eng.alloc(max(n, 16))
+        if n:
+            db.upload(d)
+        cb = eng.alloc(4 * max(1, -(-n // E.SEG)))
+        bufs.append((d, db, cb))
+    arr = (E.jfsx_range * len(lens))()
+    for i, (d, db, cb) in enumerate(bufs):
+        arr[i].data, arr[i].len, arr[i].crc = db.ptr, d.size, cb.ptr
+    eng.crc32c_segments(arr, len(lens), E.CRC_GEN, E.MEM_DEVICE)
+    for i, (d, db, cb) in enumerate(bufs):
+        want = orc.checksum(d)
+        assert cb.download().tobytes()[:len(want)] == want, lens[i]
+    eng.crc32c_segments(arr, len(lens), E.CRC_VERIFY, E.MEM_DEVICE)
+    assert all(arr[i].status == E.OK for i in range(len(lens)))
+
+
 @pytest.mark.parametrize("algo", [E.AES256GCM, E.CHACHA20P1305])
 def test_object_format_vs_oracle(eng, algo):
     wrapped = bytes(range(256))

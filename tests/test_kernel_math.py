@@ -92,6 +92,34 @@ def emulate_segment_crc(seg, tables):
     return (~(K ^ raw)) & 0xFFFFFFFF
 
 
+def emulate_full_segment_nibble(seg, tables):
+    """crc_segments_k's full-segment path: A' = S1024(A) ^ U(piece), every
+    byte lookup split into its low- and high-nibble halves (the tables are
+    linear, so T[b] = T[b & 15] ^ T[b & 240])."""
+    _, crc, crcx = tables
+    T = lambda t, v: int(crc[t * 256 + (v & 15)]) ^ int(crc[t * 256 + (v & 240)])
+    A = [0] * 64
+    for r in range(32):
+        for lane in range(64):
+            o = 1024 * r + 16 * lane
+            a = A[lane]
+            v = 0
+            for k in range(4):
+                v ^= T(24 + k, (a >> (8 * k)) & 255)
+            for j in range(16):
+                v ^= T(j, seg[o + j])
+            A[lane] = v
+    raw = 0
+    for lane in range(64):
+        raw ^= mulmod(int(crcx[lane]), A[lane])
+    return (~(int(crcx[96]) ^ raw)) & 0xFFFFFFFF
+
+
+def test_nibble_row_shift_crc_matches_crc32c(tables):
+    seg = orc.gen_block(7, 32768, 32768).tobytes()
+    assert emulate_full_segment_nibble(seg, tables) == orc.crc32c(seg)
+
+
 @pytest.mark.parametrize("L", [1, 15, 16, 17, 1000, 1024, 1025, 4111, 31999, 32767, 32768])
 def test_lane_strided_crc_matches_crc32c(L, tables):
     seg = orc.gen_block(99, L, L).tobytes()
