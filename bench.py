@@ -34,8 +34,12 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--blocks", type=int, default=16384, help="4 MiB blocks per GPU (16384 = 64 GiB)")
     ap.add_argument("--block-bytes", type=int, default=BLOCK)
-    ap.add_argument("--mode", choices=["seal", "open", "crc", "decrypt"], default="seal",
-                    help="decrypt = dataEncryptor.Decrypt end to end: batched RSA-OAEP key unwrap + Open + CRC verify")
+    ap.add_argument("--mode", choices=["seal", "open", "crc", "decrypt", "agg"], default="seal",
+                    help="decrypt = dataEncryptor.Decrypt end to end: batched RSA-OAEP key unwrap + Open + CRC verify; "
+                         "agg = one-block Seal calls from --threads threads on pinned host blocks, through the "
+                         "aggregator (jfsx_agg) and, for comparison, as direct one-block batches")
+    ap.add_argument("--threads", type=int, default=32, help="agg: submitting threads (reference: goroutines)")
+    ap.add_argument("--agg-window-us", type=int, default=500, help="agg: aggregation window")
     ap.add_argument("--algo", choices=["aes256gcm", "chacha20poly1305"], default="aes256gcm")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
@@ -110,6 +114,8 @@ def main():
     from juicefs_amd import engine as E
 
     eng = E.Engine(local, E.CTX_BITSLICE if args.aes == "bitslice" else 0)
+    if args.mode == "agg":
+        return agg_bench(args, world, rank, local, dist, eng)
     if args.mem == "host":
         return host_ingest(args, world, rank, local, dist, eng)
     nb, L = args.blocks, args.block_bytes
@@ -388,6 +394,102 @@ def host_ingest(args, world, rank, local, dist, eng):
     eng.free_pinned(hin)
     eng.free_pinned(hout)
     eng.free_pinned(hcrc)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def agg_bench(args, world, rank, local, dist, eng):
+    """The reference's call shape: every object is sealed by its own
+    synchronous call (dataEncryptor.Encrypt, encrypt.go:164-194) from one of
+    many goroutines (max-uploads, cmd/flags.go:126-127).  Blocks live in pinned
+    host memory (JFSX_MEM_HOST).  value = plaintext GB/s with the calls going
+    through the aggregator (jfsx_agg); direct = the same calls as one-block
+    jfsx_seal_batch calls (serialised on the context)."""
+    import ctypes
+    import threading
+    import numpy as np
+    from juicefs_amd import engine as E
+    nb, L = min(args.blocks, 1024), args.block_bytes
+    nseg = -(-L // E.SEG)
+    algo = E.AES256GCM if args.algo == "aes256gcm" else E.CHACHA20P1305
+    hin, hout, hcrc = eng.alloc_pinned(nb * L), eng.alloc_pinned(nb * L), eng.alloc_pinned(nb * 4 * nseg)
+    tmp = eng.alloc(L)
+    base = rank * nb
+    for b in range(nb):
+        eng.gen_synthetic(tmp, L, SEED, base + b)
+        eng.sync()
+        eng.L.jfsx_memcpy_d2h(eng.ctx, hin + b * L, tmp.ptr, L)
+    tmp.free()
+    specs = []
+    for b in range(nb):
+        key, nonce = E.gen_key(SEED, base + b)
+        specs.append({"key": key, "nonce": nonce, "src": hin + b * L, "dst": hout + b * L, "len": L,
+                      "crc": hcrc + 4 * nseg * b})
+    blks, n = eng.make_blocks(specs)
+    T = args.threads
+
+    def run(call, steps):
+        errs = []
+
+        def worker(t):
+            try:
+                for _ in range(steps):
+                    for b in range(t, nb, T):
+                        call(b)
+            except BaseException as e:  # noqa: B902 -- reported below
+                errs.append(e)
+        ts = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+        t0 = time.perf_counter()
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        if errs:
+            raise errs[0]
+        return time.perf_counter() - t0
+
+    def direct(b):
+        eng._check(eng.L.jfsx_seal_batch(eng.ctx, algo, 1, ctypes.byref(blks[b]), E.CRC_GEN, E.MEM_HOST), "seal")
+
+    d_steps = max(1, args.steps // 5)
+    run(direct, 1)
+    d_el = run(direct, d_steps)
+    with E.Aggregator(eng, window_us=args.agg_window_us) as agg:
+        def through(b):
+            agg.seal(algo, blks[b], E.CRC_GEN, E.MEM_HOST)
+        run(through, args.warmup)
+        c0, b0, k0 = agg.stats()
+        barrier(dist)
+        el = max_over_ranks(dist, run(through, args.steps), local)
+        c1, b1, k1 = agg.stats()
+    verified = 0
+    if args.verify:
+        from oracle import oracle as orc
+        for b in range(0, nb, max(1, nb // args.verify))[:args.verify]:
+            p = orc.gen_block(SEED, base + b, L)
+            key, nonce = orc.gen_key(SEED, base + b)
+            c, tag = orc.seal(orc.AES256GCM if algo == E.AES256GCM else orc.CHACHA20P1305, key, nonce, p, fast=True)
+            got = np.ctypeslib.as_array((ctypes.c_uint8 * L).from_address(hout + b * L)).tobytes()
+            if bytes(blks[b].tag) != tag or got != c:
+                raise SystemExit("bench: block %d differs from the oracle" % b)
+            verified += 1
+    value = world * nb * L * args.steps / el / 1e9
+    if rank == 0:
+        print(json.dumps({
+            "metric": "per-object sealed+checksummed GB/s, %d threads, 4 MiB host blocks (aggregator)" % T,
+            "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic (SplitMix64), pinned host memory",
+            "config": {"workload": "%d one-block Seal calls per step from %d threads, %s + CRC32C full, JFSX_MEM_HOST"
+                                   % (nb, T, args.algo), "blocks_per_gpu": nb, "block_bytes": L, "algo": args.algo,
+                       "mode": "agg", "window_us": args.agg_window_us},
+            "aggregator": {"calls": c1 - c0, "batches": b1 - b0,
+                           "mean_batch_blocks": round((k1 - k0) / max(b1 - b0, 1), 2)},
+            "direct_one_block_calls_GBs": round(nb * L * d_steps / d_el / 1e9, 2),
+            "roofline": None, "cpu_baseline": None, "verified_blocks": verified}), flush=True)
+    for h in (hin, hout, hcrc):
+        eng.free_pinned(h)
     eng.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define JFSX_ABI_VERSION 2
+#define JFSX_ABI_VERSION 3
 
 /* algorithms (encrypt.go:142-145) */
 #define JFSX_AES256GCM 0     /* "aes256gcm-rsa" (also the "" default)   */
@@ -77,6 +77,7 @@ extern "C" {
 #define JFSX_ENODEV (-19)
 #define JFSX_EIO (-5)
 #define JFSX_ENOMEM (-12)
+#define JFSX_EAGAIN (-11) /* jfsx_wait: not finished within the timeout     */
 #define JFSX_EMISFORMED (-74) /* "misformed ciphertext: %d %d" (encrypt.go:199-201) */
 
 typedef struct jfsx_ctx jfsx_ctx;
@@ -152,6 +153,40 @@ int jfsx_open_batch(jfsx_ctx *ctx, int algo, int n, jfsx_blk *blks, int crc_mode
  * volumes, staging re-read).  mode = JFSX_CRC_GEN or JFSX_CRC_VERIFY. */
 int jfsx_crc32c_segments(jfsx_ctx *ctx, int n, jfsx_range *ranges, int mode, int mem);
 
+/* Asynchronous variants: the batch is queued on the context's worker thread
+ * (batches of one context run in submission order) and the call returns a
+ * ticket at once.  blks/ranges and every buffer they name must stay valid
+ * until jfsx_wait has returned for the ticket.  jfsx_wait returns the batch's
+ * return code (as the synchronous call would) and retires the ticket;
+ * timeout_ms < 0 waits without limit, 0 polls; JFSX_EAGAIN if the batch has
+ * not finished in time (the ticket stays live).  jfsx_ctx_close runs the
+ * queued batches before it releases the context. */
+typedef uint64_t jfsx_ticket;
+int jfsx_seal_batch_async(jfsx_ctx *ctx, int algo, int n, jfsx_blk *blks, int crc_mode, int mem, jfsx_ticket *t);
+int jfsx_open_batch_async(jfsx_ctx *ctx, int algo, int n, jfsx_blk *blks, int crc_mode, int mem, jfsx_ticket *t);
+int jfsx_crc32c_segments_async(jfsx_ctx *ctx, int n, jfsx_range *ranges, int mode, int mem, jfsx_ticket *t);
+int jfsx_wait(jfsx_ctx *ctx, jfsx_ticket t, int timeout_ms);
+
+/* Aggregator: per-block calls in the reference's shape --
+ * one synchronous Encrypt / Decrypt / cache-read verify per goroutine
+ * (encrypt.go:164-216, disk_cache.go:1315-1327) -- coalesced into batches.
+ * jfsx_agg_seal / _open / _crc32c block the calling thread until its block
+ * is done and return what a one-block batch would (per-block results in
+ * blk->status or range->status).  Any number of threads may call at once.  A
+ * dispatcher thread groups waiting requests with the same (op, algo, mode,
+ * mem) and issues one batch when the group reaches max_blocks (0: 256) or
+ * max_bytes (0: 1 GiB), or when the oldest request has waited window_us.  A
+ * request the engine rejects (JFSX_EINVAL) fails alone: the batch is retried
+ * one request at a time.  Free the aggregator before closing its context. */
+typedef struct jfsx_agg jfsx_agg;
+int jfsx_agg_new(jfsx_ctx *ctx, int max_blocks, uint64_t max_bytes, uint32_t window_us, jfsx_agg **out);
+int jfsx_agg_free(jfsx_agg *agg);
+int jfsx_agg_seal(jfsx_agg *agg, int algo, jfsx_blk *blk, int crc_mode, int mem);
+int jfsx_agg_open(jfsx_agg *agg, int algo, jfsx_blk *blk, int crc_mode, int mem);
+int jfsx_agg_crc32c(jfsx_agg *agg, jfsx_range *range, int mode, int mem);
+/* requests taken, batches issued, requests those batches carried */
+int jfsx_agg_stats(jfsx_agg *agg, uint64_t *calls, uint64_t *batches, uint64_t *blocks);
+
 /* checksum(data) on the GPU: out receives 4*max(1,ceil(len/32K)) bytes.
  * data and out are host memory. */
 int jfsx_checksum(jfsx_ctx *ctx, const void *data, uint64_t len, uint8_t *out);
@@ -189,8 +224,6 @@ int jfsx_data_decrypt(jfsx_ctx *ctx, int algo, const uint8_t key[32], const void
 uint32_t jfsx_crc32c_update(uint32_t crc, const void *data, uint64_t n);
 /* CRC32C of A||B from crc(A), crc(B), len(B) (GF(2) shift by x^(8 len B)) */
 uint32_t jfsx_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
-/* object-store checksum of header || C || tag (checksum.go:31-53) from the
- * big-endian 32 KiB segment CRCs of C that a GEN|CT batch returned */
 /* Batched RSA-OAEP key unwrap: replaces, per object,
  * rsaEncryptor.Decrypt = rsa.DecryptOAEP(sha256, rand, priv, wrapped,
  * label) (pkg/object/encrypt.go:124-134, called at :207-210) for every object
@@ -207,6 +240,8 @@ int jfsx_rsa_key_free(jfsx_rsa_key *key);
 int jfsx_rsa_oaep_decrypt_batch(jfsx_ctx *ctx, const jfsx_rsa_key *key, int n, const uint8_t *ct, uint64_t ct_stride,
                                 const uint32_t *ct_len, uint8_t *msg, uint64_t msg_stride, int32_t *msg_len);
 
+/* object-store checksum of header || C || tag (checksum.go:31-53) from the
+ * big-endian 32 KiB segment CRCs of C that a GEN|CT batch returned */
 int jfsx_object_crc32c(const void *hdr, uint64_t hlen, const uint8_t *seg_crcs, uint64_t clen,
                        const uint8_t *tag, uint32_t *out);
 

@@ -385,14 +385,20 @@ int run_aead(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mo
 int run_aead_host(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mode) {
     int rc = check_aead_args(algo, n, blks, crc_mode, false);
     if (rc || n == 0) return rc;
-    // group blocks into slots
+    // group blocks into slots; a batch smaller than the ring is cut into about
+    // 2*kRing slots (>= 16 MiB each) so that its copies and transforms still
+    // overlap -- the aggregator's batches are tens of MiB
     std::vector<std::pair<int, int>> groups;  // [b0, b1)
     {
+        size_t total = 0;
+        for (int i = 0; i < n; i++)
+            total += align256(blks[i].len) + (crc_mode ? align256(4 * nseg_of(blks[i].len)) : 0);
+        const size_t slot = std::min(c->slot_bytes, std::max<size_t>((size_t)16 << 20, total / (2 * kRing)));
         int b0 = 0;
         size_t acc = 0;
         for (int i = 0; i < n; i++) {
             const size_t need = align256(blks[i].len) + (crc_mode ? align256(4 * nseg_of(blks[i].len)) : 0);
-            if (i > b0 && acc + need > c->slot_bytes) {
+            if (i > b0 && acc + need > slot) {
                 groups.push_back({b0, i});
                 b0 = i;
                 acc = 0;
@@ -684,6 +690,7 @@ int jfsx_ctx_open(int device, uint32_t flags, jfsx_ctx **out) {
 
 int jfsx_ctx_close(jfsx_ctx *c) {
     if (!c) return JFSX_EINVAL;
+    async_detach(c);  // queued _async batches run first (jfsx_agg.cpp)
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
     if (c->d_tab) (void)hipFree(c->d_tab);

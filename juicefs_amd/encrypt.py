@@ -263,11 +263,15 @@ class DataEncryptor:
 
     keyLen = 32
 
-    def __init__(self, keyEncryptor, algo, eng=None, rand=os.urandom):
+    def __init__(self, keyEncryptor, algo, eng=None, rand=os.urandom, agg=None):
+        """agg: an engine.Aggregator; one-object Encrypt/Decrypt calls made
+        concurrently from many threads (the reference's per-goroutine calls)
+        are then coalesced into engine batches."""
         self.keyEncryptor = keyEncryptor
         self.algo = algo
         self._eng = eng
         self._rand = rand
+        self._agg = agg
 
     @property
     def eng(self):
@@ -309,7 +313,11 @@ class DataEncryptor:
         if not specs:
             return []
         arr, n = self.eng.make_blocks(specs)
-        self.eng.seal_batch(self.algo, arr, n, E.CRC_GEN | E.CRC_CT if checksums else E.CRC_NONE, E.MEM_HOST)
+        mode = E.CRC_GEN | E.CRC_CT if checksums else E.CRC_NONE
+        if self._agg is not None and n == 1:
+            self._agg.seal(self.algo, arr[0], mode, E.MEM_HOST)
+        else:
+            self.eng.seal_batch(self.algo, arr, n, mode, E.MEM_HOST)
         objs = [hdrs[i] + outs[i][1][:outs[i][2]].tobytes() + bytes(arr[i].tag) for i in range(n)]
         if not checksums:
             return objs
@@ -376,8 +384,11 @@ class DataEncryptor:
             specs.append(spec)
         if specs:
             arr, cnt = self.eng.make_blocks(specs)
-            self.eng.open_batch(self.algo, arr, cnt, E.CRC_GEN | E.CRC_CT if checksums is not None else E.CRC_NONE,
-                                E.MEM_HOST)
+            mode = E.CRC_GEN | E.CRC_CT if checksums is not None else E.CRC_NONE
+            if self._agg is not None and cnt == 1:
+                self._agg.open(self.algo, arr[0], mode, E.MEM_HOST)
+            else:
+                self.eng.open_batch(self.algo, arr, cnt, mode, E.MEM_HOST)
             for k, i in enumerate(idx):
                 if checksums is not None and segs[k][2] not in (None, ""):
                     sb, hdr, want = segs[k]
@@ -392,11 +403,11 @@ class DataEncryptor:
         return res
 
 
-def NewDataEncryptor(keyEncryptor, algo, eng=None):
+def NewDataEncryptor(keyEncryptor, algo, eng=None, agg=None):
     """encrypt.go:147-162."""
     if algo not in _ALGO:
         raise EncryptError("unsupport cipher: %s" % algo)
-    return DataEncryptor(keyEncryptor, _ALGO[algo], eng)
+    return DataEncryptor(keyEncryptor, _ALGO[algo], eng, agg=agg)
 
 
 # ---------------------------------------------------------------------------

@@ -20,7 +20,7 @@ CRC_CT = 4  # flag: segment CRCs over the ciphertext (object checksum)
 CTX_BITSLICE = 1  # context flag: AES-GCM keystream from the bitsliced AES (VALU)
 MEM_DEVICE, MEM_HOST = 0, 1
 OK, ETAG, ECRC = 0, 1, 2
-EINVAL, ENODEV, EIO, ENOMEM, EMISFORMED = -22, -19, -5, -12, -74
+EINVAL, ENODEV, EIO, ENOMEM, EMISFORMED, EAGAIN = -22, -19, -5, -12, -74, -11
 SEG = 32 << 10
 
 # every symbol include/jfsx.h declares (checked by tests/test_abi.py)
@@ -32,6 +32,8 @@ EXPORTS = [
     "jfsx_data_encrypt", "jfsx_data_decrypt", "jfsx_parse_header", "jfsx_gen_synthetic", "jfsx_gen_key",
     "jfsx_debug_tables", "jfsx_crc32c_update", "jfsx_crc32c_combine", "jfsx_object_crc32c",
     "jfsx_rsa_key_new", "jfsx_rsa_key_free", "jfsx_rsa_oaep_decrypt_batch",
+    "jfsx_seal_batch_async", "jfsx_open_batch_async", "jfsx_crc32c_segments_async", "jfsx_wait",
+    "jfsx_agg_new", "jfsx_agg_free", "jfsx_agg_seal", "jfsx_agg_open", "jfsx_agg_crc32c", "jfsx_agg_stats",
 ]
 
 
@@ -107,6 +109,16 @@ def load_library(path=LIB_PATH):
             "jfsx_rsa_key_new": (I, [P, P, P, P, P, P, I, P, I, PP]),
             "jfsx_rsa_key_free": (I, [P]),
             "jfsx_rsa_oaep_decrypt_batch": (I, [P, P, I, P, U64, P, P, U64, P]),
+            "jfsx_seal_batch_async": (I, [P, I, I, ctypes.POINTER(jfsx_blk), I, I, ctypes.POINTER(U64)]),
+            "jfsx_open_batch_async": (I, [P, I, I, ctypes.POINTER(jfsx_blk), I, I, ctypes.POINTER(U64)]),
+            "jfsx_crc32c_segments_async": (I, [P, I, ctypes.POINTER(jfsx_range), I, I, ctypes.POINTER(U64)]),
+            "jfsx_wait": (I, [P, U64, I]),
+            "jfsx_agg_new": (I, [P, I, U64, U32, PP]),
+            "jfsx_agg_free": (I, [P]),
+            "jfsx_agg_seal": (I, [P, I, ctypes.POINTER(jfsx_blk), I, I]),
+            "jfsx_agg_open": (I, [P, I, ctypes.POINTER(jfsx_blk), I, I]),
+            "jfsx_agg_crc32c": (I, [P, ctypes.POINTER(jfsx_range), I, I]),
+            "jfsx_agg_stats": (I, [P, ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -281,6 +293,32 @@ class Engine:
     def crc32c_segments(self, ranges, n, mode=CRC_GEN, mem=MEM_DEVICE):
         self._check(self.L.jfsx_crc32c_segments(self.ctx, n, ranges, mode, mem), "jfsx_crc32c_segments")
 
+    # -- asynchronous batches (jfsx_*_async + jfsx_wait) ------------------
+    def _ticket(self, fn, what, *args):
+        t = ctypes.c_uint64()
+        self._check(fn(self.ctx, *args, ctypes.byref(t)), what)
+        return t.value
+
+    def seal_batch_async(self, algo, blks, n, crc_mode=CRC_GEN, mem=MEM_DEVICE):
+        """Queue a seal batch; returns a ticket for wait().  blks and the
+        buffers must stay alive until wait() returns."""
+        return self._ticket(self.L.jfsx_seal_batch_async, "jfsx_seal_batch_async", algo, n, blks, crc_mode, mem)
+
+    def open_batch_async(self, algo, blks, n, crc_mode=CRC_NONE, mem=MEM_DEVICE):
+        return self._ticket(self.L.jfsx_open_batch_async, "jfsx_open_batch_async", algo, n, blks, crc_mode, mem)
+
+    def crc32c_segments_async(self, ranges, n, mode=CRC_GEN, mem=MEM_DEVICE):
+        return self._ticket(self.L.jfsx_crc32c_segments_async, "jfsx_crc32c_segments_async", n, ranges, mode, mem)
+
+    def wait(self, ticket, timeout_ms=-1):
+        """Return code of the batch (raises on a batch-level error); False if
+        it has not finished within timeout_ms (the ticket stays live)."""
+        rc = self.L.jfsx_wait(self.ctx, ticket, timeout_ms)
+        if rc == EAGAIN:
+            return False
+        self._check(rc, "jfsx_wait")
+        return True
+
     # -- host-memory conveniences -------------------------------------------
     def seal(self, algo, key, nonce, plaintext, crc=False):
         """Seal one host buffer; returns (ciphertext, tag[, crc bytes])."""
@@ -436,3 +474,45 @@ class ChecksumError(Exception):
     def __init__(self, got, expect, seg=-1):
         super().__init__("data checksum %d != expect %d" % (got, expect))
         self.got, self.expect, self.seg = got, expect, seg
+
+
+class Aggregator:
+    """jfsx_agg: per-block calls from many threads coalesced into batches
+    (SURVEY §8f-2).  Each method blocks its caller until that block is done,
+    like dataEncryptor.Encrypt/Decrypt (encrypt.go:164-216) or the verify in
+    cacheFile.ReadAt (disk_cache.go:1315-1327); ctypes drops the GIL for the
+    wait, so Python threads submit concurrently."""
+
+    def __init__(self, eng, max_blocks=0, max_bytes=0, window_us=200):
+        self.eng = eng
+        self.L = eng.L
+        h = ctypes.c_void_p()
+        eng._check(self.L.jfsx_agg_new(eng.ctx, max_blocks, max_bytes, window_us, ctypes.byref(h)), "jfsx_agg_new")
+        self.h = h.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.jfsx_agg_free(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def seal(self, algo, blk, crc_mode=CRC_GEN, mem=MEM_HOST):
+        """blk: a jfsx_blk (results are written into it); returns 0 or raises."""
+        self.eng._check(self.L.jfsx_agg_seal(self.h, algo, ctypes.byref(blk), crc_mode, mem), "jfsx_agg_seal")
+
+    def open(self, algo, blk, crc_mode=CRC_NONE, mem=MEM_HOST):
+        self.eng._check(self.L.jfsx_agg_open(self.h, algo, ctypes.byref(blk), crc_mode, mem), "jfsx_agg_open")
+
+    def crc32c(self, rng, mode=CRC_VERIFY, mem=MEM_HOST):
+        self.eng._check(self.L.jfsx_agg_crc32c(self.h, ctypes.byref(rng), mode, mem), "jfsx_agg_crc32c")
+
+    def stats(self):
+        """(calls, batches, blocks carried by those batches)"""
+        v = [ctypes.c_uint64() for _ in range(3)]
+        self.eng._check(self.L.jfsx_agg_stats(self.h, *[ctypes.byref(x) for x in v]), "jfsx_agg_stats")
+        return tuple(x.value for x in v)

@@ -1,0 +1,234 @@
+"""Scheduling logic of the aggregator and the async queue
+(juicefs_amd/csrc/jfsx_agg.cpp), compiled for the host over stub batch entry
+points (tests/harness/agg_host.cpp): many threads making the reference's
+one-block synchronous calls (dataEncryptor.Encrypt/Decrypt,
+pkg/object/encrypt.go:164-216; the cache-read verify, disk_cache.go:1315-1327)
+must come out as few, well-formed batches, each caller getting exactly its own
+result.  The GPU behaviour of the same code is in tests/test_gpu_agg.py."""
+import ctypes
+import os
+import subprocess
+import threading
+
+import pytest
+
+from juicefs_amd import engine as E
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+FAKE_CTX = ctypes.c_void_p(0x1000)
+
+
+@pytest.fixture(scope="module")
+def H(tmp_path_factory):
+    out = str(tmp_path_factory.mktemp("agg") / "agg_host.so")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wall", "-I", os.path.join(ROOT, "include"),
+                           "-o", out, os.path.join(HERE, "harness", "agg_host.cpp"), "-lpthread"])
+    L = ctypes.CDLL(out)
+    P, I, U64, U32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32
+    BP = ctypes.POINTER(E.jfsx_blk)
+    for name, res, args in [
+        ("jfsx_agg_new", I, [P, I, U64, U32, ctypes.POINTER(P)]),
+        ("jfsx_agg_free", I, [P]),
+        ("jfsx_agg_seal", I, [P, I, BP, I, I]),
+        ("jfsx_agg_open", I, [P, I, BP, I, I]),
+        ("jfsx_agg_crc32c", I, [P, ctypes.POINTER(E.jfsx_range), I, I]),
+        ("jfsx_agg_stats", I, [P, ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
+        ("jfsx_seal_batch_async", I, [P, I, I, BP, I, I, ctypes.POINTER(U64)]),
+        ("jfsx_open_batch_async", I, [P, I, I, BP, I, I, ctypes.POINTER(U64)]),
+        ("jfsx_wait", I, [P, U64, I]),
+        ("harness_reset", None, [I]),
+        ("harness_batches", I, [P, P, P, I]),
+        ("harness_close", None, [P]),
+    ]:
+        f = getattr(L, name)
+        f.restype, f.argtypes = res, args
+    return L
+
+
+def batches(H):
+    cap = 100000
+    s, o, m = (ctypes.c_int * cap)(), (ctypes.c_int * cap)(), (ctypes.c_int * cap)()
+    n = H.harness_batches(s, o, m, cap)
+    return [(s[i], o[i], m[i]) for i in range(n)]
+
+
+def fake_tag(key, length, algo):
+    return bytes(key[k] ^ ((length >> (8 * (k & 7))) & 255) ^ algo for k in range(16))
+
+
+def mkblk(i, length):
+    b = E.jfsx_blk()
+    key = bytes((i * 31 + k) & 255 for k in range(32))
+    ctypes.memmove(b.key, key, 32)
+    b.len = length
+    return b, key
+
+
+def new_agg(H, max_blocks=0, max_bytes=0, window_us=2000):
+    h = ctypes.c_void_p()
+    assert H.jfsx_agg_new(FAKE_CTX, max_blocks, max_bytes, window_us, ctypes.byref(h)) == 0
+    return h
+
+
+def stats(H, h):
+    v = [ctypes.c_uint64() for _ in range(3)]
+    assert H.jfsx_agg_stats(h, *[ctypes.byref(x) for x in v]) == 0
+    return tuple(x.value for x in v)
+
+
+def run_threads(n, fn):
+    errs = []
+
+    def wrap(i):
+        try:
+            fn(i)
+        except BaseException as e:  # noqa: B902 -- reported below
+            errs.append(e)
+
+    ts = [threading.Thread(target=wrap, args=(i,)) for i in range(n)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    if errs:
+        raise errs[0]
+
+
+def test_concurrent_seals_coalesce_and_return_own_results(H):
+    H.harness_reset(3000)
+    h = new_agg(H, window_us=5000)
+    N, PER = 32, 8
+    got = {}
+
+    def worker(t):
+        for j in range(PER):
+            i = t * PER + j
+            b, key = mkblk(i, 1000 + i)
+            assert H.jfsx_agg_seal(h, E.AES256GCM, ctypes.byref(b), E.CRC_GEN, E.MEM_HOST) == 0
+            assert b.status == E.OK
+            got[i] = (bytes(b.tag), fake_tag(key, 1000 + i, E.AES256GCM))
+
+    run_threads(N, worker)
+    assert all(a == e for a, e in got.values()) and len(got) == N * PER
+    calls, nb, blocks = stats(H, h)
+    assert calls == blocks == N * PER
+    assert nb < calls // 4, (calls, nb)  # coalesced, not one batch per call
+    bs = batches(H)
+    assert sum(s for s, _, _ in bs) == N * PER and all(op == 0 and m == E.CRC_GEN for _, op, m in bs)
+    assert H.jfsx_agg_free(h) == 0
+
+
+def test_groups_never_mix_ops_or_modes(H):
+    H.harness_reset(1000)
+    h = new_agg(H, window_us=3000)
+    res = {}
+
+    def worker(i):
+        b, key = mkblk(i, 4096 + i)
+        kind = i % 3
+        if kind == 0:
+            rc = H.jfsx_agg_seal(h, E.CHACHA20P1305, ctypes.byref(b), E.CRC_NONE, E.MEM_HOST)
+        elif kind == 1:
+            ctypes.memmove(b.tag, fake_tag(key, 4096 + i, E.AES256GCM) if i % 2 else bytes(16), 16)
+            rc = H.jfsx_agg_open(h, E.AES256GCM, ctypes.byref(b), E.CRC_VERIFY, E.MEM_HOST)
+        else:
+            r = E.jfsx_range()
+            r.len = i
+            rc = H.jfsx_agg_crc32c(h, ctypes.byref(r), E.CRC_VERIFY, E.MEM_HOST)
+            res[i] = (rc, r.status)
+            return
+        res[i] = (rc, b.status)
+
+    run_threads(60, worker)
+    for i, (rc, st) in res.items():
+        assert rc == 0
+        if i % 3 == 1:
+            assert st == (E.OK if i % 2 else E.ETAG), i
+        elif i % 3 == 2:
+            assert st == (E.ECRC if i % 7 == 3 else E.OK), i
+    ops = {op for _, op, _ in batches(H)}
+    assert ops == {0, 1, 2}
+    calls, nb, blocks = stats(H, h)
+    assert calls == blocks == 60 and nb >= 3
+    H.jfsx_agg_free(h)
+
+
+def test_max_blocks_and_max_bytes_cap_batches(H):
+    H.harness_reset(2000)
+    h = new_agg(H, max_blocks=5, window_us=20000)
+    run_threads(40, lambda i: H.jfsx_agg_seal(h, 0, ctypes.byref(mkblk(i, 100)[0]), 0, E.MEM_HOST))
+    assert max(s for s, _, _ in batches(H)) <= 5
+    H.jfsx_agg_free(h)
+    H.harness_reset(2000)
+    h = new_agg(H, max_bytes=3000, window_us=20000)
+    run_threads(40, lambda i: H.jfsx_agg_seal(h, 0, ctypes.byref(mkblk(i, 1000)[0]), 0, E.MEM_HOST))
+    assert max(s for s, _, _ in batches(H)) <= 3
+    H.jfsx_agg_free(h)
+
+
+def test_lone_request_leaves_after_window(H):
+    H.harness_reset(0)
+    h = new_agg(H, window_us=1000)
+    b, key = mkblk(7, 77)
+    assert H.jfsx_agg_seal(h, 0, ctypes.byref(b), 0, E.MEM_HOST) == 0
+    assert bytes(b.tag) == fake_tag(key, 77, 0)
+    assert stats(H, h) == (1, 1, 1)
+    H.jfsx_agg_free(h)
+
+
+def test_invalid_request_fails_alone(H):
+    H.harness_reset(1000)
+    h = new_agg(H, window_us=5000)
+    rcs = {}
+
+    def worker(i):
+        b, _ = mkblk(i, 500)
+        b.reserved = 1 if i == 5 else 0  # the stub engine rejects this block
+        rcs[i] = H.jfsx_agg_seal(h, 0, ctypes.byref(b), 0, E.MEM_HOST)
+
+    run_threads(16, worker)
+    assert rcs[5] == E.EINVAL
+    assert all(rc == 0 for i, rc in rcs.items() if i != 5)
+    # argument errors the aggregator sees itself never reach the engine
+    b, _ = mkblk(0, 1)
+    assert H.jfsx_agg_seal(h, 9, ctypes.byref(b), 0, E.MEM_HOST) == E.EINVAL
+    assert H.jfsx_agg_seal(h, 0, ctypes.byref(b), 0, 5) == E.EINVAL
+    H.jfsx_agg_free(h)
+
+
+def test_async_tickets_order_poll_and_close(H):
+    H.harness_reset(20000)
+    ctx = ctypes.c_void_p(0x2000)
+    arrs, tickets = [], []
+    for k in range(4):
+        arr = (E.jfsx_blk * 3)()
+        for i in range(3):
+            ctypes.memmove(arr[i].key, bytes([k * 3 + i]) * 32, 32)
+            arr[i].len = 10 * k + i
+        t = ctypes.c_uint64()
+        assert H.jfsx_seal_batch_async(ctx, 1, 3, arr, 0, E.MEM_DEVICE, ctypes.byref(t)) == 0
+        arrs.append(arr)
+        tickets.append(t.value)
+    assert len(set(tickets)) == 4
+    assert H.jfsx_wait(ctx, tickets[3], 0) == E.EAGAIN  # 4 x 20 ms queued: not done yet
+    assert H.jfsx_wait(ctx, tickets[3], -1) == 0
+    for t in tickets[:3]:
+        assert H.jfsx_wait(ctx, t, -1) == 0  # earlier batches finished first (FIFO)
+    assert H.jfsx_wait(ctx, tickets[0], 0) == E.EINVAL  # retired
+    for k, arr in enumerate(arrs):
+        for i in range(3):
+            assert bytes(arr[i].tag) == fake_tag(bytes([k * 3 + i]) * 32, 10 * k + i, 1)
+    # a batch the engine rejects reports through jfsx_wait
+    bad = (E.jfsx_blk * 1)()
+    bad[0].reserved = 1
+    t = ctypes.c_uint64()
+    assert H.jfsx_open_batch_async(ctx, 0, 1, bad, 0, E.MEM_DEVICE, ctypes.byref(t)) == 0
+    assert H.jfsx_wait(ctx, t.value, -1) == E.EINVAL
+    # close runs what is still queued
+    arr = (E.jfsx_blk * 1)()
+    arr[0].len = 5
+    assert H.jfsx_seal_batch_async(ctx, 0, 1, arr, 0, E.MEM_DEVICE, ctypes.byref(t)) == 0
+    H.harness_close(ctx)
+    assert bytes(arr[0].tag) == fake_tag(bytes(32), 5, 0)
+    assert H.jfsx_wait(ctx, t.value, 0) == E.EINVAL

@@ -1,0 +1,178 @@
+"""GPU parity of the asynchronous batches (jfsx_*_async + jfsx_wait) and of
+the aggregator (jfsx_agg): many threads making one-block synchronous calls,
+as dataEncryptor.Encrypt/Decrypt (pkg/object/encrypt.go:164-216) and the
+cache-read verify (pkg/chunk/disk_cache.go:1315-1327) are made, get results
+bit-identical to the oracle while the engine sees a few large batches."""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+from juicefs_amd import encrypt as enc
+from juicefs_amd import engine as E
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+ORC = {E.AES256GCM: orc.AES256GCM, E.CHACHA20P1305: orc.CHACHA20P1305}
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = E.Engine(0)
+    yield e
+    e.close()
+
+
+def run_threads(n, fn):
+    errs = []
+
+    def wrap(i):
+        try:
+            fn(i)
+        except BaseException as e:  # noqa: B902 -- re-raised below
+            errs.append(e)
+
+    ts = [threading.Thread(target=wrap, args=(i,)) for i in range(n)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    if errs:
+        raise errs[0]
+
+
+@pytest.mark.parametrize("algo", [E.AES256GCM, E.CHACHA20P1305])
+def test_async_batches_match_oracle(eng, algo):
+    lens = [[0, 17, 32768], [4 << 20, 100003], [65536 + 5, 1, 2 << 20]]
+    jobs = []
+    for bi, group in enumerate(lens):
+        specs, keep = [], []
+        for i, n in enumerate(group):
+            p = orc.gen_block(31, 10 * bi + i, n)
+            src, dst = eng.alloc(max(n, 16)), eng.alloc(max(n, 16))
+            if n:
+                src.upload(p)
+            crc = eng.alloc(4 * max(1, -(-n // E.SEG)))
+            key, nonce = orc.gen_key(31, 10 * bi + i)
+            specs.append({"key": key, "nonce": nonce, "src": src.ptr, "dst": dst.ptr, "len": n, "crc": crc.ptr})
+            keep.append((p, key, nonce, src, dst, crc))
+        arr, cnt = eng.make_blocks(specs)
+        t = eng.seal_batch_async(algo, arr, cnt, E.CRC_GEN, E.MEM_DEVICE)
+        jobs.append((t, arr, keep))
+    for t, arr, keep in reversed(jobs):  # any wait order
+        assert eng.wait(t) is True
+        for i, (p, key, nonce, src, dst, crc) in enumerate(keep):
+            c, tag = orc.seal(ORC[algo], key, nonce, p, fast=True)
+            assert bytes(arr[i].tag) == tag and arr[i].status == E.OK
+            if p.size:
+                assert dst.download(p.size).tobytes() == c
+            want = orc.checksum(p)
+            assert crc.download(len(want)).tobytes() == want
+    with pytest.raises(E.EngineError):
+        eng.wait(jobs[0][0])  # retired ticket
+
+
+def test_async_poll_and_batch_error(eng):
+    n = 64 << 20
+    src, dst = eng.alloc(n), eng.alloc(n)
+    arr, cnt = eng.make_blocks([{"key": bytes(32), "nonce": bytes(12), "src": src.ptr, "dst": dst.ptr, "len": n}])
+    t = eng.seal_batch_async(E.AES256GCM, arr, cnt, E.CRC_NONE, E.MEM_DEVICE)
+    first = eng.wait(t, 0)
+    assert first in (True, False)
+    if first is False:
+        assert eng.wait(t) is True
+    bad, cnt = eng.make_blocks([{"key": bytes(32), "nonce": bytes(12), "src": src.ptr + 1, "dst": dst.ptr,
+                                 "len": 64}])  # unaligned device pointer -> EINVAL at run time
+    t = eng.open_batch_async(E.AES256GCM, bad, cnt, E.CRC_NONE, E.MEM_DEVICE)
+    with pytest.raises(E.EngineError) as ei:
+        eng.wait(t)
+    assert ei.value.code == E.EINVAL
+
+
+@pytest.mark.parametrize("algo", [E.AES256GCM, E.CHACHA20P1305])
+def test_aggregator_concurrent_encrypt_decrypt(eng, algo):
+    rng = np.random.default_rng(algo + 3)
+    lens = [int(x) for x in rng.integers(0, 1 << 20, 96)] + [4 << 20, 0, 1, 32768]
+    N = len(lens)
+    plains = [orc.gen_block(41, i, n) for i, n in enumerate(lens)]
+    keys = [orc.gen_key(41, i) for i in range(N)]
+    out = [None] * N
+    with E.Aggregator(eng, window_us=2000) as agg:
+        def seal(i):
+            p = plains[i]
+            c = np.empty(max(p.size, 1), np.uint8)
+            cs = np.zeros(4 * max(1, -(-p.size // E.SEG)), np.uint8)
+            arr, _ = eng.make_blocks([{"key": keys[i][0], "nonce": keys[i][1], "src": p.ctypes.data if p.size else None,
+                                       "dst": c.ctypes.data, "len": p.size, "crc": cs.ctypes.data}])
+            agg.seal(algo, arr[0], E.CRC_GEN, E.MEM_HOST)
+            assert arr[0].status == E.OK
+            out[i] = (c[:p.size].copy(), bytes(arr[0].tag), cs.tobytes())
+
+        run_threads(N, seal)
+        calls, batches, blocks = agg.stats()
+        assert calls == blocks == N and batches < N
+        for i in range(N):
+            c, tag = orc.seal(ORC[algo], keys[i][0], keys[i][1], plains[i], fast=True)
+            assert out[i][0].tobytes() == c and out[i][1] == tag, i
+            assert out[i][2][:len(orc.checksum(plains[i]))] == orc.checksum(plains[i])
+
+        # Decrypt side: in place, one block tampered -> only it fails
+        res = [None] * N
+
+        def open_(i):
+            c, tag, cs = out[i]
+            if i == 7:
+                tag = bytes([tag[0] ^ 1]) + tag[1:]
+            buf = c.copy()
+            arr, _ = eng.make_blocks([{"key": keys[i][0], "nonce": keys[i][1], "src": buf.ctypes.data if buf.size else None,
+                                       "dst": buf.ctypes.data if buf.size else None, "len": buf.size, "tag": tag,
+                                       "crc": np.frombuffer(cs, np.uint8).ctypes.data}])
+            agg.open(algo, arr[0], E.CRC_VERIFY, E.MEM_HOST)
+            res[i] = (arr[0].status, buf)
+
+        run_threads(N, open_)
+        for i in range(N):
+            st, buf = res[i]
+            if i == 7:
+                assert st == E.ETAG
+            else:
+                assert st == E.OK and buf[:lens[i]].tobytes() == plains[i].tobytes(), i
+
+
+def test_aggregator_crc_verify(eng):
+    lens = [32768 * 3 + 5, 1 << 20, 7, 0]
+    datas = [orc.gen_block(51, i, n) for i, n in enumerate(lens)]
+    sums = [bytearray(orc.checksum(d)) for d in datas]
+    sums[1][9] ^= 0x10  # segment 2 of range 1 has a wrong expected CRC
+    res = {}
+    with E.Aggregator(eng, window_us=1000) as agg:
+        def verify(i):
+            r = E.jfsx_range()
+            d = datas[i]
+            cs = (ctypes.c_uint8 * len(sums[i])).from_buffer(sums[i])
+            r.data, r.len, r.crc = d.ctypes.data if d.size else None, d.size, ctypes.addressof(cs)
+            agg.crc32c(r, E.CRC_VERIFY, E.MEM_HOST)
+            res[i] = (r.status, r.bad_seg)
+
+        run_threads(len(lens), verify)
+    assert res[1] == (E.ECRC, 2)
+    assert all(res[i][0] == E.OK for i in (0, 2, 3))
+
+
+def test_data_encryptor_through_aggregator(eng):
+    """dataEncryptor.Encrypt/Decrypt called per object from 24 threads, the
+    way cachedStore's upload and read goroutines call them, round-trip and
+    reach the engine as a few batches."""
+    rsae = enc.NewRSAEncryptor(enc.GenerateRsaKey(2048))
+    plains = [orc.gen_block(61, i, (i * 77777) % (1 << 20)).tobytes() for i in range(48)]
+    objs, back = [None] * 48, [None] * 48
+    with E.Aggregator(eng, window_us=3000) as agg:
+        de = enc.NewDataEncryptor(rsae, "aes256gcm-rsa", eng, agg=agg)
+        run_threads(48, lambda i: objs.__setitem__(i, de.Encrypt(plains[i])))
+        run_threads(48, lambda i: back.__setitem__(i, de.Decrypt(objs[i])))
+        calls, batches, blocks = agg.stats()
+    assert back == plains
+    assert calls == 96 and batches < 96
+    plain_de = enc.NewDataEncryptor(rsae, "aes256gcm-rsa", eng)
+    assert [plain_de.Decrypt(o) for o in objs[:4]] == plains[:4]
