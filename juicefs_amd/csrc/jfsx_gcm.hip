@@ -50,6 +50,15 @@ __device__ __forceinline__ uint32_t rotl8(uint32_t x) { return __builtin_amdgcn_
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
+// round key i as the T-table rounds consume it (pre-rotated for rounds 2..13, see AES_COL)
+__device__ __forceinline__ uint32_t rk_load(const uint32_t *rk, int i) {
+    uint32_t k = rk[i];
+    if (JFSX_RKR && i >= 8 && i < 56) {
+        k = (k >> 8) | (k << 24);
+        OPAQUE(k);  // keep it in an SGPR (a VALU rotate would cost 48 VGPRs)
+    }
+    return k;
+}
 
 // byte k of w moved to bits 8..15, the lane's replica offset (bits 0..7) and the
 // table base (bit 16) taken from loff: the LDS byte address of T0[byte] for this
@@ -61,8 +70,16 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 // One full AES round on LE column words.  T1 = rotl8 T0 and T3 = rotl8 T2, and
 // rotl8(a) ^ rotl8(b) = rotl8(a ^ b), so a column costs 4 v_perm (addresses),
 // 4 ds_read_b32, one xor, one alignbit and one 3-input xor (v_bitop3 0x96).
+#if JFSX_RKR
+// rounds 2..13 hold their round keys pre-rotated (rk_load: rotr8), so the key
+// joins the rotated pair's 3-input XOR and a column is 4 v_perm, 4 ds_read_b32,
+// two v_bitop3 and one alignbit
+#define AES_COL(o, i0, i1, i2, i3, rkv) \
+    o = xor3(TA(i0, 0), TB(i2, 2), rotl8(xor3(TA(i1, 1), TB(i3, 3), (rkv))));
+#else
 #define AES_COL(o, i0, i1, i2, i3, rkv) \
     o = xor3(TA(i0, 0), TB(i2, 2), rotl8(TA(i1, 1) ^ TB(i3, 3))) ^ (rkv);
+#endif
 #define AES_ROUND(o0, o1, o2, o3, i0, i1, i2, i3, r) \
     AES_COL(o0, i0, i1, i2, i3, rk[4 * (r) + 0])     \
     AES_COL(o1, i1, i2, i3, i0, rk[4 * (r) + 1])     \
@@ -92,6 +109,66 @@ __device__ __forceinline__ void aes_ctr_blocks(const char *lds, uint32_t loff, c
     }
 #pragma unroll
     for (int r = 2; r <= 13; r += 2) {
+#pragma unroll
+        for (int s = 0; s < NS; s++) { AES_ROUND(b[s][0], b[s][1], b[s][2], b[s][3], a[s][0], a[s][1], a[s][2], a[s][3], r); }
+#pragma unroll
+        for (int s = 0; s < NS; s++) { AES_ROUND(a[s][0], a[s][1], a[s][2], a[s][3], b[s][0], b[s][1], b[s][2], b[s][3], r + 1); }
+    }
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        AES_LAST(ks[s][0], a[s][0], a[s][1], a[s][2], a[s][3], rk[56]);
+        AES_LAST(ks[s][1], a[s][1], a[s][2], a[s][3], a[s][0], rk[57]);
+        AES_LAST(ks[s][2], a[s][2], a[s][3], a[s][0], a[s][1], rk[58]);
+        AES_LAST(ks[s][3], a[s][3], a[s][0], a[s][1], a[s][2], rk[59]);
+    }
+}
+
+// Counter-uniform rounds.  Within one 1 KiB row the 64 counters are C + lane,
+// so the counter's upper 24 bits U are wave-uniform except for the lanes past a
+// carry.  After round 1 only column 0 (the one fed by the counter's low byte)
+// varies with the low byte; columns 1..3 depend on U alone, and so do 12 of
+// round 2's 16 lookups.  aes_r2_uniform gives, for one U, round 2's per-column
+// sum of those 12 lookups and the round key; a wave computes a window of 64 U
+// values once (lane l <-> U0 + l) and each row reads its lanes' entries with
+// v_readlane.  A row then needs 5 table lookups for rounds 1-2 instead of 20.
+__device__ __forceinline__ void aes_r2_uniform(const char *lds, uint32_t loff, const uint32_t *rk, const uint32_t *k1,
+                                               uint32_t U, uint32_t (&u)[4]) {
+    const uint32_t x3 = __builtin_bswap32(U << 8) ^ rk[3];
+    const uint32_t a1 = k1[1] ^ TB(x3, 2);
+    const uint32_t a2 = k1[2] ^ rotl8(TA(x3, 1));
+    const uint32_t a3 = k1[3] ^ TA(x3, 0);
+#if JFSX_RKR
+    u[0] = xor3(TB(a2, 2), rotl8(xor3(TA(a1, 1), TB(a3, 3), rk[8])), 0u);
+    u[1] = xor3(TA(a1, 0), TB(a3, 2), rotl8(TA(a2, 1) ^ rk[9]));
+    u[2] = xor3(TA(a2, 0), rotl8(xor3(TA(a3, 1), TB(a1, 3), rk[10])), 0u);
+    u[3] = xor3(TA(a3, 0), TB(a1, 2), rotl8(TB(a2, 3) ^ rk[11]));
+#else
+    u[0] = xor3(TB(a2, 2), rotl8(TA(a1, 1) ^ TB(a3, 3)), rk[8]);
+    u[1] = xor3(TA(a1, 0), TB(a3, 2), rotl8(TA(a2, 1))) ^ rk[9];
+    u[2] = xor3(TA(a2, 0), rotl8(TA(a3, 1) ^ TB(a1, 3)), rk[10]);
+    u[3] = xor3(TA(a3, 0), TB(a1, 2), rotl8(TB(a2, 3))) ^ rk[11];
+#endif
+}
+
+// aes_ctr_blocks with rounds 1-2 taken from the lane's counter-uniform terms u.
+template <int NS>
+__device__ __forceinline__ void aes_ctr_blocks_u(const char *lds, uint32_t loff, const uint32_t *rk,
+                                                 const uint32_t *k1, const uint32_t (&ctr)[NS],
+                                                 const uint32_t (&u)[NS][4], uint32_t (&ks)[NS][4]) {
+    uint32_t a[NS][4], b[NS][4];
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        const uint32_t x3 = __builtin_bswap32(ctr[s]) ^ rk[3];
+        const uint32_t a0 = k1[0] ^ rotl8(TB(x3, 3));
+        b[s][0] = u[s][0] ^ TA(a0, 0);
+        b[s][1] = u[s][1] ^ rotl8(TB(a0, 3));
+        b[s][2] = u[s][2] ^ TB(a0, 2);
+        b[s][3] = u[s][3] ^ rotl8(TA(a0, 1));
+    }
+#pragma unroll
+    for (int s = 0; s < NS; s++) { AES_ROUND(a[s][0], a[s][1], a[s][2], a[s][3], b[s][0], b[s][1], b[s][2], b[s][3], 3); }
+#pragma unroll
+    for (int r = 4; r <= 13; r += 2) {
 #pragma unroll
         for (int s = 0; s < NS; s++) { AES_ROUND(b[s][0], b[s][1], b[s][2], b[s][3], a[s][0], a[s][1], a[s][2], a[s][3], r); }
 #pragma unroll
@@ -244,7 +321,7 @@ __device__ __noinline__ Stream row_generic(const char *lds, uint32_t loff, const
                                            uint64_t row) {
     uint32_t rk[60];
 #pragma unroll
-    for (int i = 0; i < 60; i++) rk[i] = sch->rk[i];
+    for (int i = 0; i < 60; i++) rk[i] = rk_load(sch->rk, i);
     const uint32_t k1[4] = {sch->k1[0], sch->k1[1], sch->k1[2], sch->k1[3]};
     const uint64_t o = row + 16 * lane;
     const uint64_t end = st.sub1;
@@ -433,7 +510,7 @@ __global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *
     // read here, after the bitsliced loop, so it holds no SGPRs through it
     uint32_t rk[60];
 #pragma unroll
-    for (int i = 0; i < 60; i++) rk[i] = sch->rk[i];
+    for (int i = 0; i < 60; i++) rk[i] = rk_load(sch->rk, i);
     uint32_t k1[4] = {sch->k1[0], sch->k1[1], sch->k1[2], sch->k1[3]};
     uint4 nxt[NS];
 #pragma unroll
@@ -445,6 +522,11 @@ __global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *
     if (NS == 1 && act[0] && rf >= r0 + 2) {
         uint4 n0 = gld16(src + ld0[0] + 1024 * r0 + lo);
         uint4 n1 = gld16(src + ld0[0] + 1024 * (r0 + 1) + lo);
+#if JFSX_UCTR
+        uint32_t uw[4] = {0, 0, 0, 0};
+        uint32_t uw0 = 0;
+        bool uwok = false;
+#endif
         for (; r0 + 1 < rf; r0 += 2) {
             const uint4 dd[2] = {n0, n1};
             const uint64_t o0 = ld0[0] + 1024 * r0 + lo;
@@ -454,7 +536,35 @@ __global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *
             }
             const uint32_t ctr2[2] = {(uint32_t)((o0 >> 4) + 2), (uint32_t)((o0 >> 4) + 66)};
             uint32_t ks2[2][4];
+#if JFSX_UCTR
+            {
+                // row counters C and C + 64 (C = the row's lane-0 counter, wave-uniform)
+                uint32_t C = (uint32_t)(((ld0[0] + 1024 * r0) >> 4) + 2);
+                OPAQUE(C);
+                // the window must hold U(C) .. U(C + 64 + 63)
+                if (!uwok || (C >> 8) < uw0 || ((C + 127) >> 8) - uw0 > 63u) {
+                    uw0 = C >> 8;
+                    aes_r2_uniform(lds, loff, rk, k1, uw0 + lane, uw);
+                    uwok = true;
+                }
+                uint32_t u2[2][4];
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const uint32_t Cr = C + 64u * u;
+                    const uint32_t i0 = (Cr >> 8) - uw0;
+                    const bool cy = (Cr & 255u) + lane >= 256u;
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const uint32_t lo_ = __builtin_amdgcn_readlane(uw[k], i0);
+                        const uint32_t hi_ = __builtin_amdgcn_readlane(uw[k], i0 + 1);
+                        u2[u][k] = cy ? hi_ : lo_;
+                    }
+                }
+                aes_ctr_blocks_u<2>(lds, loff, rk, k1, ctr2, u2, ks2);
+            }
+#else
             aes_ctr_blocks<2>(lds, loff, rk, k1, ctr2, ks2);
+#endif
 #pragma unroll
             for (int u = 0; u < 2; u++) {
                 const uint64_t o = o0 + 1024 * u;

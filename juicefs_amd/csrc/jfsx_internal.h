@@ -36,7 +36,15 @@ constexpr int kThreads = kWaves * 64;
 #ifndef JFSX_U2
 #define JFSX_U2 1
 #endif
-constexpr int kStreams = JFSX_STREAMS;         // independent segment streams per wave (ILP)
+// Counter-uniform rounds 1-2 in the two-row loop (aes_r2_uniform, jfsx_gcm.hip).
+#ifndef JFSX_UCTR
+#define JFSX_UCTR 1
+#endif
+// T-table rounds 2..13 with pre-rotated round keys folded into a v_bitop3 (AES_COL).
+#ifndef JFSX_RKR
+#define JFSX_RKR 1
+#endif
+constexpr int kStreams = JFSX_STREAMS;        // independent segment streams per wave (ILP)
 constexpr int kSlotsPerTask = kWaves * kStreams;  // GHASH/Poly partial slots per task
 constexpr int kMaxTaskBytes = 4 << 20;
 constexpr uint32_t kCrcPoly = 0x82F63B78u;  // reflected Castagnoli
