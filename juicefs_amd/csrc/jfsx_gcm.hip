@@ -193,6 +193,7 @@ struct GhLane {
     uint32_t sel[4];  // v_perm selectors: byte0 <- off byte t&3, byte1 <- R[t/4] byte (t + l) & 3
     uint32_t off[4];  // j(t) << 4 for t = 4*dd + 0..3, one byte each
     bool r1, r2;      // rotation bits of k
+    uint32_t p1, p2;  // the same bits as v_perm selectors (whole dword from src0 or src1)
 };
 
 __device__ __forceinline__ GhLane gh_lane(uint32_t lane) {
@@ -212,6 +213,8 @@ __device__ __forceinline__ GhLane gh_lane(uint32_t lane) {
     }
     g.r1 = (k & 1) != 0;
     g.r2 = (k & 2) != 0;
+    g.p1 = g.r1 ? 0x07060504u : 0x03020100u;
+    g.p2 = g.r2 ? 0x07060504u : 0x03020100u;
     return g;
 }
 
@@ -219,9 +222,10 @@ __device__ __forceinline__ GhLane gh_lane(uint32_t lane) {
 __device__ __forceinline__ void gh_rho(const uint32_t a[4], const GhLane &g, uint32_t R[4]) {
     uint32_t u[4];
 #pragma unroll
-    for (int i = 0; i < 4; i++) u[i] = g.r2 ? a[(i + 2) & 3] : a[i];
+    // v_perm with a per-lane whole-dword selector: no VCC to rebuild per select
+    for (int i = 0; i < 4; i++) u[i] = JFSX_GHPERM ? PERM(a[(i + 2) & 3], a[i], g.p2) : (g.r2 ? a[(i + 2) & 3] : a[i]);
 #pragma unroll
-    for (int i = 0; i < 4; i++) R[i] = g.r1 ? u[(i + 1) & 3] : u[i];
+    for (int i = 0; i < 4; i++) R[i] = JFSX_GHPERM ? PERM(u[(i + 1) & 3], u[i], g.p1) : (g.r1 ? u[(i + 1) & 3] : u[i]);
 }
 // a = rho^-1(R): a[i] = R[(i - k) & 3]
 __device__ __forceinline__ void gh_rho_inv(const uint32_t R[4], const GhLane &g, uint32_t a[4]) {

@@ -40,6 +40,10 @@ constexpr int kThreads = kWaves * 64;
 #ifndef JFSX_UCTR
 #define JFSX_UCTR 1
 #endif
+// GHASH accumulator rotation (gh_rho) by v_perm selectors instead of v_cndmask.
+#ifndef JFSX_GHPERM
+#define JFSX_GHPERM 1
+#endif
 // T-table rounds 2..13 with pre-rotated round keys folded into a v_bitop3 (AES_COL).
 #ifndef JFSX_RKR
 #define JFSX_RKR 1
