@@ -11,7 +11,27 @@ __device__ __forceinline__ uint4 lds_u4(const char *lds, uint32_t byteaddr) {
     return *reinterpret_cast<const uint4 *>(lds + byteaddr);
 }
 
+// 4 * byte k of x in one VALU op: v_lshlrev_b32 with an SDWA byte select on the
+// shifted operand.  With the table base below 64 KiB the base folds into the
+// ds_read offset, so a table lookup costs one VALU op instead of two or three.
+#if JFSX_CRCSDWA
+template <int K>
+__device__ __forceinline__ uint32_t byte_x4(uint32_t x) {
+    uint32_t r;
+    if constexpr (K == 0)
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(x));
+    else if constexpr (K == 1)
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(x));
+    else if constexpr (K == 2)
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(x));
+    else
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(x));
+    return r;
+}
+#define CRC_T(t, x, k) lds_u32(lds, byte_x4<(k)>(x) + CB + 1024u * (t))
+#else
 #define CRC_T(t, x, k) lds_u32(lds, ((((x) >> (8 * (k))) & 0xffu) << 2) + CB + 1024u * (t))
+#endif
 
 // crc_raw(A, 16-byte piece) = crc_raw(0, piece ^ shift(A, 1008 B) in the first word)
 // S = 16: shift by 1008 B first; S = 20: shift by 4032 B; S < 0: no shift

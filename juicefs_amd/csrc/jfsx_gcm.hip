@@ -37,13 +37,17 @@
 namespace jfsx {
 
 // ---------------------------------------------------------------------------
-// LDS map of gcm_main (bytes): [0, 64K) AES T0|T2, [64K, 128K) GHASH table,
-// [128K, 148K) CRC tables, [148K, +2K) GHASH basis staging.
+// LDS map of gcm_main (bytes): [0, 20K) CRC tables, [20K, 84K) GHASH table,
+// [84K, 148K) AES T0|T2, [148K, +2K) GHASH basis staging.  Every table's base
+// is reached through the 16-bit ds_read offset: the CRC and GHASH bases
+// directly, the AES base as 0x10000 (bit 16 of the lane's v_perm operand loff)
+// plus the offset 20K.  So no lookup spends a VALU op on its base.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kLdsGh = 0;       // GHASH T[b][j]: byte (b << 8) | (j << 4)
-constexpr uint32_t kLdsAes = 65536;  // AES [idx][T0 x32 | T2 x32]: byte 65536 | (idx << 8) | (r << 2)
-constexpr uint32_t kLdsCrc = 131072;
-constexpr uint32_t kLdsBasis = 131072 + 20480;
+constexpr uint32_t kLdsCrc = 0;
+constexpr uint32_t kLdsGh = 20480;              // GHASH T[b][j]: kLdsGh + (b << 8) | (j << 4)
+constexpr uint32_t kLdsAesOff = 20480;          // ds_read offset of the AES table
+constexpr uint32_t kLdsAes = 65536 + kLdsAesOff;  // AES [idx][T0 x32 | T2 x32]: 0x10000 | (idx << 8) | (r << 2), + offset
+constexpr uint32_t kLdsBasis = kLdsAes + 65536;
 constexpr uint32_t kLdsBytes = kLdsBasis + 2048;
 
 __device__ __forceinline__ uint32_t rotl8(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 24); }
@@ -64,8 +68,8 @@ __device__ __forceinline__ uint32_t rk_load(const uint32_t *rk, int i) {
 // table base (bit 16) taken from loff: the LDS byte address of T0[byte] for this
 // lane's replica in one v_perm_b32
 #define AES_SEL(k) (0x0c020000u | ((4u + (k)) << 8))
-#define TA(w, k) lds_u32(lds, __builtin_amdgcn_perm((w), loff, AES_SEL(k)))
-#define TB(w, k) lds_u32(lds, __builtin_amdgcn_perm((w), loff, AES_SEL(k)) + 128u)
+#define TA(w, k) lds_u32(lds, __builtin_amdgcn_perm((w), loff, AES_SEL(k)) + kLdsAesOff)
+#define TB(w, k) lds_u32(lds, __builtin_amdgcn_perm((w), loff, AES_SEL(k)) + (kLdsAesOff + 128u))
 
 // One full AES round on LE column words.  T1 = rotl8 T0 and T3 = rotl8 T2, and
 // rotl8(a) ^ rotl8(b) = rotl8(a ^ b), so a column costs 4 v_perm (addresses),

@@ -44,6 +44,10 @@ constexpr int kThreads = kWaves * 64;
 #ifndef JFSX_GHPERM
 #define JFSX_GHPERM 1
 #endif
+// CRC table addresses by an SDWA byte-select shift (byte_x4, jfsx_dev.h).
+#ifndef JFSX_CRCSDWA
+#define JFSX_CRCSDWA 1
+#endif
 // T-table rounds 2..13 with pre-rotated round keys folded into a v_bitop3 (AES_COL).
 #ifndef JFSX_RKR
 #define JFSX_RKR 1
