@@ -154,7 +154,8 @@ __device__ __forceinline__ void aes_r2_uniform(const char *lds, uint32_t loff, c
 #endif
 }
 
-// aes_ctr_blocks with rounds 1-2 taken from the lane's counter-uniform terms u.
+// aes_ctr_blocks with rounds 1-2 taken from the lane's counter-uniform terms u;
+// ks comes out without the last round key (rk[56..59]).
 template <int NS>
 __device__ __forceinline__ void aes_ctr_blocks_u(const char *lds, uint32_t loff, const uint32_t *rk,
                                                  const uint32_t *k1, const uint32_t (&ctr)[NS],
@@ -180,10 +181,11 @@ __device__ __forceinline__ void aes_ctr_blocks_u(const char *lds, uint32_t loff,
     }
 #pragma unroll
     for (int s = 0; s < NS; s++) {
-        AES_LAST(ks[s][0], a[s][0], a[s][1], a[s][2], a[s][3], rk[56]);
-        AES_LAST(ks[s][1], a[s][1], a[s][2], a[s][3], a[s][0], rk[57]);
-        AES_LAST(ks[s][2], a[s][2], a[s][3], a[s][0], a[s][1], rk[58]);
-        AES_LAST(ks[s][3], a[s][3], a[s][0], a[s][1], a[s][2], rk[59]);
+        // the last round key is left out: the caller folds it into the data XOR
+        AES_LAST(ks[s][0], a[s][0], a[s][1], a[s][2], a[s][3], 0u);
+        AES_LAST(ks[s][1], a[s][1], a[s][2], a[s][3], a[s][0], 0u);
+        AES_LAST(ks[s][2], a[s][2], a[s][3], a[s][0], a[s][1], 0u);
+        AES_LAST(ks[s][3], a[s][3], a[s][0], a[s][1], a[s][2], 0u);
     }
 }
 
@@ -576,8 +578,14 @@ __global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *
 #pragma unroll
             for (int u = 0; u < 2; u++) {
                 const uint64_t o = o0 + 1024 * u;
+#if JFSX_UCTR
+                // data ^ keystream ^ last round key in one v_bitop3
+                const uint4 x = make_uint4(xor3(dd[u].x, ks2[u][0], rk[56]), xor3(dd[u].y, ks2[u][1], rk[57]),
+                                           xor3(dd[u].z, ks2[u][2], rk[58]), xor3(dd[u].w, ks2[u][3], rk[59]));
+#else
                 const uint4 x = make_uint4(dd[u].x ^ ks2[u][0], dd[u].y ^ ks2[u][1], dd[u].z ^ ks2[u][2],
                                            dd[u].w ^ ks2[u][3]);
+#endif
                 const uint4 c = OPEN ? dd[u] : x, p = OPEN ? x : dd[u];
                 gst16(dst + o, OPEN ? p : c);
                 const uint4 cq = crc_src<CRCMODE>(c, p);
