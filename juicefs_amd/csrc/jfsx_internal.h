@@ -26,10 +26,10 @@ constexpr int kThreads = kWaves * 64;
 #define JFSX_STREAMS 1
 #endif
 // GHASH table walk issued in groups of lookups with a scheduling fence between
-// them (lower peak VGPRs): 4 = four quarters of 4 (default), 1 = two halves of
-// 8, 0 = all 16 at once.
+// them (lower peak VGPRs): 4 = four quarters of 4, 1 = two halves of 8
+// (default; +0.7% over quarters once the VALU trims landed), 0 = all 16 at once.
 #ifndef JFSX_GH8
-#define JFSX_GH8 4
+#define JFSX_GH8 1
 #endif
 // Two-row unrolled T-table loop (two AES chains interleaved); with the GHASH
 // quarters it fits the 128-VGPR cap (+2% measured).
