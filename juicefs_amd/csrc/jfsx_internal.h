@@ -27,7 +27,8 @@ constexpr int kThreads = kWaves * 64;
 #endif
 // GHASH table walk issued in groups of lookups with a scheduling fence between
 // them (lower peak VGPRs): 4 = four quarters of 4, 1 = two halves of 8
-// (default; +0.7% over quarters once the VALU trims landed), 0 = all 16 at once.
+// (default; +0.7% over quarters at 8 GiB, equal at 64 GiB, fewer spills),
+// 0 = all 16 at once.
 #ifndef JFSX_GH8
 #define JFSX_GH8 1
 #endif
