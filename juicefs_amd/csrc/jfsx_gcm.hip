@@ -159,17 +159,21 @@ __device__ __forceinline__ void aes_r2_uniform(const char *lds, uint32_t loff, c
 template <int NS>
 __device__ __forceinline__ void aes_ctr_blocks_u(const char *lds, uint32_t loff, const uint32_t *rk,
                                                  const uint32_t *k1, const uint32_t (&ctr)[NS],
-                                                 const uint32_t (&u)[NS][4], uint32_t (&ks)[NS][4]) {
+                                                 const uint32_t (&u)[NS][4], const uint32_t (&du)[NS][4],
+                                                 const uint32_t (&cym)[NS], uint32_t (&ks)[NS][4]) {
     uint32_t a[NS][4], b[NS][4];
+    // u, du wave-uniform (SGPR operands); carry lanes (cym = ~0) add du = u(U) ^ u(U + 1)
+#define UC(t, w) (__builtin_amdgcn_bitop3_b32((t), cym[s], du[s][w], 0x78) ^ u[s][w]) /* t ^ (cym & du) ^ u */
 #pragma unroll
     for (int s = 0; s < NS; s++) {
         const uint32_t x3 = __builtin_bswap32(ctr[s]) ^ rk[3];
         const uint32_t a0 = k1[0] ^ rotl8(TB(x3, 3));
-        b[s][0] = u[s][0] ^ TA(a0, 0);
-        b[s][1] = u[s][1] ^ rotl8(TB(a0, 3));
-        b[s][2] = u[s][2] ^ TB(a0, 2);
-        b[s][3] = u[s][3] ^ rotl8(TA(a0, 1));
+        b[s][0] = UC(TA(a0, 0), 0);
+        b[s][1] = UC(rotl8(TB(a0, 3)), 1);
+        b[s][2] = UC(TB(a0, 2), 2);
+        b[s][3] = UC(rotl8(TA(a0, 1)), 3);
     }
+#undef UC
 #pragma unroll
     for (int s = 0; s < NS; s++) { AES_ROUND(a[s][0], a[s][1], a[s][2], a[s][3], b[s][0], b[s][1], b[s][2], b[s][3], 3); }
 #pragma unroll
@@ -557,20 +561,20 @@ __global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *
                     aes_r2_uniform(lds, loff, rk, k1, uw0 + lane, uw);
                     uwok = true;
                 }
-                uint32_t u2[2][4];
+                uint32_t u2[2][4], d2[2][4], cym[2];
 #pragma unroll
                 for (int u = 0; u < 2; u++) {
                     const uint32_t Cr = C + 64u * u;
                     const uint32_t i0 = (Cr >> 8) - uw0;
-                    const bool cy = (Cr & 255u) + lane >= 256u;
+                    // ~0 on the lanes whose counter carried into U + 1, else 0
+                    cym[u] = (uint32_t)__builtin_amdgcn_sbfe((int)((Cr & 255u) + lane), 8, 1);
 #pragma unroll
                     for (int k = 0; k < 4; k++) {
-                        const uint32_t lo_ = __builtin_amdgcn_readlane(uw[k], i0);
-                        const uint32_t hi_ = __builtin_amdgcn_readlane(uw[k], i0 + 1);
-                        u2[u][k] = cy ? hi_ : lo_;
+                        u2[u][k] = __builtin_amdgcn_readlane(uw[k], i0);
+                        d2[u][k] = u2[u][k] ^ __builtin_amdgcn_readlane(uw[k], i0 + 1);
                     }
                 }
-                aes_ctr_blocks_u<2>(lds, loff, rk, k1, ctr2, u2, ks2);
+                aes_ctr_blocks_u<2>(lds, loff, rk, k1, ctr2, u2, d2, cym, ks2);
             }
 #else
             aes_ctr_blocks<2>(lds, loff, rk, k1, ctr2, ks2);
