@@ -8,10 +8,13 @@ the whole batch (keysetup + transform + finalize + result copy-back).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--blocks B] [--mode seal|open|crc]
 
-For N > 1 it is launched by torch.distributed.run, one rank per GPU; blocks
-shard across ranks with no collective on the data path (the only collectives
-are the timing barrier and the max-over-ranks reduction).  Rank 0 prints ONE
-JSON line.
+For N > 1 it runs one rank per GPU: either launched by torch.distributed.run
+(the driver's form), or -- when WORLD_SIZE is unset -- it starts that launcher
+itself as a child process before touching any GPU and exits with its code.
+Blocks shard across ranks with no collective on the data path (the only
+collectives are the timing barrier and the max-over-ranks reduction).  Every
+rank checks its own sampled blocks against the oracle; rank 0 prints ONE JSON
+line.
 """
 import argparse
 import json
@@ -52,7 +55,24 @@ def parse():
                     help="configs[4]: block lengths uniform in [64 KiB, 4 MiB] (seeded), non-multiples of 16/64/32768")
     ap.add_argument("--aes", choices=["ttable", "bitslice"], default="ttable",
                     help="AES-GCM keystream kernel: T-table AES in LDS, or bitsliced AES on the VALU")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="test hook: the launcher, process group, shard layout, barrier and max-over-ranks timing "
+                         "with no engine (no GPU); prints the JSON line with value null")
     return ap.parse_args()
+
+
+def spawn_ranks(args):
+    """--gpus N > 1 without a torch.distributed.run environment: start the
+    launcher as a child (one rank per GPU, rendezvous on 127.0.0.1) and return
+    its exit code.  Called before anything initialises the GPU."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def dist_setup(args):
@@ -81,18 +101,43 @@ def ragged_len(seed, block, cap):
     return lo + z % (cap - lo + 1)
 
 
+def host_cores():
+    """(threads to use, note): every core of the affinity mask, capped by the
+    cgroup CPU quota when one is set (threads beyond the quota would only be
+    throttled)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    if quota is not None and quota < aff:
+        return quota, "%d-CPU affinity mask, cgroup quota %d CPUs" % (aff, quota)
+    return aff, "%d-CPU affinity mask" % aff
+
+
 def cpu_baseline(args):
-    """The oracle's AES-NI/PCLMUL + SSE4.2 port of the Go path, timed on this
-    host's cores over a bounded sample of the same workload."""
+    """The reference's per-block CPU work (checksum() + aead.Seal, one worker
+    per core) timed on this host over a bounded sample of the same workload:
+    the AEAD through OpenSSL EVP (AES-NI/VAES + VPCLMULQDQ stitched GCM, SIMD
+    ChaCha20-Poly1305), the CRC32C as 3-stream SSE4.2 like Go's
+    castagnoliSSE42Triple.  Falls back to the oracle's AES-NI port if
+    libcrypto is not loadable."""
     from oracle import oracle as orc
-    threads = min(16, len(os.sched_getaffinity(0)))
+    threads, note = host_cores()
     algo = orc.AES256GCM if args.algo == "aes256gcm" else orc.CHACHA20P1305
     nblk = 256  # 1 GiB: BASELINE.json configs[0]
-    secs, _ = orc.bench_seal_crc(algo, threads, nblk, BLOCK, SEED)
+    fn, impl = orc.bench_seal_crc_evp, "OpenSSL EVP"
+    secs, _ = fn(algo, threads, nblk, BLOCK, SEED)
+    if secs < 0:
+        fn, impl = orc.bench_seal_crc, "oracle AES-NI/PCLMUL port"
+        secs, _ = fn(algo, threads, nblk, BLOCK, SEED)
     reps = max(1, min(64, int(args.cpu_seconds / max(secs, 1e-3))))
     total_s, total_b = 0.0, 0
     for r in range(reps):
-        s, _ = orc.bench_seal_crc(algo, threads, nblk, BLOCK, SEED + r)
+        s, _ = fn(algo, threads, nblk, BLOCK, SEED + r)
         total_s += s
         total_b += nblk * BLOCK
     model = ""
@@ -104,13 +149,39 @@ def cpu_baseline(args):
     except OSError:
         pass
     return {"value": round(total_b / total_s / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": "%d x 1 GiB (256 x 4 MiB blocks) %s seal + CRC32C full, %d threads, %s" %
-                      (reps, args.algo, threads, model)}
+            "sample": "%d x 1 GiB (256 x 4 MiB blocks) %s seal (%s) + CRC32C full (3-stream SSE4.2), "
+                      "%d threads (%s), %s" % (reps, args.algo, impl, threads, note, model)}
+
+
+def dry_run(args, world, rank, local, dist):
+    """No engine: exercises the rank launch, the shard layout, the barrier and
+    the max-over-ranks timing the real bench uses (tests/test_dist_gloo.py)."""
+    from juicefs_amd import shard
+    blocks = shard.shard(args.blocks, rank)
+    barrier(dist)
+    t0 = time.perf_counter()
+    barrier(dist)
+    el = max_over_ranks(dist, time.perf_counter() - t0 + 0.001 * rank, local)
+    first = max_over_ranks(dist, float(blocks[0]), local)
+    if rank == 0:
+        print(json.dumps({"metric": "dry run (no engine)", "value": None, "unit": "GB/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3, 3),
+                          "dry_run": True, "last_rank_first_block": int(first),
+                          "config": {"blocks_per_gpu": args.blocks,
+                                     "parallelism": "block-sharded x%d, no collective" % world}}), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     world, rank, local, dist = dist_setup(args)
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit("bench: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    if args.dry_run:
+        return dry_run(args, world, rank, local, dist)
     from juicefs_amd import engine as E
 
     eng = E.Engine(local, E.CTX_BITSLICE if args.aes == "bitslice" else 0)
@@ -128,9 +199,7 @@ def main():
     # block b occupies slot [b*L, b*L + lens[b]); ragged lengths are a seeded
     # draw per global block index, so every rank and rerun sees the same batch
     lens = [ragged_len(SEED, base + b, L) if args.ragged else L for b in range(nb)]
-    for b in range(nb):
-        eng.gen_synthetic(src, lens[b], SEED, base + b, offset=b * L)
-    eng.sync()
+    eng.gen_synthetic_batch(src, L, lens, SEED, base)  # one launch for the whole batch
 
     if args.mode == "crc":
         ranges = (E.jfsx_range * nb)()

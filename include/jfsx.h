@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define JFSX_ABI_VERSION 3
+#define JFSX_ABI_VERSION 4
 
 /* algorithms (encrypt.go:142-145) */
 #define JFSX_AES256GCM 0     /* "aes256gcm-rsa" (also the "" default)   */
@@ -71,6 +71,7 @@ extern "C" {
 #define JFSX_OK 0
 #define JFSX_ETAG 1 /* AEAD authentication failed (Go: cipher's errOpen)      */
 #define JFSX_ECRC 2 /* "data checksum %d != expect %d" (disk_cache.go:1324)   */
+#define JFSX_EOF 3  /* jfsx_cache_verify: short read (File.ReadAt's io.EOF)    */
 
 /* batch-level errors */
 #define JFSX_EINVAL (-22)
@@ -84,7 +85,15 @@ typedef struct jfsx_ctx jfsx_ctx;
 
 /* One 4 MiB-class block.  For JFSX_MEM_DEVICE batches src/dst must be
  * 16-byte aligned; dst may equal src (in place, as aead.Seal(p[:0]...) and
- * aead.Open(ciphertext[:0]...) are).  Any length 0 .. 2^32-1 is accepted. */
+ * aead.Open(ciphertext[:0]...) are).  Length limits are the ciphers' own
+ * (JFSX_EINVAL beyond them, where Go's Seal panics and Open fails):
+ *   AES-256-GCM        len <= (2^32 - 2) * 16 B  (32-bit block counter from 2;
+ *                      crypto/cipher gcm.go gcmMaxPlaintext)
+ *   ChaCha20-Poly1305  len <= 2^38 - 64 B        (x/crypto v0.19.0
+ *                      chacha20poly1305.go: block counter from 1)
+ * Open with a failed tag (status JFSX_ETAG) releases nothing: dst is zeroed,
+ * as Go's in-place aead.Open (encrypt.go:215) clears out on a mismatch, and a
+ * plaintext CRC_GEN array is zeroed too. */
 typedef struct jfsx_blk {
     uint8_t key[32];      /* data key (encrypt.go:165)                        */
     uint8_t nonce[12];    /* nonce (encrypt.go:177)                           */
@@ -187,6 +196,31 @@ int jfsx_agg_crc32c(jfsx_agg *agg, jfsx_range *range, int mode, int mem);
 /* requests taken, batches issued, requests those batches carried */
 int jfsx_agg_stats(jfsx_agg *agg, uint64_t *calls, uint64_t *batches, uint64_t *blocks);
 
+/* Multi-device context (SURVEY §8b jfsx_open_ctx(dev_mask), §8e): one
+ * jfsx_ctx per selected GPU (bit d of dev_mask = device d; 0 = every visible
+ * device).  Blocks are independent (own key, nonce, tag, CRCs), so a host-
+ * memory batch is cut into one contiguous run of blocks per device, balanced
+ * by bytes, and the runs execute concurrently, one host thread per device; no
+ * device-to-device traffic.  Results land in blks exactly as with a single
+ * context.  Batches on a multi-device context take JFSX_MEM_HOST only (device
+ * pointers belong to one GPU: use that GPU's jfsx_mctx_ctx).  A batch-level
+ * error of any device is returned (the first one, in device order). */
+typedef struct jfsx_mctx jfsx_mctx;
+int jfsx_mctx_open(uint64_t dev_mask, uint32_t flags, jfsx_mctx **out);
+int jfsx_mctx_close(jfsx_mctx *m);
+int jfsx_mctx_ndev(jfsx_mctx *m);                 /* devices in the context   */
+jfsx_ctx *jfsx_mctx_ctx(jfsx_mctx *m, int i);     /* i-th device's context    */
+int jfsx_mctx_seal_batch(jfsx_mctx *m, int algo, int n, jfsx_blk *blks, int crc_mode, int mem);
+int jfsx_mctx_open_batch(jfsx_mctx *m, int algo, int n, jfsx_blk *blks, int crc_mode, int mem);
+int jfsx_mctx_crc32c_segments(jfsx_mctx *m, int n, jfsx_range *ranges, int mode, int mem);
+/* Aggregator over every device of a multi-device context: one dispatcher
+ * thread per device takes the next ready group from one shared queue, so the
+ * per-block callers (≤ max-uploads upload goroutines, cached_store.go:371-472;
+ * readers, :673-748) spread over all GPUs.  Same call semantics as jfsx_agg_new. */
+int jfsx_agg_new_mctx(jfsx_mctx *m, int max_blocks, uint64_t max_bytes, uint32_t window_us, jfsx_agg **out);
+/* batches issued by the aggregator's dispatcher for device slot i */
+int jfsx_agg_dev_batches(jfsx_agg *agg, int i, uint64_t *batches);
+
 /* checksum(data) on the GPU: out receives 4*max(1,ceil(len/32K)) bytes.
  * data and out are host memory. */
 int jfsx_checksum(jfsx_ctx *ctx, const void *data, uint64_t len, uint8_t *out);
@@ -195,7 +229,10 @@ int jfsx_checksum(jfsx_ctx *ctx, const void *data, uint64_t len, uint8_t *out);
  * file image: file = data(length) ‖ BE32 CRCs, level 0 none / 1 full /
  * 2 shrink / 3 extend (the level openCacheFile resolved).  Copies
  * [off, off+size) into out.  Returns 0 ok, JFSX_ECRC on mismatch (got,
- * expect, bad_seg filled), 2 on short read, <0 on argument errors. */
+ * expect, bad_seg filled), JFSX_EOF on a short read, <0 on argument errors.
+ * *n_out is what Go's ReadAt returns as n.  file and out are host memory of
+ * any alignment; the verified window is staged through a per-context pinned
+ * arena (no per-call allocation). */
 int jfsx_cache_verify(jfsx_ctx *ctx, const void *file, uint64_t file_size, uint64_t length, int level,
                       uint64_t off, uint64_t size, void *out, uint64_t *n_out, uint32_t *got,
                       uint32_t *expect, int64_t *bad_seg);
@@ -253,6 +290,11 @@ int jfsx_parse_header(const void *obj, uint64_t olen, int *klen, int *nlen);
  * memory with the SplitMix64 stream of (seed, block) (documented in
  * DESIGN.md; identical to oracle/jfs_oracle.c:orc_gen_block) */
 int jfsx_gen_synthetic(jfsx_ctx *ctx, void *dst, uint64_t len, uint64_t seed, uint64_t block);
+/* batched form: block i (global index block0 + i) is written at
+ * dst + i*stride with lens[i] bytes (lens: host array), one launch for the
+ * whole batch */
+int jfsx_gen_synthetic_batch(jfsx_ctx *ctx, void *dst, uint64_t stride, int n, const uint64_t *lens, uint64_t seed,
+                             uint64_t block0);
 /* fills n keys (32 B) and nonces (12 B) with the same per-block stream as
  * orc_gen_key, host side */
 void jfsx_gen_key(uint64_t seed, uint64_t block, uint8_t key[32], uint8_t nonce[12]);

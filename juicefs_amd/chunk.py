@@ -56,7 +56,7 @@ class CacheFile:
         rc, data, n, got, exp, seg = eng.cache_verify(img, self.length, _LEVEL[self.csLevel], off, size)
         if rc == E.ECRC:
             raise ChecksumError(got, exp, seg)
-        if rc == 2:
+        if rc == E.EOF:
             raise EOFError("EOF")
         return data, n
 

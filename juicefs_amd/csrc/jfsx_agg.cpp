@@ -1,4 +1,5 @@
-// jfsx_agg.cpp -- asynchronous batches and the per-block aggregator (host C++).
+// jfsx_agg.cpp -- asynchronous batches, the per-block aggregator and the
+// multi-device context (host C++; only the public C-ABI below it is used).
 //
 // The reference encrypts and decrypts one block per call, synchronously, from
 // many goroutines at once: Encrypt from up to max-uploads (default 20,
@@ -188,7 +189,7 @@ using jfsx::kOpen;
 using jfsx::kCrc;
 
 struct jfsx_agg {
-    jfsx_ctx *c;
+    std::vector<jfsx_ctx *> cs;  // one dispatcher thread per context (device)
     int max_blocks;
     uint64_t max_bytes;
     std::chrono::microseconds window;
@@ -197,9 +198,10 @@ struct jfsx_agg {
     std::deque<Req *> q;
     bool stop = false;
     uint64_t calls = 0, batches = 0, blocks = 0;
-    std::thread th;
+    std::vector<uint64_t> dev_batches;
+    std::vector<std::thread> ths;
 
-    int call(const std::vector<Req *> &b, size_t i0, size_t n, std::vector<jfsx_blk> &blks,
+    int call(jfsx_ctx *c, const std::vector<Req *> &b, size_t i0, size_t n, std::vector<jfsx_blk> &blks,
              std::vector<jfsx_range> &rng) {
         const Req &h = *b[i0];
         if (h.op == kCrc) return jfsx_crc32c_segments(c, (int)n, rng.data() + i0, h.mode, h.mem);
@@ -210,7 +212,7 @@ struct jfsx_agg {
     // one engine call for the whole group; if the engine rejects the batch
     // (an argument error in one request), every request is retried alone so
     // the error reaches only its own caller
-    void execute(std::vector<Req *> &b) {
+    void execute(jfsx_ctx *c, std::vector<Req *> &b) {
         const size_t n = b.size();
         std::vector<jfsx_blk> blks;
         std::vector<jfsx_range> rng;
@@ -221,9 +223,9 @@ struct jfsx_agg {
             blks.resize(n);
             for (size_t i = 0; i < n; i++) blks[i] = *b[i]->blk;
         }
-        int rc = call(b, 0, n, blks, rng);
+        int rc = call(c, b, 0, n, blks, rng);
         if (rc == JFSX_EINVAL && n > 1) {
-            for (size_t i = 0; i < n; i++) b[i]->rc = call(b, i, 1, blks, rng);
+            for (size_t i = 0; i < n; i++) b[i]->rc = call(c, b, i, 1, blks, rng);
         } else {
             for (size_t i = 0; i < n; i++) b[i]->rc = rc;
         }
@@ -235,26 +237,30 @@ struct jfsx_agg {
         }
     }
 
-    void run() {
+    // Dispatcher k: take the group of the oldest request once it is full (block
+    // or byte cap) or its window has closed, run it on context k.  Several
+    // dispatchers share the queue: after every wait the head is re-read, since
+    // another dispatcher may have taken the group in the meantime.
+    void run(int k) {
         std::unique_lock<std::mutex> lk(mu);
         for (;;) {
             cv_work.wait(lk, [&] { return stop || !q.empty(); });
-            if (q.empty()) return;
-            // wait for the group of the oldest request to fill, or its window to close
-            const Clock::time_point deadline = q.front()->t0 + window;
-            for (;;) {
-                int cnt = 0;
-                uint64_t bytes = 0;
-                for (Req *r : q)
-                    if (r->same(*q.front())) cnt++, bytes += r->bytes;
-                if (stop || cnt >= max_blocks || bytes >= max_bytes || Clock::now() >= deadline) break;
+            if (q.empty()) return;  // stop, and nothing left to run
+            const Req *head = q.front();
+            int cnt = 0;
+            uint64_t bytes = 0;
+            for (Req *r : q)
+                if (r->same(*head)) cnt++, bytes += r->bytes;
+            const Clock::time_point deadline = head->t0 + window;
+            if (!(stop || cnt >= max_blocks || bytes >= max_bytes || Clock::now() >= deadline)) {
                 cv_work.wait_until(lk, deadline);
+                continue;
             }
             std::vector<Req *> b;
-            uint64_t bytes = 0;
-            const Req head = *q.front();
+            bytes = 0;
+            const Req h = *head;
             for (auto it = q.begin(); it != q.end() && (int)b.size() < max_blocks;) {
-                if ((*it)->same(head) && (b.empty() || bytes + (*it)->bytes <= max_bytes)) {
+                if ((*it)->same(h) && (b.empty() || bytes + (*it)->bytes <= max_bytes)) {
                     bytes += (*it)->bytes;
                     b.push_back(*it);
                     it = q.erase(it);
@@ -262,10 +268,12 @@ struct jfsx_agg {
                     ++it;
                 }
             }
+            if (!q.empty()) cv_work.notify_all();  // the next group may be ready for an idle dispatcher
             lk.unlock();
-            execute(b);
+            execute(cs[k], b);
             lk.lock();
             batches++;
+            dev_batches[k]++;
             blocks += b.size();
             for (Req *r : b) r->done = true;
             cv_done.notify_all();
@@ -284,19 +292,26 @@ struct jfsx_agg {
     }
 };
 
+namespace {
+int agg_start(std::vector<jfsx_ctx *> cs, int max_blocks, uint64_t max_bytes, uint32_t window_us, jfsx_agg **out) {
+    jfsx_agg *a = new (std::nothrow) jfsx_agg;
+    if (!a) return JFSX_ENOMEM;
+    a->cs = std::move(cs);
+    a->max_blocks = max_blocks ? max_blocks : 256;
+    a->max_bytes = max_bytes ? max_bytes : (uint64_t)1 << 30;
+    a->window = std::chrono::microseconds(window_us);
+    a->dev_batches.assign(a->cs.size(), 0);
+    for (size_t k = 0; k < a->cs.size(); k++) a->ths.emplace_back([a, k] { a->run((int)k); });
+    *out = a;
+    return 0;
+}
+}  // namespace
+
 extern "C" {
 
 int jfsx_agg_new(jfsx_ctx *c, int max_blocks, uint64_t max_bytes, uint32_t window_us, jfsx_agg **out) {
     if (!c || !out || max_blocks < 0) return JFSX_EINVAL;
-    jfsx_agg *a = new (std::nothrow) jfsx_agg;
-    if (!a) return JFSX_ENOMEM;
-    a->c = c;
-    a->max_blocks = max_blocks ? max_blocks : 256;
-    a->max_bytes = max_bytes ? max_bytes : (uint64_t)1 << 30;
-    a->window = std::chrono::microseconds(window_us);
-    a->th = std::thread([a] { a->run(); });
-    *out = a;
-    return 0;
+    return agg_start({c}, max_blocks, max_bytes, window_us, out);
 }
 
 int jfsx_agg_free(jfsx_agg *a) {
@@ -306,8 +321,16 @@ int jfsx_agg_free(jfsx_agg *a) {
         a->stop = true;
         a->cv_work.notify_all();
     }
-    a->th.join();  // requests already queued run first
+    for (std::thread &t : a->ths) t.join();  // requests already queued run first
     delete a;
+    return 0;
+}
+
+int jfsx_agg_dev_batches(jfsx_agg *a, int i, uint64_t *batches) {
+    if (!a || !batches || i < 0) return JFSX_EINVAL;
+    std::lock_guard<std::mutex> g(a->mu);
+    if ((size_t)i >= a->dev_batches.size()) return JFSX_EINVAL;
+    *batches = a->dev_batches[i];
     return 0;
 }
 
@@ -336,6 +359,125 @@ int jfsx_agg_stats(jfsx_agg *a, uint64_t *calls, uint64_t *batches, uint64_t *bl
     if (batches) *batches = a->batches;
     if (blocks) *blocks = a->blocks;
     return 0;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// multi-device context (SURVEY §8b jfsx_open_ctx(dev_mask), §8e): one jfsx_ctx
+// per GPU, built on the public single-device entry points only
+
+struct jfsx_mctx {
+    std::vector<jfsx_ctx *> cs;
+};
+
+namespace {
+
+// contiguous runs of blocks, one per device, balanced by bytes: run k is
+// [cut[k], cut[k+1]).  With n >= nd every device gets at least one block
+// (a lone giant block still goes to one device).
+std::vector<int> split_runs(int n, int nd, const std::function<uint64_t(int)> &len) {
+    std::vector<int> cut(nd + 1, n);
+    cut[0] = 0;
+    uint64_t total = 0;
+    for (int i = 0; i < n; i++) total += len(i) + 1;  // +1: empty blocks still count
+    uint64_t acc = 0;
+    int i = 0;
+    for (int k = 1; k < nd; k++) {
+        const uint64_t target = total * (uint64_t)k / (uint64_t)nd;
+        const int keep = n - (nd - k);  // leave one block for each later run
+        if (i < n && i == cut[k - 1]) acc += len(i) + 1, i++;  // at least one block per run
+        while (i < keep && acc + (len(i) + 1) / 2 <= target) acc += len(i) + 1, i++;
+        cut[k] = i;
+    }
+    return cut;
+}
+
+// run f(k, b0, b1) for every non-empty run, device 0's on the calling thread
+int fan_out(const std::vector<int> &cut, const std::function<int(int, int, int)> &f) {
+    const int nd = (int)cut.size() - 1;
+    std::vector<int> rc(nd, 0);
+    std::vector<std::thread> th;
+    for (int k = 1; k < nd; k++)
+        if (cut[k + 1] > cut[k]) th.emplace_back([&, k] { rc[k] = f(k, cut[k], cut[k + 1]); });
+    if (cut[1] > cut[0]) rc[0] = f(0, cut[0], cut[1]);
+    for (std::thread &t : th) t.join();
+    for (int k = 0; k < nd; k++)
+        if (rc[k]) return rc[k];
+    return 0;
+}
+
+int mctx_aead(jfsx_mctx *m, bool open, int algo, int n, jfsx_blk *blks, int crc_mode, int mem) {
+    if (!m || n < 0 || (n && !blks)) return JFSX_EINVAL;
+    if (mem != JFSX_MEM_HOST && !(mem == JFSX_MEM_DEVICE && m->cs.size() == 1)) return JFSX_EINVAL;
+    if (n == 0) return 0;
+    const std::vector<int> cut = split_runs(n, (int)m->cs.size(), [&](int i) { return blks[i].len; });
+    return fan_out(cut, [&](int k, int b0, int b1) {
+        return open ? jfsx_open_batch(m->cs[k], algo, b1 - b0, blks + b0, crc_mode, mem)
+                    : jfsx_seal_batch(m->cs[k], algo, b1 - b0, blks + b0, crc_mode, mem);
+    });
+}
+
+}  // namespace
+
+extern "C" {
+
+int jfsx_mctx_open(uint64_t dev_mask, uint32_t flags, jfsx_mctx **out) {
+    if (!out) return JFSX_EINVAL;
+    *out = nullptr;
+    int nd = 0;
+    if (jfsx_device_count(&nd) || nd <= 0) return JFSX_ENODEV;
+    if (nd < 64 && (dev_mask >> nd)) return JFSX_ENODEV;  // a selected device is not visible
+    jfsx_mctx *m = new (std::nothrow) jfsx_mctx;
+    if (!m) return JFSX_ENOMEM;
+    for (int d = 0; d < nd && d < 64; d++) {
+        if (dev_mask && !((dev_mask >> d) & 1)) continue;
+        jfsx_ctx *c = nullptr;
+        const int rc = jfsx_ctx_open(d, flags, &c);
+        if (rc) {
+            jfsx_mctx_close(m);
+            return rc;
+        }
+        m->cs.push_back(c);
+    }
+    *out = m;
+    return 0;
+}
+
+int jfsx_mctx_close(jfsx_mctx *m) {
+    if (!m) return JFSX_EINVAL;
+    for (jfsx_ctx *c : m->cs) jfsx_ctx_close(c);
+    delete m;
+    return 0;
+}
+
+int jfsx_mctx_ndev(jfsx_mctx *m) { return m ? (int)m->cs.size() : 0; }
+
+jfsx_ctx *jfsx_mctx_ctx(jfsx_mctx *m, int i) {
+    return m && i >= 0 && (size_t)i < m->cs.size() ? m->cs[i] : nullptr;
+}
+
+int jfsx_mctx_seal_batch(jfsx_mctx *m, int algo, int n, jfsx_blk *blks, int crc_mode, int mem) {
+    return mctx_aead(m, false, algo, n, blks, crc_mode, mem);
+}
+
+int jfsx_mctx_open_batch(jfsx_mctx *m, int algo, int n, jfsx_blk *blks, int crc_mode, int mem) {
+    return mctx_aead(m, true, algo, n, blks, crc_mode, mem);
+}
+
+int jfsx_mctx_crc32c_segments(jfsx_mctx *m, int n, jfsx_range *ranges, int mode, int mem) {
+    if (!m || n < 0 || (n && !ranges)) return JFSX_EINVAL;
+    if (mem != JFSX_MEM_HOST && !(mem == JFSX_MEM_DEVICE && m->cs.size() == 1)) return JFSX_EINVAL;
+    if (n == 0) return 0;
+    const std::vector<int> cut = split_runs(n, (int)m->cs.size(), [&](int i) { return ranges[i].len; });
+    return fan_out(cut, [&](int k, int b0, int b1) {
+        return jfsx_crc32c_segments(m->cs[k], b1 - b0, ranges + b0, mode, mem);
+    });
+}
+
+int jfsx_agg_new_mctx(jfsx_mctx *m, int max_blocks, uint64_t max_bytes, uint32_t window_us, jfsx_agg **out) {
+    if (!m || m->cs.empty() || !out || max_blocks < 0) return JFSX_EINVAL;
+    return agg_start(m->cs, max_blocks, max_bytes, window_us, out);
 }
 
 }  // extern "C"

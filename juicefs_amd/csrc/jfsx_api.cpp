@@ -159,6 +159,9 @@ struct jfsx_ctx {
     size_t rsa_hcap = 0;
     double ms_total = 0;
     uint64_t launches = 0;
+    std::mutex arena_mu;     // cache-verify staging (jfsx_cache_verify)
+    char *arena = nullptr;   // pinned, grow-only
+    size_t arena_cap = 0;
 };
 
 namespace {
@@ -225,6 +228,9 @@ Plan plan_tasks(const std::vector<uint64_t> &lens, uint64_t max_bytes, uint32_t 
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
 
+constexpr uint64_t kGcmMaxLen = (((uint64_t)1 << 32) - 2) * 16;
+constexpr uint64_t kCpMaxLen = ((uint64_t)1 << 38) - 64;
+
 int check_aead_args(int algo, int n, const jfsx_blk *blks, int crc_mode, bool device) {
     if (algo != JFSX_AES256GCM && algo != JFSX_CHACHA20P1305) return JFSX_EINVAL;
     if (crc_mode < 0 || (crc_mode & ~(3 | JFSX_CRC_CT)) || (crc_mode & 3) == 3 || crc_mode == JFSX_CRC_CT || n < 0)
@@ -233,8 +239,12 @@ int check_aead_args(int algo, int n, const jfsx_blk *blks, int crc_mode, bool de
         const jfsx_blk &b = blks[i];
         if (b.len && (!b.src || !b.dst)) return JFSX_EINVAL;
         if (device && b.len && (!aligned16(b.src) || !aligned16(b.dst))) return JFSX_EINVAL;
-        if (b.len >= ((uint64_t)1 << 32) * 16) return JFSX_EINVAL;  // GCM 32-bit block counter
-        if (algo == JFSX_CHACHA20P1305 && b.len > ((uint64_t)1 << 32) * 64 - 64) return JFSX_EINVAL;
+        // the ciphers' own limits: GCM's 32-bit counter runs from 2, so past
+        // (2^32 - 2) blocks it would wrap onto J0 (the tag mask) -- Go's Seal
+        // panics there (gcmMaxPlaintext); ChaCha20's 32-bit block counter runs
+        // from 1 (x/crypto v0.19.0: (1<<38) - 64)
+        if (algo == JFSX_AES256GCM && b.len > kGcmMaxLen) return JFSX_EINVAL;
+        if (algo == JFSX_CHACHA20P1305 && b.len > kCpMaxLen) return JFSX_EINVAL;
         if (crc_mode && !b.crc) return JFSX_EINVAL;
     }
     return 0;
@@ -367,13 +377,42 @@ int finish_aead(jfsx_ctx *c, Workspace &w, int k, bool open, jfsx_blk *blks) {
     return 0;
 }
 
+// Open releases nothing of a block whose tag failed: Go's in-place Open
+// (encrypt.go:215; crypto/cipher gcm.go and x/crypto chacha20poly1305 both
+// clear `out` on a mismatch) leaves zeros, and so does the engine -- dst, and
+// a plaintext CRC_GEN array (it is a function of the unauthenticated
+// plaintext).  Ciphertext CRCs (JFSX_CRC_CT) stay: the object checksum is
+// checked before the tag (checksum.go:55-82).  Device memory: zeroed on s.
+int wipe_failed(hipStream_t s, int n, const jfsx_blk *blks, int crc_mode, bool device) {
+    const bool crc_pt = (crc_mode & 3) == JFSX_CRC_GEN && !(crc_mode & JFSX_CRC_CT);
+    bool any = false;
+    for (int i = 0; i < n; i++) {
+        const jfsx_blk &b = blks[i];
+        if (b.status != JFSX_ETAG) continue;
+        any = true;
+        if (device) {
+            if (b.len) HIP_OK(hipMemsetAsync(b.dst, 0, b.len, s));
+            if (crc_pt) HIP_OK(hipMemsetAsync(b.crc, 0, 4 * nseg_of(b.len), s));
+        } else {
+            if (b.len) memset(b.dst, 0, b.len);
+            if (crc_pt) memset(b.crc, 0, 4 * nseg_of(b.len));
+        }
+    }
+    if (any && device) HIP_OK(hipStreamSynchronize(s));
+    return 0;
+}
+
 // Device-resident batch: one enqueue, one sync.
 int run_aead(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mode) {
     int rc = check_aead_args(algo, n, blks, crc_mode, true);
     if (rc || n == 0) return rc;
-    if ((rc = enqueue_aead(c, c->ws[0], c->stream, 0, algo, open, n, blks, crc_mode))) return rc;
+    if ((rc = enqueue_aead(c, c->ws[0], c->stream, 0, algo, open, n, blks, crc_mode))) {
+        (void)hipStreamSynchronize(c->stream);  // nothing of this batch left in flight
+        return rc;
+    }
     HIP_OK(hipStreamSynchronize(c->stream));
-    return finish_aead(c, c->ws[0], 0, open, blks);
+    if ((rc = finish_aead(c, c->ws[0], 0, open, blks))) return rc;
+    return open ? wipe_failed(c->stream, n, blks, crc_mode, true) : 0;
 }
 
 // Host-memory batch (host ingest): blocks are grouped into slots of up to
@@ -382,9 +421,29 @@ int run_aead(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mo
 // copies of one slot overlap the transform of the next.  Open releases no
 // plaintext of a block whose tag failed: its destination is wiped before the
 // call returns.
+int run_aead_host_ring(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mode);
+
+// On an error inside the ring, slots still in flight would keep copying into
+// the caller's dst/crc after the call returned: wait for all three streams
+// first, so an error return means nothing of the batch is still running.
 int run_aead_host(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mode) {
     int rc = check_aead_args(algo, n, blks, crc_mode, false);
     if (rc || n == 0) return rc;
+    rc = run_aead_host_ring(c, algo, open, n, blks, crc_mode);
+    if (rc) {
+        (void)hipStreamSynchronize(c->s_in);
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamSynchronize(c->s_out);
+        for (int k = 0; k < kRing; k++) {
+            c->ws[k].n = 0;
+            c->ws[k].nt = 0;
+        }
+    }
+    return rc;
+}
+
+int run_aead_host_ring(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mode) {
+    int rc = 0;
     // group blocks into slots; a batch smaller than the ring is cut into about
     // 2*kRing slots (>= 16 MiB each) so that its copies and transforms still
     // overlap -- the aggregator's batches are tens of MiB
@@ -518,9 +577,8 @@ int run_aead_host(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int c
         blks[i].crc_got = dv[i].crc_got;
         blks[i].crc_expect = dv[i].crc_expect;
         if (!open) memcpy(blks[i].tag, dv[i].tag, 16);
-        if (open && dv[i].status == JFSX_ETAG && blks[i].len) memset(blks[i].dst, 0, blks[i].len);
     }
-    return 0;
+    return open ? wipe_failed(c->stream, n, blks, crc_mode, false) : 0;
 }
 
 int run_crc(jfsx_ctx *c, int n, jfsx_range *r, int mode) {
@@ -696,6 +754,7 @@ int jfsx_ctx_close(jfsx_ctx *c) {
     if (c->d_tab) (void)hipFree(c->d_tab);
     if (c->rsa_d) (void)hipFree(c->rsa_d);
     if (c->rsa_h) (void)hipHostFree(c->rsa_h);
+    if (c->arena) (void)hipHostFree(c->arena);
     for (int k = 0; k < kRing; k++) {
         Workspace &w = c->ws[k];
         if (w.d) (void)hipFree(w.d);
@@ -842,7 +901,7 @@ int jfsx_cache_verify(jfsx_ctx *c, const void *file, uint64_t file_size, uint64_
     bool eof = false;
     if (level == 0 || (level == 1 && (off != 0 || size != length))) {
         *n_out = pread((uint8_t *)out, size, off, &eof);
-        return eof ? 2 : 0;
+        return eof ? JFSX_EOF : 0;
     }
     std::vector<uint8_t> tmp;
     uint8_t *rb = (uint8_t *)out;
@@ -863,7 +922,7 @@ int jfsx_cache_verify(jfsx_ctx *c, const void *file, uint64_t file_size, uint64_
     const uint64_t nread = pread(rb, rbsize, roff, &eof);
     int rc = 0;
     if (eof) {
-        rc = 2;
+        rc = JFSX_EOF;
     } else {
         uint64_t ioff = roff / kSeg, cstart = 0, clen = rbsize;
         bool check = true;
@@ -889,20 +948,24 @@ int jfsx_cache_verify(jfsx_ctx *c, const void *file, uint64_t file_size, uint64_
             bool eof2 = false;
             pread(ebuf.data(), 4 * nexp, length + ioff * 4, &eof2);
             if (eof2) {
-                rc = 2;
+                rc = JFSX_EOF;
             } else if (clen) {
-                // the engine needs 16-B aligned input: copy the window into pinned staging
-                void *stage = nullptr;
-                int e = jfsx_alloc_pinned(c, clen, &stage);
-                if (e) return e;
-                memcpy(stage, rb + cstart, clen);
+                // stage the window in the context's pinned arena (grow-only):
+                // the H2D then runs as one DMA, with no per-call pinning
+                std::lock_guard<std::mutex> ga(c->arena_mu);
+                int e;
+                {
+                    std::lock_guard<std::mutex> g(c->mu);
+                    HIP_OK(hipSetDevice(c->device));
+                    if ((e = ensure_host(&c->arena, &c->arena_cap, clen))) return e;
+                }
+                memcpy(c->arena, rb + cstart, clen);
                 jfsx_range r;
                 memset(&r, 0, sizeof(r));
-                r.data = stage;
+                r.data = c->arena;
                 r.len = clen;
                 r.crc = ebuf.data();
                 e = jfsx_crc32c_segments(c, 1, &r, JFSX_CRC_VERIFY, JFSX_MEM_HOST);
-                jfsx_free_pinned(c, stage);
                 if (e) return e;
                 if (r.status == JFSX_ECRC) {
                     rc = JFSX_ECRC;
@@ -1075,6 +1138,26 @@ int jfsx_gen_synthetic(jfsx_ctx *c, void *dst, uint64_t len, uint64_t seed, uint
     HIP_OK(hipSetDevice(c->device));
     if (len) launch_gen_synthetic(c->stream, (uint8_t *)dst, len, seed, block);
     HIP_OK(hipGetLastError());
+    return 0;
+}
+
+int jfsx_gen_synthetic_batch(jfsx_ctx *c, void *dst, uint64_t stride, int n, const uint64_t *lens, uint64_t seed,
+                             uint64_t block0) {
+    if (!c || n < 0 || (n && (!dst || !lens)) || !aligned16(dst) || (n > 1 && (stride & 15))) return JFSX_EINVAL;
+    for (int i = 0; i < n; i++)
+        if (lens[i] > stride && n > 1) return JFSX_EINVAL;
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    Workspace &w = c->ws[0];
+    int rc;
+    if ((rc = ensure_dev(c, &w.d, &w.dcap, 8 * (size_t)n))) return rc;
+    if ((rc = ensure_host(&w.h, &w.hcap, 8 * (size_t)n))) return rc;
+    memcpy(w.h, lens, 8 * (size_t)n);
+    HIP_OK(hipMemcpyAsync(w.d, w.h, 8 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    launch_gen_synthetic_batch(c->stream, (uint8_t *)dst, stride, n, (const uint64_t *)w.d, seed, block0);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(c->stream));  // w.h/w.d are reused by the next batch
     return 0;
 }
 

@@ -184,6 +184,42 @@ __global__ __launch_bounds__(256) void gen_synthetic_k(uint8_t *__restrict__ dst
     }
 }
 
+// batched generator: grid (x = workgroups per block, y = block), block i of
+// the batch is the stream of global block block0 + i, lens[i] bytes at
+// dst + i * stride (one launch for a whole bench batch)
+__global__ __launch_bounds__(256) void gen_synthetic_batch_k(uint8_t *__restrict__ dst, uint64_t stride,
+                                                            const uint64_t *__restrict__ lens, uint64_t seed,
+                                                            uint64_t block0) {
+    const uint64_t G = 0x9E3779B97F4A7C15ULL;
+    const uint32_t bi = blockIdx.y;
+    const uint64_t len = lens[bi];
+    uint8_t *d = dst + stride * bi;
+    const uint64_t nw2 = len / 16;
+    const uint64_t base = seed + G * (((block0 + bi) << 40) + 1);
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nw2;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t a = mix64(base + G * (2 * i)), b = mix64(base + G * (2 * i + 1));
+        *reinterpret_cast<ulonglong2 *>(d + 16 * i) = make_ulonglong2(a, b);
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 16) {
+        const uint64_t i = nw2 * 16 + threadIdx.x;
+        if (i < len) {
+            const uint64_t w = mix64(base + G * (i / 8));
+            d[i] = (uint8_t)(w >> (8 * (i % 8)));
+        }
+    }
+}
+
+void launch_gen_synthetic_batch(hipStream_t s, uint8_t *dst, uint64_t stride, int n, const uint64_t *lens,
+                                uint64_t seed, uint64_t block0) {
+    // y <= 65535 blocks per launch
+    for (int i0 = 0; i0 < n; i0 += 65535) {
+        const int m = n - i0 < 65535 ? n - i0 : 65535;
+        hipLaunchKernelGGL(gen_synthetic_batch_k, dim3(16, (unsigned)m), dim3(256), 0, s, dst + stride * i0, stride,
+                           lens + i0, seed, block0 + i0);
+    }
+}
+
 void launch_crc_segments(hipStream_t s, int ntasks, const Task *tasks, const BlkDev *blks, DevTables t) {
     if (ntasks > 0) hipLaunchKernelGGL(crc_segments_k, dim3(ntasks), dim3(kCrcWaves * 64), 0, s, tasks, blks, t);
 }

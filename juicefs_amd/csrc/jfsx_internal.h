@@ -254,6 +254,8 @@ void launch_cp_finalize(hipStream_t s, int n, bool open, int crc_mode, const Blk
 void launch_crc_segments(hipStream_t s, int ntasks, const Task *tasks, const BlkDev *blks, DevTables t);
 void launch_crc_finalize(hipStream_t s, int n, int crc_mode, const BlkDev *blks, BlkOut *out);
 void launch_gen_synthetic(hipStream_t s, uint8_t *dst, uint64_t len, uint64_t seed, uint64_t block);
+void launch_gen_synthetic_batch(hipStream_t s, uint8_t *dst, uint64_t stride, int n, const uint64_t *lens,
+                                uint64_t seed, uint64_t block0);
 // batched RSA-OAEP unwrap (jfsx_rsa.hip): key = device jfsx_rsa::Key
 void async_detach(jfsx_ctx *c);  // jfsx_agg.cpp
 void launch_rsa_unwrap(hipStream_t s, const void *key, int n, const uint8_t *ct, uint32_t *mh, uint8_t *em,

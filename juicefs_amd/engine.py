@@ -20,6 +20,7 @@ CRC_CT = 4  # flag: segment CRCs over the ciphertext (object checksum)
 CTX_BITSLICE = 1  # context flag: AES-GCM keystream from the bitsliced AES (VALU)
 MEM_DEVICE, MEM_HOST = 0, 1
 OK, ETAG, ECRC = 0, 1, 2
+EOF = 3  # jfsx_cache_verify: short read
 EINVAL, ENODEV, EIO, ENOMEM, EMISFORMED, EAGAIN = -22, -19, -5, -12, -74, -11
 SEG = 32 << 10
 
@@ -34,6 +35,9 @@ EXPORTS = [
     "jfsx_rsa_key_new", "jfsx_rsa_key_free", "jfsx_rsa_oaep_decrypt_batch",
     "jfsx_seal_batch_async", "jfsx_open_batch_async", "jfsx_crc32c_segments_async", "jfsx_wait",
     "jfsx_agg_new", "jfsx_agg_free", "jfsx_agg_seal", "jfsx_agg_open", "jfsx_agg_crc32c", "jfsx_agg_stats",
+    "jfsx_gen_synthetic_batch", "jfsx_mctx_open", "jfsx_mctx_close", "jfsx_mctx_ndev", "jfsx_mctx_ctx",
+    "jfsx_mctx_seal_batch", "jfsx_mctx_open_batch", "jfsx_mctx_crc32c_segments", "jfsx_agg_new_mctx",
+    "jfsx_agg_dev_batches",
 ]
 
 
@@ -119,6 +123,16 @@ def load_library(path=LIB_PATH):
             "jfsx_agg_open": (I, [P, I, ctypes.POINTER(jfsx_blk), I, I]),
             "jfsx_agg_crc32c": (I, [P, ctypes.POINTER(jfsx_range), I, I]),
             "jfsx_agg_stats": (I, [P, ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
+            "jfsx_gen_synthetic_batch": (I, [P, P, U64, I, P, U64, U64]),
+            "jfsx_mctx_open": (I, [U64, U32, PP]),
+            "jfsx_mctx_close": (I, [P]),
+            "jfsx_mctx_ndev": (I, [P]),
+            "jfsx_mctx_ctx": (P, [P, I]),
+            "jfsx_mctx_seal_batch": (I, [P, I, I, ctypes.POINTER(jfsx_blk), I, I]),
+            "jfsx_mctx_open_batch": (I, [P, I, I, ctypes.POINTER(jfsx_blk), I, I]),
+            "jfsx_mctx_crc32c_segments": (I, [P, I, ctypes.POINTER(jfsx_range), I, I]),
+            "jfsx_agg_new_mctx": (I, [P, I, U64, U32, PP]),
+            "jfsx_agg_dev_batches": (I, [P, I, ctypes.POINTER(U64)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -242,6 +256,12 @@ class Engine:
 
     def gen_synthetic(self, buf, length, seed, block, offset=0):
         self._check(self.L.jfsx_gen_synthetic(self.ctx, buf.ptr + offset, length, seed, block), "gen_synthetic")
+
+    def gen_synthetic_batch(self, buf, stride, lens, seed, block0, offset=0):
+        """Blocks block0 .. block0+len(lens)-1 at buf + offset + i*stride, one launch."""
+        ln = np.asarray(lens, dtype=np.uint64)
+        self._check(self.L.jfsx_gen_synthetic_batch(self.ctx, buf.ptr + offset, stride, ln.size, ln.ctypes.data,
+                                                    seed, block0), "gen_synthetic_batch")
 
     def sync(self):
         self._check(self.L.jfsx_ctx_sync(self.ctx), "sync")
@@ -476,19 +496,79 @@ class ChecksumError(Exception):
         self.got, self.expect, self.seg = got, expect, seg
 
 
+class MultiEngine:
+    """jfsx_mctx: one context per selected GPU (dev_mask bit d = device d, 0 =
+    all visible).  Host-memory batches are cut into one contiguous run of
+    blocks per device, balanced by bytes, and run concurrently (SURVEY §8e:
+    independent blocks, no collective)."""
+
+    def __init__(self, dev_mask=0, flags=0):
+        self.L = load_library()
+        m = ctypes.c_void_p()
+        rc = self.L.jfsx_mctx_open(dev_mask, flags, ctypes.byref(m))
+        if rc:
+            raise EngineError(rc, "jfsx_mctx_open(0x%x)" % dev_mask)
+        self.m = m.value
+
+    @property
+    def ndev(self):
+        return self.L.jfsx_mctx_ndev(self.m)
+
+    def close(self):
+        if getattr(self, "m", None):
+            self.L.jfsx_mctx_close(self.m)
+            self.m = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc:
+            raise EngineError(rc, what)
+
+    def seal_batch(self, algo, blks, n, crc_mode=CRC_GEN, mem=MEM_HOST):
+        self._check(self.L.jfsx_mctx_seal_batch(self.m, algo, n, blks, crc_mode, mem), "jfsx_mctx_seal_batch")
+
+    def open_batch(self, algo, blks, n, crc_mode=CRC_NONE, mem=MEM_HOST):
+        self._check(self.L.jfsx_mctx_open_batch(self.m, algo, n, blks, crc_mode, mem), "jfsx_mctx_open_batch")
+
+    def crc32c_segments(self, ranges, n, mode=CRC_GEN, mem=MEM_HOST):
+        self._check(self.L.jfsx_mctx_crc32c_segments(self.m, n, ranges, mode, mem), "jfsx_mctx_crc32c_segments")
+
+
 class Aggregator:
     """jfsx_agg: per-block calls from many threads coalesced into batches
     (SURVEY §8f-2).  Each method blocks its caller until that block is done,
     like dataEncryptor.Encrypt/Decrypt (encrypt.go:164-216) or the verify in
     cacheFile.ReadAt (disk_cache.go:1315-1327); ctypes drops the GIL for the
-    wait, so Python threads submit concurrently."""
+    wait, so Python threads submit concurrently.  Over a MultiEngine, one
+    dispatcher per GPU takes groups from one shared queue."""
 
     def __init__(self, eng, max_blocks=0, max_bytes=0, window_us=200):
         self.eng = eng
         self.L = eng.L
         h = ctypes.c_void_p()
-        eng._check(self.L.jfsx_agg_new(eng.ctx, max_blocks, max_bytes, window_us, ctypes.byref(h)), "jfsx_agg_new")
+        if isinstance(eng, MultiEngine):
+            self.ndev = eng.ndev
+            eng._check(self.L.jfsx_agg_new_mctx(eng.m, max_blocks, max_bytes, window_us, ctypes.byref(h)),
+                       "jfsx_agg_new_mctx")
+        else:
+            self.ndev = 1
+            eng._check(self.L.jfsx_agg_new(eng.ctx, max_blocks, max_bytes, window_us, ctypes.byref(h)),
+                       "jfsx_agg_new")
         self.h = h.value
+
+    def dev_batches(self):
+        """batches issued per device slot"""
+        out = []
+        for i in range(self.ndev):
+            v = ctypes.c_uint64()
+            self.eng._check(self.L.jfsx_agg_dev_batches(self.h, i, ctypes.byref(v)), "jfsx_agg_dev_batches")
+            out.append(v.value)
+        return out
 
     def close(self):
         if getattr(self, "h", None):

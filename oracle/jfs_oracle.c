@@ -39,6 +39,7 @@
 #include <string.h>
 #include <pthread.h>
 #include <time.h>
+#include <dlfcn.h>
 #include <immintrin.h>
 #include <wmmintrin.h>
 #include <nmmintrin.h>
@@ -122,6 +123,54 @@ __attribute__((target("sse4.2"))) ORC_EXPORT uint32_t orc_crc32c_update_hw(uint3
     return ~c32;
 }
 
+/* x^(8n) mod P in the reflected convention (bit 31 = x^0), for combining
+ * CRC registers of adjacent spans: reg(A||B) = reg(A) * x^(8|B|) ^ reg0(B) */
+static uint32_t crc_mulmod_r(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+    for (int i = 0; i < 32; i++) {
+        if (a & 0x80000000u) p ^= b;
+        a <<= 1;
+        b = (b & 1) ? (b >> 1) ^ 0x82F63B78u : b >> 1;
+    }
+    return p;
+}
+static uint32_t crc_xpow8_r(uint64_t n) {
+    uint32_t r = 0x80000000u, x = 0x00800000u; /* x^0, x^8 */
+    for (; n; n >>= 1) {
+        if (n & 1) r = crc_mulmod_r(x, r);
+        x = crc_mulmod_r(x, x);
+    }
+    return r;
+}
+
+/* Three interleaved crc32 streams over thirds of the span, combined by GF(2)
+ * shifts: the shape of Go's castagnoliSSE42Triple (hash/crc32, amd64), which
+ * hides the crc32 instruction's latency.  Same value as orc_crc32c_update_hw. */
+__attribute__((target("sse4.2"))) ORC_EXPORT uint32_t orc_crc32c_update_hw3(uint32_t crc, const uint8_t *p,
+                                                                           uint64_t n) {
+    static __thread uint64_t k_cached;
+    static __thread uint32_t xk_cached;
+    const uint64_t k = (n / 24) * 8; /* bytes per stream, a multiple of 8 */
+    if (k < 256) return orc_crc32c_update_hw(crc, p, n);
+    if (k != k_cached) {
+        k_cached = k;
+        xk_cached = crc_xpow8_r(k);
+    }
+    uint64_t a = (uint32_t)~crc, b = 0, c = 0;
+    const uint8_t *pa = p, *pb = p + k, *pc = p + 2 * k;
+    for (uint64_t i = 0; i < k; i += 8) {
+        uint64_t wa, wb, wc;
+        memcpy(&wa, pa + i, 8);
+        memcpy(&wb, pb + i, 8);
+        memcpy(&wc, pc + i, 8);
+        a = _mm_crc32_u64(a, wa);
+        b = _mm_crc32_u64(b, wb);
+        c = _mm_crc32_u64(c, wc);
+    }
+    uint32_t r = crc_mulmod_r(xk_cached, crc_mulmod_r(xk_cached, (uint32_t)a) ^ (uint32_t)b) ^ (uint32_t)c;
+    return orc_crc32c_update_hw(~r, p + 3 * k, n - 3 * k);
+}
+
 #define CS_BLOCK (32 << 10) /* csBlock, disk_cache.go:1207 */
 
 static inline void put_be32(uint8_t *p, uint32_t v) {
@@ -145,7 +194,7 @@ ORC_EXPORT int64_t orc_checksum(const uint8_t *data, int64_t length, uint8_t *ou
     for (int64_t start = 0, end = 0; start < length; start = end) {
         end = start + CS_BLOCK;
         if (end > length) end = length;
-        uint32_t sum = hw ? orc_crc32c_update_hw(0, data + start, (uint64_t)(end - start))
+        uint32_t sum = hw ? orc_crc32c_update_hw3(0, data + start, (uint64_t)(end - start))
                           : orc_crc32c_update(0, data + start, (uint64_t)(end - start));
         put_be32(out + off, sum);
         off += 4;
@@ -931,4 +980,141 @@ ORC_EXPORT double orc_bench_seal_crc(int algo, int nthreads, uint64_t nblocks, u
     free(th);
     if (digest) *digest = dg;
     return el;
+}
+
+/* ------------------------------------------------------------------ */
+/* CPU baseline through OpenSSL EVP (libcrypto.so.3, dlopen'ed): the   */
+/* strongest AEAD the host has (AES-NI/VAES + (V)PCLMULQDQ stitched    */
+/* GCM, SIMD ChaCha20-Poly1305), plus the 3-stream SSE4.2 checksum().  */
+/* BASELINE.md §4 names this as the preferred CPU path.  Returns wall  */
+/* seconds, or -1 when libcrypto is not loadable.                      */
+/* ------------------------------------------------------------------ */
+typedef void *(*evp_ctx_new_t)(void);
+typedef void (*evp_ctx_free_t)(void *);
+typedef const void *(*evp_cipher_t)(void);
+typedef int (*evp_init_t)(void *, const void *, void *, const uint8_t *, const uint8_t *);
+typedef int (*evp_update_t)(void *, uint8_t *, int *, const uint8_t *, int);
+typedef int (*evp_final_t)(void *, uint8_t *, int *);
+typedef int (*evp_ctrl_t)(void *, int, int, void *);
+
+static struct {
+    int ok;
+    evp_ctx_new_t ctx_new;
+    evp_ctx_free_t ctx_free;
+    evp_cipher_t gcm, chacha;
+    evp_init_t init;
+    evp_update_t update;
+    evp_final_t final;
+    evp_ctrl_t ctrl;
+} evp;
+
+static int evp_load(void) {
+    if (evp.ok) return evp.ok > 0;
+    void *h = dlopen("libcrypto.so.3", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+        evp.ok = -1;
+        return 0;
+    }
+    evp.ctx_new = (evp_ctx_new_t)dlsym(h, "EVP_CIPHER_CTX_new");
+    evp.ctx_free = (evp_ctx_free_t)dlsym(h, "EVP_CIPHER_CTX_free");
+    evp.gcm = (evp_cipher_t)dlsym(h, "EVP_aes_256_gcm");
+    evp.chacha = (evp_cipher_t)dlsym(h, "EVP_chacha20_poly1305");
+    evp.init = (evp_init_t)dlsym(h, "EVP_EncryptInit_ex");
+    evp.update = (evp_update_t)dlsym(h, "EVP_EncryptUpdate");
+    evp.final = (evp_final_t)dlsym(h, "EVP_EncryptFinal_ex");
+    evp.ctrl = (evp_ctrl_t)dlsym(h, "EVP_CIPHER_CTX_ctrl");
+    evp.ok = (evp.ctx_new && evp.ctx_free && evp.gcm && evp.chacha && evp.init && evp.update && evp.final &&
+              evp.ctrl) ? 1 : -1;
+    return evp.ok > 0;
+}
+
+/* one Seal through EVP: 0 ok */
+static int evp_seal(void *ctx, int algo, const uint8_t key[32], const uint8_t nonce[12], const uint8_t *p,
+                    uint64_t len, uint8_t *c, uint8_t tag[16]) {
+    if (evp.init(ctx, algo == ALGO_AES256GCM ? evp.gcm() : evp.chacha(), NULL, key, nonce) != 1) return -1;
+    uint64_t off = 0;
+    while (off < len) {
+        int chunk = len - off > (1u << 30) ? (1 << 30) : (int)(len - off), out = 0;
+        if (evp.update(ctx, c + off, &out, p + off, chunk) != 1) return -1;
+        off += (uint64_t)chunk;
+    }
+    int fin = 0;
+    if (evp.final(ctx, c + len, &fin) != 1) return -1;
+    return evp.ctrl(ctx, 0x10 /* EVP_CTRL_AEAD_GET_TAG */, 16, tag) == 1 ? 0 : -1;
+}
+
+/* exported for the tests: the EVP Seal must equal the oracle's */
+ORC_EXPORT int orc_evp_seal(int algo, const uint8_t key[32], const uint8_t nonce[12], const uint8_t *p,
+                            uint64_t len, uint8_t *c, uint8_t tag[16]) {
+    if (!evp_load()) return -1;
+    void *ctx = evp.ctx_new();
+    int rc = evp_seal(ctx, algo, key, nonce, p, len, c, tag);
+    evp.ctx_free(ctx);
+    return rc;
+}
+
+typedef struct {
+    bench_job j;
+    int rc;
+} evp_job;
+
+static void *evp_worker(void *arg) {
+    evp_job *e = (evp_job *)arg;
+    bench_job *j = &e->j;
+    void *ctx = evp.ctx_new();
+    uint32_t dg = 0;
+    e->rc = 0;
+    for (uint64_t b = j->b0; b < j->b1; b++) {
+        uint8_t key[32], nonce[12], tag[16];
+        orc_gen_key(j->seed, b, key, nonce);
+        uint8_t *p = j->pbuf + (b - j->b0) * j->blen;
+        orc_checksum(p, (int64_t)j->blen, j->crc, 1);
+        if (evp_seal(ctx, j->algo, key, nonce, p, j->blen, j->cbuf, tag)) e->rc = -1;
+        dg ^= le32(tag) ^ le32(j->crc);
+    }
+    evp.ctx_free(ctx);
+    j->digest = dg;
+    return NULL;
+}
+
+/* as orc_bench_seal_crc, with the AEAD from OpenSSL EVP; same digest */
+ORC_EXPORT double orc_bench_seal_crc_evp(int algo, int nthreads, uint64_t nblocks, uint64_t blen, uint64_t seed,
+                                         uint32_t *digest) {
+    if (!evp_load()) return -1.0;
+    if (nthreads < 1) nthreads = 1;
+    evp_job *jobs = (evp_job *)calloc((size_t)nthreads, sizeof(evp_job));
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    uint64_t per = (nblocks + nthreads - 1) / nthreads;
+    for (int t = 0; t < nthreads; t++) {
+        bench_job *j = &jobs[t].j;
+        j->algo = algo;
+        j->seed = seed;
+        j->blen = blen;
+        j->b0 = (uint64_t)t * per < nblocks ? (uint64_t)t * per : nblocks;
+        j->b1 = j->b0 + per < nblocks ? j->b0 + per : nblocks;
+        uint64_t nb = j->b1 - j->b0;
+        j->pbuf = (uint8_t *)malloc(nb ? nb * blen : 1);
+        j->cbuf = (uint8_t *)malloc(blen + 16);
+        j->crc = (uint8_t *)malloc((size_t)orc_checksum_len((int64_t)blen));
+        for (uint64_t b = j->b0; b < j->b1; b++) orc_gen_block(seed, b, j->pbuf + (b - j->b0) * blen, blen);
+    }
+    double t0 = now_s();
+    for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, evp_worker, &jobs[t]);
+    uint32_t dg = 0;
+    int rc = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        dg ^= jobs[t].j.digest;
+        rc |= jobs[t].rc;
+    }
+    double el = now_s() - t0;
+    for (int t = 0; t < nthreads; t++) {
+        free(jobs[t].j.pbuf);
+        free(jobs[t].j.cbuf);
+        free(jobs[t].j.crc);
+    }
+    free(jobs);
+    free(th);
+    if (digest) *digest = dg;
+    return rc ? -1.0 : el;
 }

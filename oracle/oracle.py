@@ -38,6 +38,9 @@ def lib():
             "orc_gen_key": (None, [U64, U64, P, P]),
             "orc_crc32c_update": (U32, [U32, P, U64]),
             "orc_crc32c_update_hw": (U32, [U32, P, U64]),
+            "orc_crc32c_update_hw3": (U32, [U32, P, U64]),
+            "orc_evp_seal": (I, [I, P, P, P, U64, P, P]),
+            "orc_bench_seal_crc_evp": (ctypes.c_double, [I, I, U64, U64, U64, P]),
             "orc_checksum_len": (I64, [I64]),
             "orc_checksum": (I64, [P, I64, P, I]),
             "orc_open_cache_file": (I, [I64, I64, I]),
@@ -95,7 +98,7 @@ def gen_key(seed, b):
 
 def crc32c(data, crc=0, hw=False):
     d = _np(data)
-    f = lib().orc_crc32c_update_hw if hw else lib().orc_crc32c_update
+    f = {False: lib().orc_crc32c_update, True: lib().orc_crc32c_update_hw, 3: lib().orc_crc32c_update_hw3}[hw]
     return f(crc, d.ctypes.data if d.size else None, d.size)
 
 
@@ -226,4 +229,21 @@ def data_decrypt(algo, key, obj):
 def bench_seal_crc(algo, nthreads, nblocks, blen, seed):
     dg = ctypes.c_uint32()
     secs = lib().orc_bench_seal_crc(algo, nthreads, nblocks, blen, seed, ctypes.byref(dg))
+    return secs, dg.value
+
+
+def evp_seal(algo, key, nonce, plaintext):
+    """OpenSSL EVP Seal (the CPU baseline's AEAD); None if libcrypto is absent."""
+    p = _np(plaintext)
+    c = np.empty(max(p.size, 1), np.uint8)
+    tag = np.empty(16, np.uint8)
+    if lib().orc_evp_seal(algo, key, nonce, p.ctypes.data, p.size, c.ctypes.data, tag.ctypes.data):
+        return None
+    return c[:p.size].tobytes(), tag.tobytes()
+
+
+def bench_seal_crc_evp(algo, nthreads, nblocks, blen, seed):
+    """(seconds, digest), seconds < 0 if libcrypto is absent."""
+    dg = ctypes.c_uint32()
+    secs = lib().orc_bench_seal_crc_evp(algo, nthreads, nblocks, blen, seed, ctypes.byref(dg))
     return secs, dg.value

@@ -1,6 +1,8 @@
-// Host build of the aggregator and the async queue (juicefs_amd/csrc/jfsx_agg.cpp)
-// over stub batch entry points, so their scheduling logic -- grouping, windows,
-// size caps, error isolation, ordering, shutdown -- is testable without a GPU.
+// Host build of the aggregator, the async queue and the multi-device context
+// (juicefs_amd/csrc/jfsx_agg.cpp) over stub batch entry points, so their
+// scheduling logic -- grouping, windows, size caps, error isolation, ordering,
+// shutdown, the per-device split and the per-device dispatchers -- is testable
+// without a GPU.  Fake devices are contexts 0x1000 + 0x100*d.
 // The stubs record every batch they receive and compute a position-free fake
 // "tag" so results can be matched to their requesters.
 #include <chrono>
@@ -15,14 +17,20 @@ std::mutex h_mu;
 std::vector<int> h_sizes;   // blocks per batch, in issue order
 std::vector<int> h_ops;     // 0 seal, 1 open, 2 crc
 std::vector<int> h_modes;
+std::vector<intptr_t> h_ctxs;  // context of each batch
+std::vector<uint64_t> h_first;  // len of the first block of each batch
 int h_sleep_us = 2000;
+int h_ndev = 4;
+int h_open_ctx = 0;  // contexts opened and not closed
 
-int stub(int op, int n, int mode) {
+int stub(jfsx_ctx *c, int op, int n, int mode, uint64_t first_len = 0) {
     {
         std::lock_guard<std::mutex> g(h_mu);
         h_sizes.push_back(n);
         h_ops.push_back(op);
         h_modes.push_back(mode);
+        h_ctxs.push_back((intptr_t)c);
+        h_first.push_back(first_len);
     }
     std::this_thread::sleep_for(std::chrono::microseconds(h_sleep_us));
     return 0;
@@ -32,10 +40,11 @@ int stub(int op, int n, int mode) {
 extern "C" {
 
 // fake transform: tag[i] = key[i] ^ (len >> 8*(i&7)); reserved != 0 -> EINVAL
-int jfsx_seal_batch(jfsx_ctx *, int algo, int n, jfsx_blk *b, int crc_mode, int mem) {
+int jfsx_seal_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *b, int crc_mode, int mem) {
     for (int i = 0; i < n; i++)
         if (b[i].reserved) return JFSX_EINVAL;
-    stub(0, n, crc_mode);
+    if (mem == JFSX_MEM_DEVICE && (intptr_t)c == 0x1300) return JFSX_EIO;  // fake device 3 fails device batches
+    stub(c, 0, n, crc_mode, n ? b[0].len : 0);
     for (int i = 0; i < n; i++) {
         for (int k = 0; k < 16; k++) b[i].tag[k] = b[i].key[k] ^ (uint8_t)(b[i].len >> (8 * (k & 7))) ^ (uint8_t)algo;
         b[i].status = JFSX_OK;
@@ -43,10 +52,10 @@ int jfsx_seal_batch(jfsx_ctx *, int algo, int n, jfsx_blk *b, int crc_mode, int 
     return 0;
 }
 
-int jfsx_open_batch(jfsx_ctx *, int algo, int n, jfsx_blk *b, int crc_mode, int mem) {
+int jfsx_open_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *b, int crc_mode, int mem) {
     for (int i = 0; i < n; i++)
         if (b[i].reserved) return JFSX_EINVAL;
-    stub(1, n, crc_mode);
+    stub(c, 1, n, crc_mode, n ? b[0].len : 0);
     for (int i = 0; i < n; i++) {
         bool ok = true;
         for (int k = 0; k < 16; k++)
@@ -56,9 +65,28 @@ int jfsx_open_batch(jfsx_ctx *, int algo, int n, jfsx_blk *b, int crc_mode, int 
     return 0;
 }
 
-int jfsx_crc32c_segments(jfsx_ctx *, int n, jfsx_range *r, int mode, int mem) {
-    stub(2, n, mode);
+int jfsx_crc32c_segments(jfsx_ctx *c, int n, jfsx_range *r, int mode, int mem) {
+    stub(c, 2, n, mode, n ? r[0].len : 0);
     for (int i = 0; i < n; i++) r[i].status = r[i].len % 7 == 3 ? JFSX_ECRC : JFSX_OK;
+    return 0;
+}
+
+int jfsx_device_count(int *n) {
+    *n = h_ndev;
+    return h_ndev ? 0 : JFSX_ENODEV;
+}
+
+int jfsx_ctx_open(int device, uint32_t flags, jfsx_ctx **out) {
+    if (device < 0 || device >= h_ndev) return JFSX_ENODEV;
+    std::lock_guard<std::mutex> g(h_mu);
+    h_open_ctx++;
+    *out = (jfsx_ctx *)(intptr_t)(0x1000 + 0x100 * device);
+    return 0;
+}
+
+int jfsx_ctx_close(jfsx_ctx *) {
+    std::lock_guard<std::mutex> g(h_mu);
+    h_open_ctx--;
     return 0;
 }
 
@@ -67,7 +95,23 @@ void harness_reset(int sleep_us) {
     h_sizes.clear();
     h_ops.clear();
     h_modes.clear();
+    h_ctxs.clear();
+    h_first.clear();
     h_sleep_us = sleep_us;
+}
+
+void harness_set_ndev(int n) { h_ndev = n; }
+int harness_open_ctx(void) { return h_open_ctx; }
+
+// per batch: device index of its context and the len of its first block
+int harness_batch_devs(int *dev, uint64_t *first, int cap) {
+    std::lock_guard<std::mutex> g(h_mu);
+    const int n = (int)h_ctxs.size();
+    for (int i = 0; i < n && i < cap; i++) {
+        dev[i] = (int)((h_ctxs[i] - 0x1000) / 0x100);
+        first[i] = h_first[i];
+    }
+    return n;
 }
 
 int harness_batches(int *sizes, int *ops, int *modes, int cap) {

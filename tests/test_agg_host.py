@@ -40,6 +40,18 @@ def H(tmp_path_factory):
         ("harness_reset", None, [I]),
         ("harness_batches", I, [P, P, P, I]),
         ("harness_close", None, [P]),
+        ("harness_set_ndev", None, [I]),
+        ("harness_open_ctx", I, []),
+        ("harness_batch_devs", I, [P, P, I]),
+        ("jfsx_mctx_open", I, [U64, U32, ctypes.POINTER(P)]),
+        ("jfsx_mctx_close", I, [P]),
+        ("jfsx_mctx_ndev", I, [P]),
+        ("jfsx_mctx_ctx", P, [P, I]),
+        ("jfsx_mctx_seal_batch", I, [P, I, I, BP, I, I]),
+        ("jfsx_mctx_open_batch", I, [P, I, I, BP, I, I]),
+        ("jfsx_mctx_crc32c_segments", I, [P, I, ctypes.POINTER(E.jfsx_range), I, I]),
+        ("jfsx_agg_new_mctx", I, [P, I, U64, U32, ctypes.POINTER(P)]),
+        ("jfsx_agg_dev_batches", I, [P, I, ctypes.POINTER(U64)]),
     ]:
         f = getattr(L, name)
         f.restype, f.argtypes = res, args
@@ -232,3 +244,134 @@ def test_async_tickets_order_poll_and_close(H):
     H.harness_close(ctx)
     assert bytes(arr[0].tag) == fake_tag(bytes(32), 5, 0)
     assert H.jfsx_wait(ctx, t.value, 0) == E.EINVAL
+
+
+# ---------------------------------------------------------------------------
+# multi-device context (jfsx_mctx) and the per-device dispatchers
+
+
+def batch_devs(H):
+    cap = 100000
+    d, f = (ctypes.c_int * cap)(), (ctypes.c_uint64 * cap)()
+    n = H.harness_batch_devs(d, f, cap)
+    return [(d[i], f[i]) for i in range(n)]
+
+
+def mctx(H, mask=0, ndev=4):
+    H.harness_set_ndev(ndev)
+    m = ctypes.c_void_p()
+    assert H.jfsx_mctx_open(mask, 0, ctypes.byref(m)) == 0
+    return m
+
+
+def test_mctx_open_mask_and_close(H):
+    m = mctx(H, 0)
+    assert H.jfsx_mctx_ndev(m) == 4
+    assert [H.jfsx_mctx_ctx(m, i) for i in range(4)] == [0x1000, 0x1100, 0x1200, 0x1300]
+    assert H.jfsx_mctx_ctx(m, 4) is None
+    assert H.jfsx_mctx_close(m) == 0
+    m = mctx(H, 0b1010)
+    assert H.jfsx_mctx_ndev(m) == 2 and H.jfsx_mctx_ctx(m, 1) == 0x1300
+    H.jfsx_mctx_close(m)
+    assert H.harness_open_ctx() == 0  # every context closed again
+    x = ctypes.c_void_p()
+    assert H.jfsx_mctx_open(1 << 4, 0, ctypes.byref(x)) == E.ENODEV  # device 4 not visible
+    H.harness_set_ndev(0)
+    assert H.jfsx_mctx_open(0, 0, ctypes.byref(x)) == E.ENODEV
+    H.harness_set_ndev(4)
+
+
+@pytest.mark.parametrize("lens", [[4 << 20] * 64, [1000 * (i % 7 + 1) for i in range(37)], [5, 0, 0, 9], [1 << 30]])
+def test_mctx_batch_splits_runs_by_bytes(H, lens):
+    """A host batch is cut into contiguous per-device runs balanced by bytes;
+    every block is processed exactly once, by one device, and gets its own
+    result."""
+    H.harness_reset(0)
+    m = mctx(H)
+    n = len(lens)
+    arr = (E.jfsx_blk * n)()
+    keys = []
+    for i, ln in enumerate(lens):
+        key = bytes([(i * 7 + k) & 255 for k in range(32)])
+        ctypes.memmove(arr[i].key, key, 32)
+        arr[i].len = ln
+        keys.append(key)
+    assert H.jfsx_mctx_seal_batch(m, 1, n, arr, E.CRC_GEN, E.MEM_HOST) == 0
+    for i, ln in enumerate(lens):
+        assert bytes(arr[i].tag) == fake_tag(keys[i], ln, 1), i
+    bd = batch_devs(H)
+    sizes = [s for s, _, _ in batches(H)]
+    assert sum(sizes) == n and len(bd) == min(4, n) and len({d for d, _ in bd}) == len(bd)
+    if len(set(lens)) == 1 and n % 4 == 0:
+        assert sizes == [n // 4] * 4  # equal blocks: equal runs
+    # runs are contiguous and in order: device d's first block follows device d-1's run
+    order = sorted(zip([d for d, _ in bd], sizes))
+    start = 0
+    for d, sz in order:
+        start += sz
+    assert start == n
+    total = sum(lens) + n
+    for (d, _), sz in zip(bd, sizes):
+        assert sz >= 1
+    if n >= 8 and len(set(lens)) > 1:
+        # balanced: no run exceeds its fair share by more than one block
+        per = {}
+        i = 0
+        for d, sz in order:
+            per[d] = sum(lens[i:i + sz]) + sz
+            i += sz
+        assert max(per.values()) <= total / 4 + max(lens) + 1
+    H.jfsx_mctx_close(m)
+
+
+def test_mctx_errors(H):
+    H.harness_reset(0)
+    m = mctx(H)
+    arr = (E.jfsx_blk * 8)()
+    for i in range(8):
+        arr[i].len = 100
+    # device pointers belong to one GPU: a 4-device context refuses MEM_DEVICE
+    assert H.jfsx_mctx_seal_batch(m, 0, 8, arr, 0, E.MEM_DEVICE) == E.EINVAL
+    assert H.jfsx_mctx_seal_batch(m, 0, 0, arr, 0, E.MEM_HOST) == 0
+    # an engine error on one device reaches the caller
+    arr[5].reserved = 1
+    assert H.jfsx_mctx_seal_batch(m, 0, 8, arr, 0, E.MEM_HOST) == E.EINVAL
+    H.jfsx_mctx_close(m)
+    # a one-device context passes device batches through; the stub device 3 fails them
+    m = mctx(H, 0b1000)
+    arr[5].reserved = 0
+    assert H.jfsx_mctx_seal_batch(m, 0, 8, arr, 0, E.MEM_DEVICE) == E.EIO
+    r = (E.jfsx_range * 3)()
+    assert H.jfsx_mctx_crc32c_segments(m, 3, r, E.CRC_GEN, E.MEM_HOST) == 0
+    H.jfsx_mctx_close(m)
+
+
+def test_agg_over_devices_spreads_batches(H):
+    """One dispatcher per device: with slow batches, concurrent per-block calls
+    run on every device at once, and each caller still gets its own result."""
+    H.harness_reset(20000)
+    m = mctx(H)
+    h = ctypes.c_void_p()
+    assert H.jfsx_agg_new_mctx(m, 8, 0, 2000, ctypes.byref(h)) == 0
+    res = {}
+
+    def worker(i):
+        b, key = mkblk(i, 1000 + i)
+        rc = H.jfsx_agg_seal(h, 0, ctypes.byref(b), E.CRC_GEN, E.MEM_HOST)
+        res[i] = rc == 0 and bytes(b.tag) == fake_tag(key, 1000 + i, 0)
+
+    run_threads(96, worker)
+    assert all(res.values()) and len(res) == 96
+    per = []
+    for i in range(4):
+        v = ctypes.c_uint64()
+        assert H.jfsx_agg_dev_batches(h, i, ctypes.byref(v)) == 0
+        per.append(v.value)
+    assert H.jfsx_agg_dev_batches(h, 4, ctypes.byref(ctypes.c_uint64())) == E.EINVAL
+    assert all(p >= 1 for p in per), per  # every device took work
+    calls, nb, blocks = stats(H, h)
+    assert calls == blocks == 96 and nb == sum(per)
+    assert max(s for s, _, _ in batches(H)) <= 8
+    assert {d for d, _ in batch_devs(H)} == {0, 1, 2, 3}
+    H.jfsx_agg_free(h)
+    H.jfsx_mctx_close(m)

@@ -64,3 +64,21 @@ def test_strong_split_covers_all():
         for world in (1, 2, 4, 8):
             got = [i for r in range(world) for i in shard.shard_strong(total, r, world)]
             assert got == list(range(total))
+
+
+def test_bench_gpus_2_launches_two_ranks():
+    """`python bench.py --gpus 2` with no torch.distributed.run environment
+    starts the launcher itself (two ranks, gloo on CPU here); rank 0 prints one
+    line with n_gpus 2 and the max over ranks of the timing."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run",
+                          "--blocks", "5"], env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["dry_run"] is True
+    assert rec["last_rank_first_block"] == 5  # rank 1 owns blocks [5, 10)
+    assert rec["ms_per_step"] >= 1.0  # rank 1's extra 1 ms: the max over ranks is reported

@@ -176,3 +176,49 @@ def test_data_encryptor_through_aggregator(eng):
     assert calls == 96 and batches < 96
     plain_de = enc.NewDataEncryptor(rsae, "aes256gcm-rsa", eng)
     assert [plain_de.Decrypt(o) for o in objs[:4]] == plains[:4]
+
+
+@pytest.mark.parametrize("algo", [E.AES256GCM, E.CHACHA20P1305])
+def test_multi_device_context_host_batch(algo):
+    """jfsx_mctx over every visible GPU (one on the test box): a host batch
+    split into per-device runs gives the oracle's bytes, tags and CRCs; the
+    aggregator over the same context serves per-block callers."""
+    m = E.MultiEngine(0)
+    try:
+        assert m.ndev == E.device_count()
+        lens = [0, 5, 32769, 1 << 20, 777777, 4 << 20, 3, 65536]
+        ps, outs, crcs, specs = [], [], [], []
+        for i, n in enumerate(lens):
+            key, nonce = orc.gen_key(123, i)
+            p = orc.gen_block(123, i, n)
+            o = np.zeros(max(n, 1), np.uint8)
+            cb = np.zeros(4 * max(1, -(-n // E.SEG)), np.uint8)
+            ps.append(p), outs.append(o), crcs.append(cb)
+            specs.append({"key": key, "nonce": nonce, "src": p.ctypes.data if n else None, "dst": o.ctypes.data,
+                          "len": n, "crc": cb.ctypes.data})
+        arr, nb = E.Engine.make_blocks(specs)
+        m.seal_batch(algo, arr, nb, E.CRC_GEN, E.MEM_HOST)
+        for i, n in enumerate(lens):
+            key, nonce = orc.gen_key(123, i)
+            c, tag = orc.seal(ORC[algo], key, nonce, ps[i], fast=True)
+            assert bytes(arr[i].tag) == tag and outs[i][:n].tobytes() == c, i
+            assert crcs[i].tobytes() == orc.checksum(ps[i], hw=True), i
+        with E.Aggregator(m, window_us=2000) as agg:
+            res = {}
+
+            def worker(i):
+                key, nonce = orc.gen_key(123, i)
+                p = ps[i]
+                c, tag = orc.seal(ORC[algo], key, nonce, p, fast=True)
+                q = np.zeros(max(p.size, 1), np.uint8)
+                a, _ = E.Engine.make_blocks([{"key": key, "nonce": nonce, "src": outs[i].ctypes.data,
+                                              "dst": q.ctypes.data, "len": p.size, "tag": tag,
+                                              "crc": crcs[i].ctypes.data}])
+                agg.open(algo, a[0], E.CRC_VERIFY, E.MEM_HOST)
+                res[i] = (a[0].status, q[:p.size].tobytes() == p.tobytes())
+
+            run_threads(len(lens), worker)
+            assert all(v == (E.OK, True) for v in res.values()), res
+            assert sum(agg.dev_batches()) >= 1
+    finally:
+        m.close()

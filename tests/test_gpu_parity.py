@@ -221,8 +221,8 @@ def test_large_batch_sample_vs_oracle(eng, algo):
     dst = eng.alloc(nb * L)
     crc = eng.alloc(nb * 512)
     specs = []
+    eng.gen_synthetic_batch(src, L, [L] * nb, 0x4A465321, 0)
     for b in range(nb):
-        eng.gen_synthetic(src, L, 0x4A465321, b, offset=b * L)
         key, nonce = orc.gen_key(0x4A465321, b)
         specs.append({"key": key, "nonce": nonce, "src": src.ptr + b * L, "dst": dst.ptr + b * L, "len": L,
                       "crc": crc.ptr + 512 * b})
@@ -282,3 +282,17 @@ def test_host_ingest_pipeline_ring(eng, algo):
                 assert plain[i][:n].tobytes() == ps[i].tobytes(), i
     finally:
         eng.set_slot_bytes(256 << 20)
+
+
+def test_gen_synthetic_batch_matches_oracle_stream(eng):
+    """The bench's one-launch generator writes block block0+i at i*stride
+    with its own (ragged) length: the oracle's gen_block stream."""
+    lens = [0, 1, 15, 16, 17, 4095, 100003, 1 << 20, 65536]
+    stride = 1 << 20
+    buf = eng.alloc(stride * len(lens))
+    buf.upload(np.full(stride * len(lens), 0x5A, np.uint8))
+    eng.gen_synthetic_batch(buf, stride, lens, 77, 1000)
+    for i, n in enumerate(lens):
+        got = buf.download(stride, offset=i * stride)
+        assert got[:n].tobytes() == orc.gen_block(77, 1000 + i, n).tobytes(), n
+        assert (got[n:] == 0x5A).all(), n  # nothing past the block

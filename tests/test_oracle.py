@@ -114,3 +114,30 @@ def test_object_format_roundtrip():
         bad[-1] ^= 0x80
         with pytest.raises(ValueError, match="open failed"):
             orc.data_decrypt(algo, key, bytes(bad))
+
+
+def test_crc32c_three_stream_matches_serial():
+    """orc_crc32c_update_hw3 (three interleaved crc32 streams + GF(2)
+    combine, the CPU baseline's checksum()) equals the serial CRC32C."""
+    from oracle import oracle as orc
+    for n in (0, 1, 7, 767, 768, 769, 5000, 32767, 32768, 32769, 100000, 1 << 20):
+        d = orc.gen_block(1, n, n)
+        assert orc.crc32c(d, hw=3) == orc.crc32c(d) == orc.crc32c(d, hw=True), n
+        assert orc.crc32c(d, 0xDEADBEEF, hw=3) == orc.crc32c(d, 0xDEADBEEF), n
+
+
+def test_evp_baseline_matches_oracle():
+    """The CPU baseline's AEAD (OpenSSL EVP) gives the oracle's bytes, and its
+    timed loop the same tag/CRC digest as the port's."""
+    import pytest
+    from oracle import oracle as orc
+    if orc.evp_seal(0, bytes(32), bytes(12), b"x") is None:
+        pytest.skip("libcrypto.so.3 not loadable")
+    for algo in (orc.AES256GCM, orc.CHACHA20P1305):
+        k, nc = orc.gen_key(5, algo)
+        for n in (0, 1, 16, 1000, 65537, 1 << 20):
+            p = orc.gen_block(5, n, n)
+            assert orc.evp_seal(algo, k, nc, p) == orc.seal(algo, k, nc, p), (algo, n)
+        s1, d1 = orc.bench_seal_crc(algo, 2, 4, 1 << 20, 9)
+        s2, d2 = orc.bench_seal_crc_evp(algo, 2, 4, 1 << 20, 9)
+        assert s2 > 0 and d1 == d2

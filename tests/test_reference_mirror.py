@@ -50,3 +50,38 @@ def test_new_data_encryptor_dispatch():
     assert enc.NewDataEncryptor(Null(), "chacha20-rsa").algo == 1
     with pytest.raises(enc.EncryptError, match="unsupport cipher: sm4"):
         enc.NewDataEncryptor(Null(), "sm4")
+
+
+def _pem_fixtures():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "pem_fixtures.json")) as f:
+        return json.load(f)
+
+
+def test_parse_pkcs8_fixture():
+    """TestParsePKCS8 (encrypt_test.go:69-78) on the reference's own key
+    fixture: the right passphrase parses, a wrong one fails."""
+    from juicefs_amd import encrypt as enc
+    fx = _pem_fixtures()
+    k = enc.ParseRsaPrivateKeyFromPem(fx["keyInPKCS8"].encode(), b"12345678")
+    with pytest.raises(enc.EncryptError):
+        enc.ParseRsaPrivateKeyFromPem(fx["keyInPKCS8"].encode(), b"1234567")
+    # the parsed key wraps and unwraps a data key (rsaEncryptor, encrypt.go:124-134)
+    e = enc.NewRSAEncryptor(k)
+    secret = bytes(range(100, 132))
+    assert e.Decrypt(e.Encrypt(secret)) == secret
+
+
+def test_parse_pem_without_password_fixture():
+    """TestParsePemWithoutPassword (encrypt_test.go:80-89): a PKCS#1 key parses
+    with no passphrase, and a passphrase given for an unencrypted key is
+    ignored."""
+    from juicefs_amd import encrypt as enc
+    fx = _pem_fixtures()
+    k1 = enc.ParseRsaPrivateKeyFromPem(fx["pemWithoutPass"].encode(), None)
+    k2 = enc.ParseRsaPrivateKeyFromPem(fx["pemWithoutPass"].encode(), b"123")
+    assert k1.size == k2.size == 128  # 1024-bit fixture key
+    e1, e2 = enc.NewRSAEncryptor(k1), enc.NewRSAEncryptor(k2)
+    secret = bytes(32)
+    assert e2.Decrypt(e1.Encrypt(secret)) == secret
