@@ -12,6 +12,8 @@ and folded into the whole-object value on the host (jfsx_crc32c_combine);
 Encrypted stores get it fused into the Seal/Open pass instead (JFSX_CRC_CT,
 encrypt.DataEncryptor.EncryptBatch(checksums=True)).
 """
+import re
+
 import numpy as np
 
 from . import engine as E
@@ -80,16 +82,25 @@ class checksumReader:
         return b"".join(out)
 
 
+def parse_checksum(checksum):
+    """strconv.Atoi(checksum) then uint32(...) (checksum.go:76-81): an optional
+    sign and decimal digits that fit an int64; None for "" or anything Atoi
+    rejects (the reference logs "invalid crc32c" and skips verification)."""
+    if checksum is None or not re.fullmatch(r"[+-]?[0-9]+", checksum):
+        return None
+    v = int(checksum)
+    if not -(1 << 63) <= v < (1 << 63):
+        return None
+    return v & 0xFFFFFFFF
+
+
 def verifyChecksum(body, checksum, contentLength, eng=None):
     """checksum.go:72-82: no checksum -> body unchanged; an unparsable one is
     logged and ignored; otherwise a checksumReader."""
-    if checksum is None or checksum == "":
+    expected = parse_checksum(checksum)
+    if expected is None:
         return body
-    try:
-        expected = int(checksum)
-    except ValueError:
-        return body
-    return checksumReader(body, expected & 0xFFFFFFFF, contentLength, eng)
+    return checksumReader(body, expected, contentLength, eng)
 
 
 class ChecksumStorage:

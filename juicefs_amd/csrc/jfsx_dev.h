@@ -28,7 +28,18 @@ __device__ __forceinline__ uint32_t byte_x4(uint32_t x) {
         asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(x));
     return r;
 }
+#ifdef JFSX_ABLATE_CRCBANK
+// timing experiment only (wrong CRCs): every lookup keeps its SDWA address op
+// plus one v_and_or_b32, but lands in the lane's own bank (conflict-free)
+__device__ __forceinline__ uint32_t abl_bank(uint32_t a) {
+    uint32_t r;
+    asm volatile("v_and_or_b32 %0, %1, 0, %2" : "=v"(r) : "v"(a), "v"((threadIdx.x & 31u) << 2));
+    return r;
+}
+#define CRC_T(t, x, k) lds_u32(lds, abl_bank(byte_x4<(k)>(x)) + CB + 1024u * (t))
+#else
 #define CRC_T(t, x, k) lds_u32(lds, byte_x4<(k)>(x) + CB + 1024u * (t))
+#endif
 #else
 #define CRC_T(t, x, k) lds_u32(lds, ((((x) >> (8 * (k))) & 0xffu) << 2) + CB + 1024u * (t))
 #endif

@@ -330,8 +330,9 @@ class DataEncryptor:
         the object-store CRC32Cs to verify in the same pass; a mismatch yields
         the store's "verify checksum failed" error (checksum.go:65)."""
         import numpy as np
-        from .checksum import ChecksumVerifyError
+        from .checksum import ChecksumVerifyError, parse_checksum
         res = [None] * len(ciphertexts)
+        want = [parse_checksum(checksums[i]) if checksums is not None else None for i in range(len(ciphertexts))]
         specs, idx, bufs, segs = [], [], [], []
         parsed = []
         for i, c in enumerate(ciphertexts):
@@ -390,16 +391,25 @@ class DataEncryptor:
             else:
                 self.eng.open_batch(self.algo, arr, cnt, mode, E.MEM_HOST)
             for k, i in enumerate(idx):
-                if checksums is not None and segs[k][2] not in (None, ""):
-                    sb, hdr, want = segs[k]
+                if want[i] is not None:
+                    sb, hdr, _ = segs[k]
                     got = self.eng.object_crc32c(hdr, sb, bufs[k][2], bytes(arr[k].tag))
-                    if got != (int(want) & 0xFFFFFFFF):  # the store's read fails before Decrypt
-                        res[i] = ChecksumVerifyError(got, int(want) & 0xFFFFFFFF)
+                    if got != want[i]:  # the store's read fails before Decrypt
+                        res[i] = ChecksumVerifyError(got, want[i])
                         continue
                 if arr[k].status == E.ETAG:
                     res[i] = EncryptError(_ERR_OPEN[self.algo])
                 else:
                     res[i] = bufs[k][1][:bufs[k][2]].tobytes()
+        # objects that failed before the AEAD pass (header, key unwrap, nonce):
+        # the store's checksumReader still runs first (checksum.go:55-70), so a
+        # checksum mismatch is the error they report
+        opened = set(idx)
+        for i, c in enumerate(ciphertexts):
+            if want[i] is not None and i not in opened:
+                got = E.crc32c_update(0, bytes(c))
+                if got != want[i]:
+                    res[i] = ChecksumVerifyError(got, want[i])
         return res
 
 

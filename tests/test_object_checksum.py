@@ -49,6 +49,13 @@ def test_verify_checksum_passthrough_rules():
     body = b"abc"
     assert cs.verifyChecksum(body, "", 3) is body       # no metadata: unchecked
     assert cs.verifyChecksum(body, "xyz", 3) is body    # unparsable: logged and ignored
+    # strconv.Atoi's grammar: sign and digits only, int64 range; uint32() wraps
+    assert cs.parse_checksum("2591144780") == 2591144780
+    assert cs.parse_checksum("+7") == 7 and cs.parse_checksum("-1") == 0xFFFFFFFF
+    assert cs.parse_checksum(str((1 << 32) + 5)) == 5
+    for bad in ("", " 7", "7 ", "1_0", "0x10", "9223372036854775808", None):
+        assert cs.parse_checksum(bad) is None, bad
+        assert cs.verifyChecksum(body, bad, 3) is body
 
 
 # ---------------------------------------------------------------------------
@@ -178,3 +185,30 @@ def test_encrypted_store_with_checksum_metadata(eng, algo):
     with pytest.raises(cs.ChecksumVerifyError) as ei:
         store.Get("k")
     assert str(ei.value.got) == orc.object_checksum(bytes(bad))
+
+
+@pytest.mark.gpu
+def test_checksum_error_precedes_header_and_key_errors(eng):
+    """An object that fails before the AEAD pass (misformed header, wrapped
+    key that does not unwrap) still reports the store's checksum mismatch
+    first, as the reference's checksumReader runs before Decrypt sees the
+    bytes (checksum.go:55-70, encrypt.go:232-255); an unparsable expected
+    checksum is ignored (checksum.go:76-80)."""
+    from juicefs_amd import checksum as cs
+    from juicefs_amd import encrypt as enc
+    de = enc.NewDataEncryptor(enc.NewRSAEncryptor(enc.GenerateRsaKey(2048)), "aes256gcm-rsa", eng)
+    good = de.Encrypt(b"hello world" * 100)
+    misformed = good[:200]
+    badkey = bytearray(good)
+    badkey[10] ^= 1  # inside the wrapped key
+    for obj in (misformed, bytes(badkey)):
+        wrong = str((E.crc32c_update(0, obj) + 1) & 0xFFFFFFFF)
+        r = de.DecryptBatch([obj], [wrong])[0]
+        assert isinstance(r, cs.ChecksumVerifyError), r
+        assert r.got == E.crc32c_update(0, obj)
+        right = str(E.crc32c_update(0, obj))
+        r = de.DecryptBatch([obj], [right])[0]
+        assert isinstance(r, enc.EncryptError) and not isinstance(r, cs.ChecksumVerifyError), r
+        r = de.DecryptBatch([obj], ["not-a-number"])[0]
+        assert isinstance(r, enc.EncryptError), r
+    assert de.DecryptBatch([good], ["x1"])[0] == b"hello world" * 100
