@@ -144,7 +144,8 @@ int jfsx_ctx_set_timing(jfsx_ctx *ctx, int enable);
 int jfsx_ctx_set_slot_bytes(jfsx_ctx *ctx, uint64_t bytes);
 int jfsx_ctx_kernel_time(jfsx_ctx *ctx, double *ms_total, uint64_t *launches, int reset);
 
-/* memory helpers (engine-owned pinned staging, device buffers) */
+/* memory helpers (engine-owned pinned staging, device buffers); pinned memory
+ * is portable: any context of the process (any GPU) may stream from it */
 int jfsx_alloc_pinned(jfsx_ctx *ctx, size_t bytes, void **p);
 int jfsx_free_pinned(jfsx_ctx *ctx, void *p);
 int jfsx_alloc_device(jfsx_ctx *ctx, size_t bytes, void **p);

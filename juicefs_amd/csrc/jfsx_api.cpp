@@ -810,7 +810,8 @@ int jfsx_ctx_kernel_time(jfsx_ctx *c, double *ms_total, uint64_t *launches, int 
 int jfsx_alloc_pinned(jfsx_ctx *c, size_t bytes, void **p) {
     if (!c || !p) return JFSX_EINVAL;
     HIP_OK(hipSetDevice(c->device));
-    return hipHostMalloc(p, bytes, hipHostMallocDefault) == hipSuccess ? 0 : JFSX_ENOMEM;
+    // portable: the multi-device context's other GPUs DMA from it as well
+    return hipHostMalloc(p, bytes, hipHostMallocPortable) == hipSuccess ? 0 : JFSX_ENOMEM;
 }
 int jfsx_free_pinned(jfsx_ctx *c, void *p) {
     if (!c) return JFSX_EINVAL;

@@ -1,0 +1,213 @@
+/* The cgo shim's call sequence, made from C through
+ * the C-ABI exactly as the Go side makes it, checked against the CPU oracle.
+ *
+ *   §2 gpuEncryptor.Encrypt  -> jfsx_data_encrypt (12 args, obj_crc NULL / set)
+ *      gpuEncryptor.Decrypt  -> jfsx_parse_header, [key unwrap], jfsx_data_decrypt (10 args)
+ *   §3 upload goroutines     -> jfsx_agg_seal / jfsx_agg_open on descriptors in
+ *                               C memory whose src/dst/crc point into the pinned
+ *                               pool (jfsx_alloc_pinned), from many threads;
+ *                               the same over jfsx_mctx (every GPU)
+ *   §4 checksum()            -> jfsx_checksum
+ *      cacheFile.ReadAt      -> jfsx_checksum of rb, compared with the stored
+ *                               CRCs; and jfsx_cache_verify for the level logic
+ *
+ * Built in-tree by tests/harness/Makefile (from __graft_entry__.build());
+ * run by tests/test_shim_sequence.py on the GPU box.  Exit 0 = all equal. */
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/jfsx.h"
+#include "../../oracle/jfs_oracle.c"
+
+#define CHECK(c)                                                               \
+    do {                                                                       \
+        if (!(c)) {                                                            \
+            fprintf(stderr, "shim check failed: %s (line %d)\n", #c, __LINE__); \
+            exit(1);                                                           \
+        }                                                                      \
+    } while (0)
+
+enum { SEED = 77, NTHREADS = 8, PER_THREAD = 3 };
+static const uint64_t kLens[NTHREADS * PER_THREAD] = {
+    0, 1, 17, 4096, 32767, 32768, 32769, 100003, 1 << 20, (4 << 20) - 3, 4 << 20, 65536 + 5,
+    777, 5, 300000, 2 << 20, 3 << 20, 16, 1000000, 12345, 98309, 131072, 4095, 262144 + 9};
+
+/* --- §2: one object per call ------------------------------------------ */
+static void encrypt_decrypt(jfsx_ctx *ctx, int algo) {
+    uint8_t wrapped[256];
+    for (int k = 0; k < 256; k++) wrapped[k] = (uint8_t)(k * 7 + algo);
+    for (int i = 0; i < 6; i++) {
+        const uint64_t n = kLens[i * 4 + 1];
+        uint8_t key[32], nonce[12];
+        orc_gen_key(SEED, 1000 + i, key, nonce);
+        uint8_t *p = malloc(n + 1), *obj = malloc(n + 287), *ref = malloc(n + 287), *back = malloc(n + 287);
+        orc_gen_block(SEED, 1000 + i, p, n);
+        uint64_t olen = 0;
+        uint32_t ocrc = 0;
+        CHECK(jfsx_data_encrypt(ctx, algo, key, nonce, wrapped, 256, p, n, obj, n + 287, &olen, NULL) == 0);
+        CHECK(olen == n + 287);
+        CHECK(orc_data_encrypt(algo, key, nonce, wrapped, 256, p, n, ref) == (int64_t)olen);
+        CHECK(memcmp(obj, ref, olen) == 0);
+        /* S3/OSS/COS: the object checksum in the same pass (checksum.go:31-53) */
+        CHECK(jfsx_data_encrypt(ctx, algo, key, nonce, wrapped, 256, p, n, obj, n + 287, &olen, &ocrc) == 0);
+        CHECK(ocrc == orc_crc32c_update(0, obj, olen));
+        /* Decrypt: header, (key unwrap by the Go side), open */
+        int klen = 0, nlen = 0;
+        CHECK(jfsx_parse_header(obj, olen, &klen, &nlen) == 0 && klen == 256 && nlen == 12);
+        uint64_t pl = 0;
+        CHECK(jfsx_data_decrypt(ctx, algo, key, obj, olen, back, olen, &pl, NULL, NULL) == 0);
+        CHECK(pl == n && memcmp(back, p, n) == 0);
+        uint32_t got = 0;
+        CHECK(jfsx_data_decrypt(ctx, algo, key, obj, olen, back, olen, &pl, &ocrc, &got) == 0 && got == ocrc);
+        obj[olen - 1] ^= 1; /* tag */
+        CHECK(jfsx_data_decrypt(ctx, algo, key, obj, olen, back, olen, &pl, NULL, NULL) == JFSX_ETAG);
+        CHECK(jfsx_parse_header(obj, 271, &klen, &nlen) == JFSX_EMISFORMED);
+        free(p), free(obj), free(ref), free(back);
+    }
+}
+
+/* --- §3: per-block calls through the aggregator, descriptors in C memory -- */
+typedef struct {
+    jfsx_agg *agg;
+    int algo, t;
+    uint8_t *pool; /* pinned: plaintext | ciphertext | crc, per block */
+    int bad;
+} worker_arg;
+
+static uint64_t slot_bytes(void) { return (4 << 20) + 4096; }
+
+static void *worker(void *vp) {
+    worker_arg *a = (worker_arg *)vp;
+    for (int j = 0; j < PER_THREAD; j++) {
+        const int i = a->t * PER_THREAD + j;
+        const uint64_t n = kLens[i];
+        uint8_t *p = a->pool + (uint64_t)i * 3 * slot_bytes(), *c = p + slot_bytes(), *crc = c + slot_bytes();
+        jfsx_blk *b = (jfsx_blk *)calloc(1, sizeof(jfsx_blk)); /* C memory: cgo may pass it */
+        orc_gen_key(SEED, (uint64_t)i, b->key, b->nonce);
+        b->src = p;
+        b->dst = c;
+        b->len = n;
+        b->crc = crc;
+        if (jfsx_agg_seal(a->agg, a->algo, b, JFSX_CRC_GEN, JFSX_MEM_HOST) || b->status != JFSX_OK) a->bad++;
+        uint8_t tag[16];
+        memcpy(tag, b->tag, 16);
+        /* read back: open + verify of the sealed block into the plaintext slot */
+        memset(b, 0, sizeof(*b));
+        orc_gen_key(SEED, (uint64_t)i, b->key, b->nonce);
+        memcpy(b->tag, tag, 16);
+        b->src = c;
+        b->dst = p;
+        b->len = n;
+        b->crc = crc;
+        if (jfsx_agg_open(a->agg, a->algo, b, JFSX_CRC_VERIFY, JFSX_MEM_HOST) || b->status != JFSX_OK) a->bad++;
+        free(b);
+    }
+    return NULL;
+}
+
+static void aggregated(jfsx_ctx *ctx, jfsx_mctx *m, int algo) {
+    void *pool = NULL;
+    const uint64_t total = (uint64_t)NTHREADS * PER_THREAD * 3 * slot_bytes();
+    CHECK(jfsx_alloc_pinned(ctx, total, &pool) == 0);
+    uint8_t *pl = (uint8_t *)pool;
+    for (int i = 0; i < NTHREADS * PER_THREAD; i++)
+        orc_gen_block(SEED, (uint64_t)i, pl + (uint64_t)i * 3 * slot_bytes(), kLens[i]);
+    jfsx_agg *agg = NULL;
+    CHECK((m ? jfsx_agg_new_mctx(m, 0, 0, 500, &agg) : jfsx_agg_new(ctx, 0, 0, 500, &agg)) == 0);
+    pthread_t th[NTHREADS];
+    worker_arg wa[NTHREADS];
+    for (int t = 0; t < NTHREADS; t++) {
+        wa[t] = (worker_arg){agg, algo, t, pl, 0};
+        CHECK(pthread_create(&th[t], NULL, worker, &wa[t]) == 0);
+    }
+    for (int t = 0; t < NTHREADS; t++) {
+        pthread_join(th[t], NULL);
+        CHECK(wa[t].bad == 0);
+    }
+    uint64_t calls = 0, batches = 0, blocks = 0;
+    CHECK(jfsx_agg_stats(agg, &calls, &batches, &blocks) == 0);
+    CHECK(calls == 2 * NTHREADS * PER_THREAD && blocks == calls && batches >= 2);
+    CHECK(jfsx_agg_free(agg) == 0);
+    /* after the round trip each plaintext slot holds its block again, and
+     * the ciphertext / CRCs are the oracle's */
+    for (int i = 0; i < NTHREADS * PER_THREAD; i++) {
+        const uint64_t n = kLens[i];
+        uint8_t *p = pl + (uint64_t)i * 3 * slot_bytes(), *c = p + slot_bytes(), *crc = c + slot_bytes();
+        uint8_t *want = malloc(n + 1), *wc = malloc(n + 1), *wcrc = malloc(4 * (n / 32768 + 2));
+        uint8_t key[32], nonce[12], tag[16];
+        orc_gen_key(SEED, (uint64_t)i, key, nonce);
+        orc_gen_block(SEED, (uint64_t)i, want, n);
+        CHECK(memcmp(p, want, n) == 0);
+        if (algo == JFSX_AES256GCM)
+            orc_aes256gcm_seal_ni(key, nonce, want, n, wc, tag);
+        else
+            orc_chacha20poly1305_seal(key, nonce, NULL, 0, want, n, wc, tag);
+        CHECK(memcmp(c, wc, n) == 0);
+        const int64_t cl = orc_checksum(want, (int64_t)n, wcrc, 1);
+        CHECK(memcmp(crc, wcrc, (size_t)cl) == 0);
+        free(want), free(wc), free(wcrc);
+    }
+    CHECK(jfsx_free_pinned(ctx, pool) == 0);
+}
+
+/* --- §4: checksum() and the ReadAt verify ------------------------------ */
+static void cache_checksums(jfsx_ctx *ctx) {
+    for (int i = 0; i < 10; i++) {
+        const uint64_t n = kLens[i + 3];
+        const int64_t cl = orc_checksum_len((int64_t)n);
+        uint8_t *file = malloc(n + (uint64_t)cl), *ref = malloc((size_t)cl), *gpu = malloc((size_t)cl);
+        orc_gen_block(SEED, 500 + (uint64_t)i, file, n);
+        CHECK(jfsx_checksum(ctx, file, n, gpu) == 0);
+        orc_checksum(file, (int64_t)n, ref, 0);
+        CHECK(memcmp(gpu, ref, (size_t)cl) == 0);
+        memcpy(file + n, gpu, (size_t)cl); /* flushPage: data || checksum(data) */
+        /* ReadAt full-block verify: checksum(rb) against the stored CRCs */
+        if (n) {
+            file[n / 2] ^= 0x20;
+            CHECK(jfsx_checksum(ctx, file, n, gpu) == 0);
+            const int64_t seg = (int64_t)(n / 2) / 32768;
+            CHECK(memcmp(gpu, file + n, (size_t)cl) != 0 && memcmp(gpu + 4 * seg, file + n + 4 * seg, 4) != 0);
+            file[n / 2] ^= 0x20;
+        }
+        /* level logic: jfsx_cache_verify == orc_cache_readat on a few ranges */
+        for (int level = 0; level < 4; level++) {
+            const uint64_t offs[3] = {0, n / 3, n > 100 ? n - 100 : 0};
+            for (int r = 0; r < 3; r++) {
+                const uint64_t off = offs[r], size = r == 0 ? n : (n - off) / 2 + 1;
+                uint8_t *o1 = malloc(size + 1), *o2 = malloc(size + 1);
+                uint64_t n1 = 0;
+                int64_t n2 = 0, b1 = -1, b2 = -1;
+                uint32_t g1 = 0, e1 = 0, g2 = 0, e2 = 0;
+                const int rc1 = jfsx_cache_verify(ctx, file, n + (uint64_t)cl, n, level, off, size, o1, &n1, &g1, &e1, &b1);
+                const int rc2 = orc_cache_readat(file, (int64_t)n + cl, (int64_t)n, level, (int64_t)off, (int64_t)size, o2,
+                                                 &n2, &g2, &e2, &b2);
+                CHECK(rc1 == (rc2 == 0 ? 0 : rc2 == 1 ? JFSX_ECRC : JFSX_EOF));
+                CHECK(n1 == (uint64_t)n2 && memcmp(o1, o2, n1) == 0);
+                free(o1), free(o2);
+            }
+        }
+        free(file), free(ref), free(gpu);
+    }
+}
+
+int main(void) {
+    CHECK(jfsx_abi_version() == JFSX_ABI_VERSION);
+    int nd = 0;
+    CHECK(jfsx_device_count(&nd) == 0 && nd > 0);
+    jfsx_ctx *ctx = NULL;
+    CHECK(jfsx_ctx_open(0, 0, &ctx) == 0);
+    jfsx_mctx *m = NULL;
+    CHECK(jfsx_mctx_open(0, 0, &m) == 0 && jfsx_mctx_ndev(m) == nd);
+    for (int algo = 0; algo < 2; algo++) {
+        encrypt_decrypt(ctx, algo);
+        aggregated(ctx, NULL, algo);
+        aggregated(ctx, m, algo);
+    }
+    cache_checksums(ctx);
+    CHECK(jfsx_mctx_close(m) == 0);
+    CHECK(jfsx_ctx_close(ctx) == 0);
+    printf("shim sequence ok (%d device%s)\n", nd, nd == 1 ? "" : "s");
+    return 0;
+}
