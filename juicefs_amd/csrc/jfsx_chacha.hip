@@ -57,6 +57,42 @@ __device__ __forceinline__ P5 p_mul(const P5 &a, const P5 &b) {
     return r;
 }
 
+// Horner step a * b + m mod p for the main loop: b is r or r^253 (limbs
+// < 2^26), sb[i] = 5 * b.l[i] precomputed, m a message block (limbs < 2^26).
+// The message limbs and each carry enter the next limb's product sum as its
+// first addend, carries are 32-bit (every d_i < 2^57, so d_i >> 26 < 2^31),
+// and the top carry folds back into limb 0 times 5 (d4 has no wrapped
+// products: d4 < 2^54.4, 5 * (d4 >> 26) < 2^31).  Output limbs < 2^26 except
+// l[1] < 2^26 + 2^6.
+__device__ __forceinline__ P5 p_mul_add(const P5 &a, const P5 &b, const uint32_t (&sb)[5], const P5 &m) {
+    typedef uint64_t u64;
+    P5 r;
+    u64 d = (u64)m.l[0] + (u64)a.l[0] * b.l[0] + (u64)a.l[1] * sb[4] + (u64)a.l[2] * sb[3] + (u64)a.l[3] * sb[2] +
+            (u64)a.l[4] * sb[1];
+    r.l[0] = (uint32_t)d & M26;
+    uint32_t c = (uint32_t)(d >> 26);
+    d = (u64)(c + m.l[1]) + (u64)a.l[0] * b.l[1] + (u64)a.l[1] * b.l[0] + (u64)a.l[2] * sb[4] +
+        (u64)a.l[3] * sb[3] + (u64)a.l[4] * sb[2];
+    r.l[1] = (uint32_t)d & M26;
+    c = (uint32_t)(d >> 26);
+    d = (u64)(c + m.l[2]) + (u64)a.l[0] * b.l[2] + (u64)a.l[1] * b.l[1] + (u64)a.l[2] * b.l[0] +
+        (u64)a.l[3] * sb[4] + (u64)a.l[4] * sb[3];
+    r.l[2] = (uint32_t)d & M26;
+    c = (uint32_t)(d >> 26);
+    d = (u64)(c + m.l[3]) + (u64)a.l[0] * b.l[3] + (u64)a.l[1] * b.l[2] + (u64)a.l[2] * b.l[1] +
+        (u64)a.l[3] * b.l[0] + (u64)a.l[4] * sb[4];
+    r.l[3] = (uint32_t)d & M26;
+    c = (uint32_t)(d >> 26);
+    d = (u64)(c + m.l[4]) + (u64)a.l[0] * b.l[4] + (u64)a.l[1] * b.l[3] + (u64)a.l[2] * b.l[2] +
+        (u64)a.l[3] * b.l[1] + (u64)a.l[4] * b.l[0];
+    r.l[4] = (uint32_t)d & M26;
+    c = (uint32_t)(d >> 26);
+    const uint32_t t = r.l[0] + c * 5u;
+    r.l[0] = t & M26;
+    r.l[1] += t >> 26;
+    return r;
+}
+
 __device__ __forceinline__ P5 p_add(const P5 &a, const P5 &b) {
     P5 r;
 #pragma unroll
@@ -127,6 +163,68 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return __builtin_a
     c += d; b = rotl(b ^ c, 12);   \
     a += b; d = rotl(d ^ a, 8);    \
     c += d; b = rotl(b ^ c, 7);
+
+// Counter-uniform first column round: of the first double round's column
+// quarter rounds, three never touch the counter word (x12) and the fourth
+// starts with a += b on key words.  A wave computes those once per task
+// (wave-uniform, SGPRs) and each block starts from them: 37 of the block's
+// 960 + 16 ALU ops are gone.
+struct CpUni {
+    uint32_t a0;      // x0 + x4
+    uint32_t w[16];   // state after the three counter-free column QRs (x1..3, x5..7, x9..11, x13..15)
+    uint32_t in[16];  // input words (for the final add; in[12] unused)
+};
+
+__device__ __forceinline__ CpUni cp_uniform(const uint32_t *key, const uint32_t *nonce) {
+    CpUni u;
+    uint32_t x[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key[0], key[1], key[2], key[3],
+                      key[4], key[5], key[6], key[7], 0u, nonce[0], nonce[1], nonce[2]};
+#pragma unroll
+    for (int i = 0; i < 16; i++) u.in[i] = x[i];
+    CP_QR(x[1], x[5], x[9], x[13]);
+    CP_QR(x[2], x[6], x[10], x[14]);
+    CP_QR(x[3], x[7], x[11], x[15]);
+    u.a0 = x[0] + x[4];
+#pragma unroll
+    for (int i = 0; i < 16; i++) u.w[i] = x[i];
+    // wave-uniform: keep them in SGPRs
+    u.a0 = __builtin_amdgcn_readfirstlane(u.a0);
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        u.w[i] = __builtin_amdgcn_readfirstlane(u.w[i]);
+        u.in[i] = __builtin_amdgcn_readfirstlane(u.in[i]);
+    }
+    return u;
+}
+
+__device__ __forceinline__ void chacha_block_u(const CpUni &u, uint32_t ctr, uint32_t out[16]) {
+    // column QR(x0, x4, x8, x12) from a = x0 + x4
+    uint32_t x0 = u.a0, x4 = u.in[4], x8 = u.in[8], x12 = rotl(ctr ^ x0, 16);
+    x8 += x12; x4 = rotl(x4 ^ x8, 12);
+    x0 += x4; x12 = rotl(x12 ^ x0, 8);
+    x8 += x12; x4 = rotl(x4 ^ x8, 7);
+    uint32_t x1 = u.w[1], x2 = u.w[2], x3 = u.w[3], x5 = u.w[5], x6 = u.w[6], x7 = u.w[7], x9 = u.w[9],
+             x10 = u.w[10], x11 = u.w[11], x13 = u.w[13], x14 = u.w[14], x15 = u.w[15];
+    CP_QR(x0, x5, x10, x15);
+    CP_QR(x1, x6, x11, x12);
+    CP_QR(x2, x7, x8, x13);
+    CP_QR(x3, x4, x9, x14);
+#pragma unroll
+    for (int i = 1; i < 10; i++) {
+        CP_QR(x0, x4, x8, x12);
+        CP_QR(x1, x5, x9, x13);
+        CP_QR(x2, x6, x10, x14);
+        CP_QR(x3, x7, x11, x15);
+        CP_QR(x0, x5, x10, x15);
+        CP_QR(x1, x6, x11, x12);
+        CP_QR(x2, x7, x8, x13);
+        CP_QR(x3, x4, x9, x14);
+    }
+    out[0] = x0 + u.in[0]; out[1] = x1 + u.in[1]; out[2] = x2 + u.in[2]; out[3] = x3 + u.in[3];
+    out[4] = x4 + u.in[4]; out[5] = x5 + u.in[5]; out[6] = x6 + u.in[6]; out[7] = x7 + u.in[7];
+    out[8] = x8 + u.in[8]; out[9] = x9 + u.in[9]; out[10] = x10 + u.in[10]; out[11] = x11 + u.in[11];
+    out[12] = x12 + ctr; out[13] = x13 + u.in[13]; out[14] = x14 + u.in[14]; out[15] = x15 + u.in[15];
+}
 
 __device__ __forceinline__ void chacha_block(const uint32_t *key, const uint32_t *nonce, uint32_t ctr,
                                              uint32_t out[16]) {
@@ -271,6 +369,13 @@ __global__ __launch_bounds__(kCpWaves * 64) void cp_main_k(const Task *__restric
 #pragma unroll
     for (int i = 0; i < 3; i++) nonce[i] = sch->nonce[i];
     const P5 r1 = p_load(sch->r), r253 = p_load(sch->r253);
+    const CpUni uni = cp_uniform(key, nonce);
+    uint32_t s1[5], s253[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+        s1[i] = 5u * r1.l[i];
+        s253[i] = 5u * r253.l[i];
+    }
 
     const uint32_t wave = tid >> 6, lane = tid & 63;
     const uint64_t c0 = task.c0, c1 = task.c1;
@@ -296,7 +401,7 @@ __global__ __launch_bounds__(kCpWaves * 64) void cp_main_k(const Task *__restric
 #pragma unroll
         for (int q = 0; q < 4; q++) d[q] = gld16(src + o + 16 * q);
         uint32_t ks[16];
-        chacha_block(key, nonce, (uint32_t)(o / 64 + 1), ks);
+        chacha_block_u(uni, (uint32_t)(o / 64 + 1), ks);
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const uint4 x = make_uint4(d[q].x ^ ks[4 * q], d[q].y ^ ks[4 * q + 1], d[q].z ^ ks[4 * q + 2],
@@ -304,7 +409,8 @@ __global__ __launch_bounds__(kCpWaves * 64) void cp_main_k(const Task *__restric
             const uint4 c = OPEN ? d[q] : x, p = OPEN ? x : d[q];
             gst16(dst + o + 16 * q, OPEN ? p : c);
             const uint4 cq = crc_src<CRCMODE>(c, p);
-            st.A = p_add(p_mul(st.A, q == 0 ? r253 : r1), p_from_words(c.x, c.y, c.z, c.w, 1));
+            st.A = q == 0 ? p_mul_add(st.A, r253, s253, p_from_words(c.x, c.y, c.z, c.w, 1))
+                          : p_mul_add(st.A, r1, s1, p_from_words(c.x, c.y, c.z, c.w, 1));
             if (CRCMODE) {
                 st.C = q == 0 ? crc_piece<kLdsCrcCp, 20>(lds, st.C, cq.x, cq.y, cq.z, cq.w)
                               : crc_piece<kLdsCrcCp, -1>(lds, st.C, cq.x, cq.y, cq.z, cq.w);
