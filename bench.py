@@ -53,6 +53,12 @@ def parse():
                          "(configs[2], host ingest)")
     ap.add_argument("--ragged", action="store_true",
                     help="configs[4]: block lengths uniform in [64 KiB, 4 MiB] (seeded), non-multiples of 16/64/32768")
+    ap.add_argument("--ragged-align", type=int, default=0,
+                    help="diagnostic: round ragged lengths up to a multiple of this many bytes")
+    ap.add_argument("--fixed-len", type=int, default=0,
+                    help="diagnostic: every block this long, placed in --block-bytes slots")
+    ap.add_argument("--packed", action="store_true",
+                    help="place blocks back to back (256-B aligned) instead of one per --block-bytes slot")
     ap.add_argument("--aes", choices=["ttable", "bitslice"], default="ttable",
                     help="AES-GCM keystream kernel: T-table AES in LDS, or bitsliced AES on the VALU")
     ap.add_argument("--dry-run", action="store_true",
@@ -198,13 +204,24 @@ def main():
     base = rank * nb  # global block index: blocks shard across ranks (juicefs_amd.shard.shard)
     # block b occupies slot [b*L, b*L + lens[b]); ragged lengths are a seeded
     # draw per global block index, so every rank and rerun sees the same batch
-    lens = [ragged_len(SEED, base + b, L) if args.ragged else L for b in range(nb)]
-    eng.gen_synthetic_batch(src, L, lens, SEED, base)  # one launch for the whole batch
+    lens = [ragged_len(SEED, base + b, L) if args.ragged else (args.fixed_len or L) for b in range(nb)]
+    if args.ragged and args.ragged_align:
+        lens = [min(L, -(-x // args.ragged_align) * args.ragged_align) for x in lens]
+    if args.packed:
+        offs, o = [], 0
+        for x in lens:
+            offs.append(o)
+            o += -(-x // 256) * 256
+        for b in range(nb):
+            eng.gen_synthetic_batch(src, L, [lens[b]], SEED, base + b, offset=offs[b])
+    else:
+        offs = [b * L for b in range(nb)]
+        eng.gen_synthetic_batch(src, L, lens, SEED, base)  # one launch for the whole batch
 
     if args.mode == "crc":
         ranges = (E.jfsx_range * nb)()
         for b in range(nb):
-            ranges[b].data, ranges[b].len, ranges[b].crc = src.ptr + b * L, lens[b], crc.ptr + 4 * nseg * b
+            ranges[b].data, ranges[b].len, ranges[b].crc = src.ptr + offs[b], lens[b], crc.ptr + 4 * nseg * b
         eng.crc32c_segments(ranges, nb, E.CRC_GEN, E.MEM_DEVICE)
 
         def step():
@@ -214,7 +231,7 @@ def main():
         specs = []
         for b in range(nb):
             key, nonce = E.gen_key(SEED, base + b)
-            specs.append({"key": key, "nonce": nonce, "src": src.ptr + b * L, "dst": dst.ptr + b * L, "len": lens[b],
+            specs.append({"key": key, "nonce": nonce, "src": src.ptr + offs[b], "dst": dst.ptr + offs[b], "len": lens[b],
                           "crc": crc.ptr + 4 * nseg * b})
         blks, n = eng.make_blocks(specs)
         if args.mode == "seal":
@@ -303,7 +320,7 @@ def main():
             key, nonce = orc.gen_key(SEED, base + b)
             c, tag = orc.seal(orc.AES256GCM if algo == E.AES256GCM else orc.CHACHA20P1305, key, nonce, p,
                               fast=algo == E.AES256GCM)
-            ok = bytes(blks[b].tag) == tag and dst.download(lens[b], offset=b * L).tobytes() == c
+            ok = bytes(blks[b].tag) == tag and dst.download(lens[b], offset=offs[b]).tobytes() == c
             if args.crc == "full":
                 cs = orc.checksum(p, hw=True)
                 ok = ok and crc.download(len(cs), offset=4 * nseg * b).tobytes() == cs

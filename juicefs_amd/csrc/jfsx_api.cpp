@@ -112,6 +112,8 @@ void make_crc_tables(std::vector<uint32_t> &crc, std::vector<uint32_t> &crcx) {
     for (int l = 0; l < 64; l++) crcx[l] = xpow8(16 * (63 - l));
     for (int k = 0; k < 32; k++) crcx[64 + k] = x8[k];
     crcx[96] = crc_mulmod_h(xpow8(kSeg), 0xffffffffu);
+    // x^(8 * 1024 k), k = 1..31: whole-row shifts (crc_xpow8_fast, jfsx_internal.h)
+    for (int k = 1; k < 32; k++) crcx[96 + k] = xpow8(1024 * (uint64_t)k);
     for (int l = 0; l < 64; l++) crcx[128 + l] = xpow8(64 * (63 - l));
 }
 
@@ -151,6 +153,7 @@ struct jfsx_ctx {
     hipEvent_t ev_in[kRing] = {}, ev_comp[kRing] = {}, ev_out[kRing] = {};
     hipEvent_t ev_k0[kRing] = {}, ev_k1[kRing] = {};  // main-kernel timing per slot
     size_t slot_bytes = (size_t)256 << 20;
+    int ncu = 256;  // compute units: persistent transform kernels launch one workgroup per CU
     bool timing = false;
     bool bitslice = false;  // JFSX_CTX_BITSLICE
     char *rsa_d = nullptr;  // batched RSA unwrap: ct | halves | em | len (device, grow-only)
@@ -284,6 +287,7 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, int k, int algo, bool
     const size_t o_part = off; off = align256(off + 32 * std::max<uint64_t>(plan.nslots, 1));
     const size_t o_pexp = off; off = align256(off + 4 * std::max<uint64_t>(plan.nslots, 1));
     const size_t o_calc = off; off = align256(off + 4 * std::max<uint64_t>(crc_calc_words, 1));
+    const size_t o_queue = off; off = align256(off + 4);  // persistent kernel's task counter
     int rc;
     if ((rc = ensure_dev(c, &w.d, &w.dcap, off))) return rc;
     if ((rc = ensure_host(&w.h, &w.hcap, std::max(h_bytes, sizeof(BlkOut) * n)))) return rc;
@@ -315,7 +319,17 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, int k, int algo, bool
         if (bd.nslots == 0) bd.slot0 = plan.tasks[t].slot0;
         bd.nslots += slots;
     }
-    if (nt) memcpy(h + o_task, plan.tasks.data(), sizeof(Task) * nt);
+    if (nt) {
+        Task *ht = (Task *)(h + o_task);
+        memcpy(ht, plan.tasks.data(), sizeof(Task) * nt);
+#ifdef JFSX_ABLATE_TRACE
+        for (size_t t = 0; t < nt; t++) ht[t].trace = (uint32_t)t;
+#endif
+        // the persistent GCM kernel takes tasks in array order: largest first,
+        // so that the last tasks handed out are short (slots stay per task)
+        if (gcm)
+            std::stable_sort(ht, ht + nt, [](const Task &a, const Task &b) { return a.c1 - a.c0 > b.c1 - b.c0; });
+    }
     if (up) {
         HIP_OK(hipMemcpyAsync(d, h, h_bytes, hipMemcpyHostToDevice, up));
         HIP_OK(hipEventRecord(up_ev, up));
@@ -336,7 +350,8 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, int k, int algo, bool
         GcmSched *dsch = (GcmSched *)(d + o_sched);
         launch_gcm_keysetup(s, n, dk, db, dsch, c->tabs);
         if (c->timing) HIP_OK(hipEventRecord(c->ev_k0[k], s));
-        launch_gcm_main(s, (int)nt, open, crc_mode, c->bitslice, dt, db, dsch, dpart, dpexp, c->tabs);
+        launch_gcm_main(s, (int)nt, c->ncu, (uint32_t *)(d + o_queue), open, crc_mode, c->bitslice, dt, db, dsch, dpart,
+                        dpexp, c->tabs);
         if (c->timing) HIP_OK(hipEventRecord(c->ev_k1[k], s));
         launch_gcm_finalize(s, n, open, crc_mode, db, dsch, dpart, dpexp, dout);
     } else {
@@ -707,6 +722,9 @@ int jfsx_ctx_open(int device, uint32_t flags, jfsx_ctx **out) {
     jfsx_ctx *c = new jfsx_ctx();
     c->device = device;
     c->bitslice = (flags & JFSX_CTX_BITSLICE) != 0;
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+        c->ncu = ncu;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) != hipSuccess) {

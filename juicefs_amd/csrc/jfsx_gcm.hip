@@ -48,7 +48,11 @@ constexpr uint32_t kLdsGh = 20480;              // GHASH T[b][j]: kLdsGh + (b <<
 constexpr uint32_t kLdsAesOff = 20480;          // ds_read offset of the AES table
 constexpr uint32_t kLdsAes = 65536 + kLdsAesOff;  // AES [idx][T0 x32 | T2 x32]: 0x10000 | (idx << 8) | (r << 2), + offset
 constexpr uint32_t kLdsBasis = kLdsAes + 65536;
-constexpr uint32_t kLdsBytes = kLdsBasis + 2048;
+// row-split tasks: per segment of the task, the XOR of the waves' raw CRC
+// shares (128 segments of 32 KiB per 4 MiB task) and a flag per segment
+constexpr uint32_t kLdsSegRaw = kLdsBasis + 2048;
+constexpr uint32_t kLdsSegFlag = kLdsSegRaw + 512;
+constexpr uint32_t kLdsBytes = kLdsSegFlag + 512;
 
 __device__ __forceinline__ uint32_t rotl8(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 24); }
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -303,21 +307,59 @@ struct Stream {
     uint64_t seg0;        // start of the current segment
 };
 
-// CRC32C of one finished segment: shift lane CRCs to the segment end, reduce, store
+// CRC32C of segment [seg0, seg1) (seg1: its true end in the block) from this
+// stream's lane accumulators A.  A lane's last piece in the segment ends at
+// lend (segment relative), or, when lend == 0, at the end of its slot in the
+// row that ends at tailRef (shift xl to the row end, then seg1 - tailRef more
+// bytes).  When the stream covers only part of the segment (row-split tasks)
+// the wave's raw share is XORed into the task's LDS slot and the CRC is
+// finished once all waves are done (gcm_main_k's end); otherwise it is stored.
+// the segment's raw share into the task's LDS slot (lane 0 only)
+__device__ __forceinline__ void crc_share(char *lds, uint32_t slot, uint32_t raw) {
+    atomicXor(reinterpret_cast<uint32_t *>(lds + kLdsSegRaw) + slot, raw);
+    reinterpret_cast<uint32_t *>(lds + kLdsSegFlag)[slot] = 1u;
+}
+
+// Fast-loop form: a whole 32 KiB segment ended with the stream's row in its
+// last row (every lane's last piece there): shift by xl, reduce, store -- or,
+// when the stream began inside the segment, hand in the share.
 template <int CRCMODE>
-__device__ __forceinline__ void crc_segment_end(const BlkDev &blk, const DevTables &tab, uint32_t lane, uint32_t xl,
-                                                uint64_t seg0, uint64_t seg1, uint32_t A, uint32_t lend) {
+__device__ __forceinline__ void crc_segment_done(const BlkDev &blk, const DevTables &tab, uint32_t lane, uint32_t xl,
+                                                 uint64_t seg0, uint32_t A, bool partial, char *lds, uint64_t c0) {
+    const uint32_t raw = wave_xor(crc_mulmod(xl, A));
+    if (lane == 0) {
+        if (partial) {
+            crc_share(lds, (uint32_t)((seg0 - c0) / kSeg), raw);
+            return;
+        }
+        const uint32_t crc = ~(tab.crcx[96] ^ raw);
+        const uint64_t si = seg0 / kSeg;
+        if ((CRCMODE & 3) == 1)
+            *reinterpret_cast<uint32_t *>(blk.crc + 4 * si) = __builtin_bswap32(crc);
+        else
+            blk.crc_calc[si] = crc;
+    }
+}
+
+template <int CRCMODE>
+__device__ __noinline__ void crc_segment_end(const BlkDev &blk, const DevTables &tab, uint32_t lane, uint32_t xl,
+                                             uint64_t seg0, uint64_t seg1, uint32_t A, uint32_t lend,
+                                             uint64_t tailRef, bool partial, char *lds, uint32_t slot) {
     const uint32_t Lseg = (uint32_t)(seg1 - seg0);
-    uint32_t v, K;
-    if (Lseg == (uint32_t)kSeg) {
-        v = crc_mulmod(xl, A);
-        K = tab.crcx[96];
+    uint32_t v;
+    if (lend == 0) {
+        const uint32_t sh = tailRef == seg1 ? xl : crc_mulmod(crc_xpow8_fast((uint32_t)(seg1 - tailRef), tab.crcx), xl);
+        v = crc_mulmod(sh, A);
     } else {
-        v = crc_mulmod(crc_xpow8(Lseg - lend, tab.crcx + 64), A);
-        K = crc_mulmod(crc_xpow8(Lseg, tab.crcx + 64), 0xffffffffu);
+        v = crc_mulmod(crc_xpow8_fast(Lseg - lend, tab.crcx), A);
     }
     const uint32_t raw = wave_xor(v);
     if (lane == 0) {
+        if (partial) {
+            crc_share(lds, slot, raw);
+            return;
+        }
+        const uint32_t K = Lseg == (uint32_t)kSeg ? tab.crcx[96] : crc_mulmod(crc_xpow8_fast(Lseg, tab.crcx), 0xffffffffu);
         const uint32_t crc = ~(K ^ raw);
         const uint64_t si = seg0 / kSeg;
         if ((CRCMODE & 3) == 1)
@@ -330,9 +372,9 @@ __device__ __forceinline__ void crc_segment_end(const BlkDev &blk, const DevTabl
 // Generic (guarded) processing of one row of one stream: handles the ragged
 // tail of a block (partial 16-B piece, lanes past the end, partial segment).
 template <bool OPEN, int CRCMODE>
-__device__ __noinline__ Stream row_generic(const char *lds, uint32_t loff, const GhLane gl, const GcmSched *sch,
+__device__ __noinline__ Stream row_generic(char *lds, uint32_t loff, const GhLane gl, const GcmSched *sch,
                                            const BlkDev blk, const DevTables tab, uint32_t lane, uint32_t xl, Stream st,
-                                           uint64_t row) {
+                                           uint64_t row, uint64_t c0, uint64_t c1) {
     uint32_t rk[60];
 #pragma unroll
     for (int i = 0; i < 60; i++) rk[i] = rk_load(sch->rk, i);
@@ -374,9 +416,10 @@ __device__ __noinline__ Stream row_generic(const char *lds, uint32_t loff, const
             st.A = crc_partial<kLdsCrc>(lds, st.A, pw, (int)(end - o));
             st.lend = (uint32_t)(end - st.seg0);
         }
-        const uint64_t seg1 = st.seg0 + kSeg < end ? st.seg0 + kSeg : end;
+        const uint64_t seg1 = st.seg0 + kSeg < c1 ? st.seg0 + kSeg : c1;  // the segment's true end
         if (row + 1024 >= seg1) {
-            crc_segment_end<CRCMODE>(blk, tab, lane, xl, st.seg0, seg1, st.A, st.lend);
+            crc_segment_end<CRCMODE>(blk, tab, lane, xl, st.seg0, seg1, st.A, st.lend, row, st.seg0 < st.sub0, lds,
+                                     (uint32_t)((st.seg0 - c0) / kSeg));
             st.A = 0;
             st.lend = 0;
             st.seg0 = seg1;
@@ -395,71 +438,91 @@ struct GcmShape {
     static constexpr uint32_t threads = waves * 64u;
 };
 
+#ifdef JFSX_ABLATE_TRACE
+// diagnostic build only (make variant V=TRACE): per workgroup start / end
+// times (s_memrealtime, 100 MHz), HW_ID | XCC_ID << 32 and the task's bytes
+__device__ uint64_t g_wgtrace[4 * 65536];
+#endif
+
+// One task (a block's <= 4 MiB byte range) on the whole workgroup.  The AES
+// and CRC tables are already in LDS; the GHASH table of the task's key is
+// built here.  Every thread of the workgroup calls this.
 template <bool OPEN, int CRCMODE, int NS, int BS>
-__global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *__restrict__ tasks,
-                                                       const BlkDev *__restrict__ blks,
-                                                       const GcmSched *__restrict__ sched,
-                                                       uint32_t *__restrict__ partial, uint32_t *__restrict__ pexp,
-                                                       DevTables tab) {
-    __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
-    const Task task = tasks[blockIdx.x];
+__device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDev *__restrict__ blks,
+                                         const GcmSched *__restrict__ sched, uint32_t *__restrict__ partial,
+                                         uint32_t *__restrict__ pexp, const DevTables &tab, uint32_t tid,
+                                         uint32_t wave, uint32_t lane, uint32_t loff, const GhLane &gl, uint32_t xl) {
+#ifdef JFSX_ABLATE_TRACE
+    const uint64_t trace_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     const BlkDev blk = blks[task.blk];
     const GcmSched *sch = sched + task.blk;
-    const uint32_t tid = threadIdx.x;
-
-    // ---- stage tables ----
-    {
-        const uint4 *ga = reinterpret_cast<const uint4 *>(tab.aes);
-        uint4 *la = reinterpret_cast<uint4 *>(lds + kLdsAes);
-        for (uint32_t i = tid; i < 4096; i += GcmShape<BS>::threads) la[i] = ga[i];
-        if (CRCMODE) {
-            const uint4 *gc = reinterpret_cast<const uint4 *>(tab.crc);
-            uint4 *lc = reinterpret_cast<uint4 *>(lds + kLdsCrc);
-            for (uint32_t i = tid; i < 1280; i += GcmShape<BS>::threads) lc[i] = gc[i];
-        }
-        if (tid < 128)
-            reinterpret_cast<uint4 *>(lds + kLdsBasis)[tid] = reinterpret_cast<const uint4 *>(sch->basis)[tid];
-    }
+    if (tid < 128)
+        reinterpret_cast<uint4 *>(lds + kLdsBasis)[tid] = reinterpret_cast<const uint4 *>(sch->basis)[tid];
+    if (tid < 256) reinterpret_cast<uint32_t *>(lds + kLdsSegRaw)[tid] = 0u;  // raw shares and flags
     __syncthreads();
     {
         uint4 *lg = reinterpret_cast<uint4 *>(lds + kLdsGh);
         const uint4 *lb = reinterpret_cast<const uint4 *>(lds + kLdsBasis);
-        for (uint32_t e = tid; e < 4096; e += GcmShape<BS>::threads) {
-            uint32_t b = e >> 4, j = e & 15;  // entry (b, j) at byte (b << 8) | (j << 4)
+#ifdef JFSX_ABLATE_GHBUILD
+        if (false)  // timing experiment only: wrong tags
+#endif
+        // entry (b, j) at byte (b << 8) | (j << 4) is the XOR of basis[8j + k]
+        // over the set bits 7 - k of b: a thread shares the six low bits' sum
+        // across the four entries that differ only in bits 7..6
+        for (uint32_t u = tid; u < 1024; u += GcmShape<BS>::threads) {
+            const uint32_t j = u & 15, blow = u >> 4;
             uint4 z = make_uint4(0, 0, 0, 0);
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                if ((b >> (7 - k)) & 1) {
-                    uint4 v = lb[8 * j + k];
+            for (int k = 2; k < 8; k++) {
+                if ((blow >> (7 - k)) & 1) {
+                    const uint4 v = lb[8 * j + k];
                     z.x ^= v.x; z.y ^= v.y; z.z ^= v.z; z.w ^= v.w;
                 }
             }
-            lg[e] = z;
+            const uint4 h0 = lb[8 * j], h1 = lb[8 * j + 1];
+            lg[(blow << 4) | j] = z;
+            lg[((blow | 64) << 4) | j] = make_uint4(z.x ^ h1.x, z.y ^ h1.y, z.z ^ h1.z, z.w ^ h1.w);
+            lg[((blow | 128) << 4) | j] = make_uint4(z.x ^ h0.x, z.y ^ h0.y, z.z ^ h0.z, z.w ^ h0.w);
+            lg[((blow | 192) << 4) | j] =
+                make_uint4(z.x ^ h0.x ^ h1.x, z.y ^ h0.y ^ h1.y, z.z ^ h0.z ^ h1.z, z.w ^ h0.w ^ h1.w);
         }
     }
     __syncthreads();
 
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;  // wave index in an SGPR
-    const uint32_t loff = ((lane & 31) << 2) | 0x00010000u;  // AES replica offset | table base
-    const GhLane gl = gh_lane(lane);
-    const uint32_t xl = CRCMODE ? tab.crcx[lane] : 0u;
     const uint64_t c0 = task.c0, c1 = task.c1;
     const uint32_t nseg = (uint32_t)((c1 - c0 + kSeg - 1) / kSeg);
     constexpr uint32_t V = GcmShape<BS>::waves * NS;  // virtual waves (streams) per task
 
+    // Row split (T-table kernel, one stream per wave): the task's rows are cut
+    // into 16 contiguous runs of equal length, so a task of any size keeps
+    // every wave busy (a 64 KiB block has 2 segments: with whole segments per
+    // wave 14 of 16 waves would idle).  A segment shared by two waves gets its
+    // CRC from both waves' raw shares (crc_segment_end, task end below).  The
+    // bitsliced kernel keys whole 32 KiB segments and keeps the segment split.
+    constexpr bool kRowSplit = !BS && NS == 1;
+    // in pairs of rows: every stream starts on an even row, as the two-row
+    // loop's segment-end test assumes (only its second row can end a segment)
+    const uint32_t npairs = (uint32_t)((c1 - c0 + 2047) / 2048);
     Stream st[NS];
 #pragma unroll
     for (int s = 0; s < NS; s++) {
         const uint32_t v = wave * NS + s;
-        const uint32_t sa = v * nseg / V, sb = (v + 1) * nseg / V;
-        st[s].sub0 = c0 + (uint64_t)sa * kSeg;
-        st[s].sub1 = sb > sa ? (c0 + (uint64_t)sb * kSeg < c1 ? c0 + (uint64_t)sb * kSeg : c1) : st[s].sub0;
+        if (kRowSplit) {
+            const uint32_t ra = 2 * (v * npairs / V), rb = 2 * ((v + 1) * npairs / V);
+            st[s].sub0 = c0 + (uint64_t)ra * 1024;
+            st[s].sub1 = rb > ra ? (c0 + (uint64_t)rb * 1024 < c1 ? c0 + (uint64_t)rb * 1024 : c1) : st[s].sub0;
+        } else {
+            const uint32_t sa = v * nseg / V, sb = (v + 1) * nseg / V;
+            st[s].sub0 = c0 + (uint64_t)sa * kSeg;
+            st[s].sub1 = sb > sa ? (c0 + (uint64_t)sb * kSeg < c1 ? c0 + (uint64_t)sb * kSeg : c1) : st[s].sub0;
+        }
         st[s].acc[0] = st[s].acc[1] = st[s].acc[2] = st[s].acc[3] = 0;
         st[s].jlast = 0;
         st[s].has = false;
         st[s].A = 0;
         st[s].lend = 0;
-        st[s].seg0 = st[s].sub0;
+        st[s].seg0 = c0 + (st[s].sub0 - c0) / kSeg * kSeg;  // start of the segment holding the stream's first row
     }
     // rows that are full for every non-empty stream: the fast path.  Empty
     // streams (tasks with fewer segments than streams) alias stream 0's loads
@@ -513,7 +576,7 @@ __global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *
                 if (CRCMODE) st[0].A = crc_piece<kLdsCrc>(lds, st[0].A, cq.x, cq.y, cq.z, cq.w);
             }
             if (CRCMODE) {
-                crc_segment_end<CRCMODE>(blk, tab, lane, xl, st[0].seg0, st[0].seg0 + kSeg, st[0].A, 0);
+                crc_segment_done<CRCMODE>(blk, tab, lane, xl, st[0].seg0, st[0].A, false, lds, c0);
                 st[0].A = 0;
                 st[0].seg0 += kSeg;
             }
@@ -541,6 +604,8 @@ __global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *
         uint32_t uw0 = 0;
         bool uwok = false;
 #endif
+        // task row index of the stream's first row: even (row pairs, see above)
+        const uint32_t rb0 = (uint32_t)((ld0[0] - c0) >> 11) << 1;
         for (; r0 + 1 < rf; r0 += 2) {
             const uint4 dd[2] = {n0, n1};
             const uint64_t o0 = ld0[0] + 1024 * r0 + lo;
@@ -597,8 +662,9 @@ __global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *
                 ghash_step(lds, st[0].acc, gl, c);
 #endif
                 if (CRCMODE) st[0].A = crc_piece<kLdsCrc>(lds, st[0].A, cq.x, cq.y, cq.z, cq.w);
-                if (CRCMODE && ((r0 + u) & 31) == 31) {
-                    crc_segment_end<CRCMODE>(blk, tab, lane, xl, st[0].seg0, st[0].seg0 + kSeg, st[0].A, 0);
+                if (CRCMODE && ((rb0 + (uint32_t)r0 + u) & 31) == 31) {
+                    crc_segment_done<CRCMODE>(blk, tab, lane, xl, st[0].seg0, st[0].A, st[0].seg0 < st[0].sub0, lds,
+                                              c0);
                     st[0].A = 0;
                     st[0].seg0 += kSeg;
                 }
@@ -630,11 +696,12 @@ __global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *
             ghash_step(lds, st[s].acc, gl, c);
             if (CRCMODE) st[s].A = crc_piece<kLdsCrc>(lds, st[s].A, cq.x, cq.y, cq.z, cq.w);
         }
-        if (CRCMODE && (r & 31) == 31) {
+        if (CRCMODE && ((uint32_t)((ld0[0] - c0) >> 10) + (uint32_t)r & 31) == 31) {
+            // (NS > 1 only with the segment split: every stream starts on a segment)
 #pragma unroll
             for (int s = 0; s < NS; s++) {
                 if (!act[s]) continue;
-                crc_segment_end<CRCMODE>(blk, tab, lane, xl, st[s].seg0, st[s].seg0 + kSeg, st[s].A, 0);
+                crc_segment_done<CRCMODE>(blk, tab, lane, xl, st[s].seg0, st[s].A, st[s].seg0 < st[s].sub0, lds, c0);
                 st[s].A = 0;
                 st[s].seg0 += kSeg;
             }
@@ -645,15 +712,20 @@ __global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *
         if (rf && act[s]) {
             st[s].has = true;
             st[s].jlast = (st[s].sub0 + 1024 * (rf - 1) + lo) >> 4;
-            st[s].lend = (uint32_t)(st[s].sub0 + 1024 * rf - st[s].seg0);  // only meaningful if mid-segment
-            if (st[s].lend) st[s].lend = st[s].lend - 1024 + (uint32_t)lo + 16;
         }
+        // lanes whose last piece lies in the last full row: their CRC shift to
+        // a segment end starts at that row's end (lend == 0, crc_segment_end)
+        const uint64_t tailRef = st[s].sub0 + 1024 * rf;
         // ragged remainder of this stream (block tail or unequal streams)
-        for (uint64_t row = st[s].sub0 + 1024 * rf; row < st[s].sub1; row += 1024)
-            st[s] = row_generic<OPEN, CRCMODE>(lds, loff, gl, sch, blk, tab, lane, xl, st[s], row);
-        // a stream that ended mid-segment on the fast path still owes that segment's CRC
+        for (uint64_t row = tailRef; row < st[s].sub1; row += 1024)
+            st[s] = row_generic<OPEN, CRCMODE>(lds, loff, gl, sch, blk, tab, lane, xl, st[s], row, c0, c1);
+        // a stream that ended inside a segment still owes that segment's CRC
+        // (or, when another wave holds the rest of the segment, its share)
         if (CRCMODE && act[s] && st[s].seg0 < st[s].sub1) {
-            crc_segment_end<CRCMODE>(blk, tab, lane, xl, st[s].seg0, st[s].sub1, st[s].A, st[s].lend);
+            const uint64_t seg1 = st[s].seg0 + kSeg < c1 ? st[s].seg0 + kSeg : c1;
+            crc_segment_end<CRCMODE>(blk, tab, lane, xl, st[s].seg0, seg1, st[s].A, st[s].lend, tailRef,
+                                     st[s].seg0 < st[s].sub0 || st[s].sub1 < seg1, lds,
+                                     (uint32_t)((st[s].seg0 - c0) / kSeg));
             st[s].seg0 = st[s].sub1;
         }
     }
@@ -668,7 +740,11 @@ __global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *
             const uint32_t e = (uint32_t)(wend + 1 - st[s].jlast);  // in [2, 65]
             uint32_t a[4];
             gh_rho_inv(st[s].acc, gl, a);
+#ifdef JFSX_ABLATE_LIFT
+            z = g_from_mem(a);  // timing experiment only: wrong tags
+#else
             z = g_mul(g_from_mem(a), g_from_mem(sch->hpow[e]));
+#endif
         }
         uint32_t zm[4];
         g_to_mem(z, zm);
@@ -688,6 +764,85 @@ __global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *
                 pexp[u] = 0;
             }
         }
+    }
+
+#ifdef JFSX_ABLATE_TRACE
+    __syncthreads();
+    if (tid == 0 && task.trace < 65536) {
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        g_wgtrace[4 * task.trace + 0] = trace_t0;
+        g_wgtrace[4 * task.trace + 1] = __builtin_amdgcn_s_memrealtime();
+        g_wgtrace[4 * task.trace + 2] = hw | ((uint64_t)xcc << 32);
+        g_wgtrace[4 * task.trace + 3] = task.c1 - task.c0;
+    }
+#endif
+    // ---- segments shared by two or more waves: sum the raw shares, finish ----
+    if (CRCMODE && kRowSplit) {
+        __syncthreads();
+        if (wave == 0) {
+            const uint32_t *raw = reinterpret_cast<const uint32_t *>(lds + kLdsSegRaw);
+            const uint32_t *flag = reinterpret_cast<const uint32_t *>(lds + kLdsSegFlag);
+            for (uint32_t k = lane; k < nseg; k += 64) {
+                if (!flag[k]) continue;
+                const uint64_t s0 = c0 + (uint64_t)k * kSeg;
+                const uint32_t Lseg = (uint32_t)((s0 + kSeg < c1 ? s0 + kSeg : c1) - s0);
+                const uint32_t K = Lseg == (uint32_t)kSeg ? tab.crcx[96]
+                                                          : crc_mulmod(crc_xpow8_fast(Lseg, tab.crcx), 0xffffffffu);
+                const uint32_t crc = ~(K ^ raw[k]);
+                const uint64_t si = s0 / kSeg;
+                if ((CRCMODE & 3) == 1)
+                    *reinterpret_cast<uint32_t *>(blk.crc + 4 * si) = __builtin_bswap32(crc);
+                else
+                    blk.crc_calc[si] = crc;
+            }
+        }
+    }
+}
+
+// gcm_main: persistent workgroups, one per CU (the LDS tables allow one),
+// taking tasks from a queue until it is empty.  The AES and CRC tables are
+// staged once per workgroup.  Tasks come largest first (the host sorts them),
+// so the queue's tail is made of small tasks.  A grid of one workgroup per
+// task would leave CUs idle between tasks of mixed sizes: workgroups are
+// dispatched in order, round-robin over the XCDs, and the next one waits for
+// a CU of its own XCD (measured with the TRACE variant on configs[4]'s
+// 64 KiB-4 MiB blocks: CUs 79 % busy, 115 us mean gap between tasks).
+template <bool OPEN, int CRCMODE, int NS, int BS>
+__global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *__restrict__ tasks, uint32_t ntasks,
+                                                       uint32_t *__restrict__ queue,
+                                                       const BlkDev *__restrict__ blks,
+                                                       const GcmSched *__restrict__ sched,
+                                                       uint32_t *__restrict__ partial, uint32_t *__restrict__ pexp,
+                                                       DevTables tab) {
+    __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
+    __shared__ uint32_t s_task;
+    const uint32_t tid = threadIdx.x;
+    {
+        const uint4 *ga = reinterpret_cast<const uint4 *>(tab.aes);
+        uint4 *la = reinterpret_cast<uint4 *>(lds + kLdsAes);
+        for (uint32_t i = tid; i < 4096; i += GcmShape<BS>::threads) la[i] = ga[i];
+        if (CRCMODE) {
+            const uint4 *gc = reinterpret_cast<const uint4 *>(tab.crc);
+            uint4 *lc = reinterpret_cast<uint4 *>(lds + kLdsCrc);
+            for (uint32_t i = tid; i < 1280; i += GcmShape<BS>::threads) lc[i] = gc[i];
+        }
+    }
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;  // wave index in an SGPR
+    const uint32_t loff = ((lane & 31) << 2) | 0x00010000u;  // AES replica offset | table base
+    const GhLane gl = gh_lane(lane);
+    const uint32_t xl = CRCMODE ? tab.crcx[lane] : 0u;
+    if (tid == 0) s_task = atomicAdd(queue, 1u);
+    for (;;) {
+        // also orders this task's table writes after the previous task's readers
+        __syncthreads();
+        const uint32_t ti = __builtin_amdgcn_readfirstlane(s_task);
+        if (ti >= ntasks) break;  // the same for every wave: the queue is exhausted
+        __syncthreads();          // every wave holds ti: s_task may take the next index
+        if (tid == 0) s_task = atomicAdd(queue, 1u);  // the next task's index arrives during this one
+        gcm_task<OPEN, CRCMODE, NS, BS>(lds, tasks[ti], blks, sched, partial, pexp, tab, tid, wave, lane, loff, gl,
+                                        xl);
     }
 }
 
@@ -866,17 +1021,20 @@ void launch_gcm_keysetup(hipStream_t s, int n, const KeyIn *keys, const BlkDev *
     if (n > 0) hipLaunchKernelGGL(gcm_keysetup_k, dim3(n), dim3(64), 0, s, keys, blks, sched, t.aes);
 }
 
-void launch_gcm_main(hipStream_t s, int ntasks, bool open, int crc_mode, bool bitslice, const Task *tasks,
-                     const BlkDev *blks, const GcmSched *sched, uint32_t *partial, uint32_t *pexp, DevTables t) {
+void launch_gcm_main(hipStream_t s, int ntasks, int ncu, uint32_t *queue, bool open, int crc_mode, bool bitslice,
+                     const Task *tasks, const BlkDev *blks, const GcmSched *sched, uint32_t *partial, uint32_t *pexp,
+                     DevTables t) {
     if (ntasks <= 0) return;
+    const unsigned grid = (unsigned)(ntasks < ncu ? ntasks : ncu);  // persistent: one workgroup per CU
+    (void)hipMemsetAsync(queue, 0, 4, s);
 #define L(O, C)                                                                                              \
     do {                                                                                                     \
         if (bitslice)                                                                                        \
-            hipLaunchKernelGGL((gcm_main_k<O, C, 1, 1>), dim3(ntasks), dim3(GcmShape<1>::threads), 0, s, tasks, \
-                               blks, sched, partial, pexp, t);                                               \
+            hipLaunchKernelGGL((gcm_main_k<O, C, 1, 1>), dim3(grid), dim3(GcmShape<1>::threads), 0, s, tasks,    \
+                               (uint32_t)ntasks, queue, blks, sched, partial, pexp, t);                      \
         else                                                                                                 \
-            hipLaunchKernelGGL((gcm_main_k<O, C, kStreams, 0>), dim3(ntasks), dim3(GcmShape<0>::threads), 0, s, \
-                               tasks, blks, sched, partial, pexp, t);                                        \
+            hipLaunchKernelGGL((gcm_main_k<O, C, kStreams, 0>), dim3(grid), dim3(GcmShape<0>::threads), 0, s,    \
+                               tasks, (uint32_t)ntasks, queue, blks, sched, partial, pexp, t);               \
     } while (0)
     switch ((open ? 8 : 0) | crc_mode) {
         case 8: L(true, 0); break;
@@ -906,3 +1064,10 @@ void launch_gcm_finalize(hipStream_t s, int n, bool open, int crc_mode, const Bl
 }
 
 }  // namespace jfsx
+
+#ifdef JFSX_ABLATE_TRACE
+extern "C" __attribute__((visibility("default"))) int jfsx_debug_wgtrace(uint64_t *out, int n) {
+    if (n > 65536) n = 65536;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(jfsx::g_wgtrace), 32 * (size_t)n) == hipSuccess ? 0 : -5;
+}
+#endif

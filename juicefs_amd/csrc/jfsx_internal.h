@@ -79,6 +79,9 @@ struct Task {
     uint32_t blk;
     uint32_t slot0;
     uint64_t c0, c1;  // byte range of the block; c0 % kSeg == 0
+#ifdef JFSX_ABLATE_TRACE
+    uint32_t trace, pad;  // diagnostic builds: index in the planned order
+#endif
 };
 
 struct BlkOut {        // written by finalize, copied back to the host
@@ -224,6 +227,19 @@ __device__ __forceinline__ uint32_t crc_xpow8(uint64_t n, const uint32_t *x8pow)
     return r;
 }
 
+// x^(8n) mod P for n < 32768 from the context's crcx table: whole 1 KiB rows
+// (crcx[96 + k] = x^(8*1024k)), then 16-byte steps (crcx[63 - j] =
+// x^(8*16j)), then the last 0..15 bytes by squares (crcx[64 + b]) -- at most
+// five products instead of one per set bit of n
+__device__ __forceinline__ uint32_t crc_xpow8_fast(uint32_t n, const uint32_t *crcx) {
+    const uint32_t k = n >> 10, j = (n >> 4) & 63, r = n & 15;
+    uint32_t v = k ? crcx[96 + k] : 0x80000000u;
+    if (j) v = k ? crc_mulmod(v, crcx[63 - j]) : crcx[63 - j];
+    for (int b = 0; b < 4; b++)
+        if ((r >> b) & 1) v = crc_mulmod(v, crcx[64 + b]);
+    return v;
+}
+
 // wave-wide XOR reduction
 __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
     for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off, 64);
@@ -242,8 +258,10 @@ struct DevTables {
 };
 void launch_gcm_keysetup(hipStream_t s, int n, const KeyIn *keys, const BlkDev *blks, GcmSched *sched,
                          DevTables t);
-void launch_gcm_main(hipStream_t s, int ntasks, bool open, int crc_mode, bool bitslice, const Task *tasks,
-                     const BlkDev *blks, const GcmSched *sched, uint32_t *partial, uint32_t *pexp, DevTables t);
+// persistent over min(ntasks, ncu) workgroups; queue: 4 device bytes (zeroed here, on s)
+void launch_gcm_main(hipStream_t s, int ntasks, int ncu, uint32_t *queue, bool open, int crc_mode, bool bitslice,
+                     const Task *tasks, const BlkDev *blks, const GcmSched *sched, uint32_t *partial, uint32_t *pexp,
+                     DevTables t);
 void launch_gcm_finalize(hipStream_t s, int n, bool open, int crc_mode, const BlkDev *blks, const GcmSched *sched,
                          const uint32_t *partial, const uint32_t *pexp, BlkOut *out);
 void launch_cp_keysetup(hipStream_t s, int n, const KeyIn *keys, const BlkDev *blks, CpSched *sched);

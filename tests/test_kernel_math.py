@@ -176,3 +176,28 @@ def test_lane_strided_ghash_matches_gcm(nbytes, wave_bytes):
     L = bytes(8) + (8 * nbytes).to_bytes(8, "big")
     init = _xor(EJ0, _gmul(L, H))
     assert _xor(init, S) == tag
+
+
+def xpow8_fast(n, crcx):
+    """crc_xpow8_fast (jfsx_internal.h): whole rows, 16-byte steps, then squares."""
+    k, j, r = n >> 10, (n >> 4) & 63, n & 15
+    v = int(crcx[96 + k]) if k else 0x80000000
+    if j:
+        v = mulmod(v, int(crcx[63 - j])) if k else int(crcx[63 - j])
+    for b in range(4):
+        if (r >> b) & 1:
+            v = mulmod(v, int(crcx[64 + b]))
+    return v
+
+
+def test_fast_shift_powers_match_squares(tables):
+    """The row-shift table crcx[97..127] and the three-step x^(8n) agree with
+    the square-and-multiply powers for every distance a segment can need."""
+    _, _, crcx = tables
+    x8 = crcx[64:96]
+    for k in range(1, 32):
+        assert int(crcx[96 + k]) == xpow8(1024 * k, x8), k
+    rng = np.random.default_rng(3)
+    for n in [0, 1, 15, 16, 17, 1008, 1023, 1024, 1025, 32767, 31 * 1024, 31 * 1024 + 1008] + \
+            [int(x) for x in rng.integers(0, 32768, 300)]:
+        assert xpow8_fast(n, crcx) == xpow8(n, x8), n
