@@ -231,6 +231,18 @@ Plan plan_tasks(const std::vector<uint64_t> &lens, uint64_t max_bytes, uint32_t 
 
 bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
 
+// tasks reordered by size, largest first, in units of 4 KiB (stable within a unit)
+void order_largest_first(Task *t, size_t n, size_t max_units) {
+    bool sorted = true;
+    for (size_t i = 1; i < n && sorted; i++) sorted = ((t[i - 1].c1 - t[i - 1].c0) >> 12) >= ((t[i].c1 - t[i].c0) >> 12);
+    if (sorted) return;
+    std::vector<size_t> start(max_units + 2, 0);
+    for (size_t i = 0; i < n; i++) start[max_units - std::min<size_t>((t[i].c1 - t[i].c0) >> 12, max_units) + 1]++;
+    for (size_t u = 1; u < start.size(); u++) start[u] += start[u - 1];
+    std::vector<Task> tmp(t, t + n);
+    for (size_t i = 0; i < n; i++) t[start[max_units - std::min<size_t>((tmp[i].c1 - tmp[i].c0) >> 12, max_units)]++] = tmp[i];
+}
+
 constexpr uint64_t kGcmMaxLen = (((uint64_t)1 << 32) - 2) * 16;
 constexpr uint64_t kCpMaxLen = ((uint64_t)1 << 38) - 64;
 
@@ -325,10 +337,11 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, int k, int algo, bool
 #ifdef JFSX_ABLATE_TRACE
         for (size_t t = 0; t < nt; t++) ht[t].trace = (uint32_t)t;
 #endif
-        // the persistent GCM kernel takes tasks in array order: largest first,
-        // so that the last tasks handed out are short (slots stay per task)
-        if (gcm)
-            std::stable_sort(ht, ht + nt, [](const Task &a, const Task &b) { return a.c1 - a.c0 > b.c1 - b.c0; });
+        // the persistent transform kernels take tasks in array order: largest
+        // first, so that the last tasks handed out are short (slots stay per
+        // task).  A counting sort on 4 KiB units: O(n), on the host's
+        // critical path for every batch
+        order_largest_first(ht, nt, (size_t)(gcm ? kMaxTaskBytes : kCpTaskBytes) >> 12);
     }
     if (up) {
         HIP_OK(hipMemcpyAsync(d, h, h_bytes, hipMemcpyHostToDevice, up));
@@ -358,7 +371,8 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, int k, int algo, bool
         CpSched *dsch = (CpSched *)(d + o_sched);
         launch_cp_keysetup(s, n, dk, db, dsch);
         if (c->timing) HIP_OK(hipEventRecord(c->ev_k0[k], s));
-        launch_cp_main(s, (int)nt, open, crc_mode, dt, db, dsch, dpart, dpexp, c->tabs);
+        launch_cp_main(s, (int)nt, c->ncu, (uint32_t *)(d + o_queue), open, crc_mode, dt, db, dsch, dpart, dpexp,
+                       c->tabs);
         if (c->timing) HIP_OK(hipEventRecord(c->ev_k1[k], s));
         launch_cp_finalize(s, n, open, crc_mode, db, dsch, dpart, dpexp, dout);
     }

@@ -346,23 +346,14 @@ __device__ __noinline__ CpStream cp_row_generic(const char *lds, const CpSched *
     return st;
 }
 
+// One task (a block's <= 1 MiB range) on the workgroup's four waves, whole
+// 32 KiB segments per wave; the CRC tables are already in LDS.
 template <bool OPEN, int CRCMODE>
-__global__ __launch_bounds__(kCpWaves * 64) void cp_main_k(const Task *__restrict__ tasks,
-                                                          const BlkDev *__restrict__ blks,
-                                                          const CpSched *__restrict__ sched,
-                                                          uint32_t *__restrict__ partial, uint32_t *__restrict__ pexp,
-                                                          DevTables tab) {
-    __shared__ __attribute__((aligned(16))) char lds[CRCMODE ? 24576 : 16];
-    const Task task = tasks[blockIdx.x];
+__device__ __forceinline__ void cp_task(const char *lds, const Task task, const BlkDev *__restrict__ blks,
+                                        const CpSched *__restrict__ sched, uint32_t *__restrict__ partial,
+                                        uint32_t *__restrict__ pexp, const DevTables &tab, uint32_t tid) {
     const BlkDev blk = blks[task.blk];
     const CpSched *sch = sched + task.blk;
-    const uint32_t tid = threadIdx.x;
-    if (CRCMODE) {
-        const uint4 *gc = reinterpret_cast<const uint4 *>(tab.crc);
-        uint4 *lc = reinterpret_cast<uint4 *>(lds);
-        for (uint32_t i = tid; i < 1536; i += kCpWaves * 64) lc[i] = gc[i];
-        __syncthreads();
-    }
     uint32_t key[8], nonce[3];
 #pragma unroll
     for (int i = 0; i < 8; i++) key[i] = sch->key[i];
@@ -446,6 +437,36 @@ __global__ __launch_bounds__(kCpWaves * 64) void cp_main_k(const Task *__restric
         for (int i = 0; i < 5; i++) partial[8 * slot + i] = z.l[i];
         const uint64_t nblk = (blk.len + 15) >> 4;
         pexp[slot] = (uint32_t)(nblk - wend);
+    }
+}
+
+// cp_main: persistent workgroups (kCpGroupsPerCu per CU, the occupancy the
+// kernel's registers allow) taking tasks, largest first, from a queue; the
+// CRC tables are staged once per workgroup.  See gcm_main_k for why a grid of
+// one workgroup per task leaves CUs idle on mixed block sizes.
+template <bool OPEN, int CRCMODE>
+__global__ __launch_bounds__(kCpWaves * 64) void cp_main_k(const Task *__restrict__ tasks, uint32_t ntasks,
+                                                          uint32_t *__restrict__ queue,
+                                                          const BlkDev *__restrict__ blks,
+                                                          const CpSched *__restrict__ sched,
+                                                          uint32_t *__restrict__ partial, uint32_t *__restrict__ pexp,
+                                                          DevTables tab) {
+    __shared__ __attribute__((aligned(16))) char lds[CRCMODE ? 24576 : 16];
+    __shared__ uint32_t s_task;
+    const uint32_t tid = threadIdx.x;
+    if (CRCMODE) {
+        const uint4 *gc = reinterpret_cast<const uint4 *>(tab.crc);
+        uint4 *lc = reinterpret_cast<uint4 *>(lds);
+        for (uint32_t i = tid; i < 1536; i += kCpWaves * 64) lc[i] = gc[i];
+    }
+    if (tid == 0) s_task = atomicAdd(queue, 1u);
+    for (;;) {
+        __syncthreads();
+        const uint32_t ti = __builtin_amdgcn_readfirstlane(s_task);
+        if (ti >= ntasks) break;  // the same for every wave: the queue is exhausted
+        __syncthreads();          // every wave holds ti: s_task may take the next index
+        if (tid == 0) s_task = atomicAdd(queue, 1u);
+        cp_task<OPEN, CRCMODE>(lds, tasks[ti], blks, sched, partial, pexp, tab, tid);
     }
 }
 
@@ -542,11 +563,14 @@ void launch_cp_keysetup(hipStream_t s, int n, const KeyIn *keys, const BlkDev *b
     if (n > 0) hipLaunchKernelGGL(cp_keysetup_k, dim3(n), dim3(64), 0, s, keys, blks, sched);
 }
 
-void launch_cp_main(hipStream_t s, int ntasks, bool open, int crc_mode, const Task *tasks, const BlkDev *blks,
-                    const CpSched *sched, uint32_t *partial, uint32_t *pexp, DevTables t) {
+void launch_cp_main(hipStream_t s, int ntasks, int ncu, uint32_t *queue, bool open, int crc_mode, const Task *tasks,
+                    const BlkDev *blks, const CpSched *sched, uint32_t *partial, uint32_t *pexp, DevTables t) {
     if (ntasks <= 0) return;
-    dim3 g(ntasks), bl(kCpWaves * 64);
-#define L(O, C) hipLaunchKernelGGL((cp_main_k<O, C>), g, bl, 0, s, tasks, blks, sched, partial, pexp, t)
+    const int groups = ncu * kCpGroupsPerCu;
+    dim3 g(ntasks < groups ? ntasks : groups), bl(kCpWaves * 64);
+    (void)hipMemsetAsync(queue, 0, 4, s);
+#define L(O, C) hipLaunchKernelGGL((cp_main_k<O, C>), g, bl, 0, s, tasks, (uint32_t)ntasks, queue, blks, sched, \
+                                   partial, pexp, t)
     switch ((open ? 8 : 0) | crc_mode) {
         case 8: L(true, 0); break;
         case 9: L(true, 1); break;

@@ -121,6 +121,7 @@ struct CpSched {
 constexpr uint64_t kCrcTaskBytes = 4 << 20;  // bytes per CRC-only task (crc_segments_k)
 constexpr int kCpWaves = 4;                 // waves per ChaCha20-Poly1305 workgroup
 constexpr int kCpTaskBytes = 1 << 20;       // bytes per ChaCha task (<= kCpWaves * segments)
+constexpr int kCpGroupsPerCu = 4;           // cp_main_k occupancy: 4 waves/SIMD at <= 128 VGPRs
 
 // ---------------------------------------------------------------------------
 // GF(2^128) in GCM convention.  "BE words": w[0] holds bytes 0..3 big-endian;
@@ -265,8 +266,8 @@ void launch_gcm_main(hipStream_t s, int ntasks, int ncu, uint32_t *queue, bool o
 void launch_gcm_finalize(hipStream_t s, int n, bool open, int crc_mode, const BlkDev *blks, const GcmSched *sched,
                          const uint32_t *partial, const uint32_t *pexp, BlkOut *out);
 void launch_cp_keysetup(hipStream_t s, int n, const KeyIn *keys, const BlkDev *blks, CpSched *sched);
-void launch_cp_main(hipStream_t s, int ntasks, bool open, int crc_mode, const Task *tasks, const BlkDev *blks,
-                    const CpSched *sched, uint32_t *partial, uint32_t *pexp, DevTables t);
+void launch_cp_main(hipStream_t s, int ntasks, int ncu, uint32_t *queue, bool open, int crc_mode, const Task *tasks,
+                    const BlkDev *blks, const CpSched *sched, uint32_t *partial, uint32_t *pexp, DevTables t);
 void launch_cp_finalize(hipStream_t s, int n, bool open, int crc_mode, const BlkDev *blks, const CpSched *sched,
                         const uint32_t *partial, const uint32_t *pexp, BlkOut *out);
 void launch_crc_segments(hipStream_t s, int ntasks, const Task *tasks, const BlkDev *blks, DevTables t);
