@@ -369,7 +369,7 @@ def main():
         dist.destroy_process_group()
 
 
-PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r1", "pmc_traffic.json")
+PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r2", "pmc_traffic.json")
 
 
 def pmc_traffic(args, plain_per_launch):
@@ -385,7 +385,7 @@ def pmc_traffic(args, plain_per_launch):
         return None, None
     if args.crc != "full":
         return None, None
-    return int(k["bytes_per_plain_byte"] * plain_per_launch), "profiles/r1/pmc_traffic.json (%s)" % k["kernel"]
+    return int(k["bytes_per_plain_byte"] * plain_per_launch), "profiles/r2/pmc_traffic.json (%s, %s)" % (k["kernel"], k.get("batch", ""))
 
 
 def pcie_probe(eng, nbytes=1 << 30):
