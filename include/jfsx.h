@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define JFSX_ABI_VERSION 4
+#define JFSX_ABI_VERSION 5
 
 /* algorithms (encrypt.go:142-145) */
 #define JFSX_AES256GCM 0     /* "aes256gcm-rsa" (also the "" default)   */
@@ -72,6 +72,7 @@ extern "C" {
 #define JFSX_ETAG 1 /* AEAD authentication failed (Go: cipher's errOpen)      */
 #define JFSX_ECRC 2 /* "data checksum %d != expect %d" (disk_cache.go:1324)   */
 #define JFSX_EOF 3  /* jfsx_cache_verify: short read (File.ReadAt's io.EOF)    */
+#define JFSX_EFORMAT 4 /* malformed LZ4 block (lz4.DecompressSafe's error)      */
 
 /* batch-level errors */
 #define JFSX_EINVAL (-22)
@@ -282,6 +283,33 @@ int jfsx_rsa_oaep_decrypt_batch(jfsx_ctx *ctx, const jfsx_rsa_key *key, int n, c
  * big-endian 32 KiB segment CRCs of C that a GEN|CT batch returned */
 int jfsx_object_crc32c(const void *hdr, uint64_t hlen, const uint8_t *seg_crcs, uint64_t clen,
                        const uint8_t *tag, uint32_t *out);
+
+/* LZ4 block stage: the "lz4" Compressor of pkg/compress
+ * (compress.go:107-125) that cachedStore.upload runs before the object is
+ * put (cached_store.go:371-392) and cachedStore.load after it is read
+ * (:680-745).  Bytes are those of the LZ4 C library the reference binds
+ * through github.com/hungys/go-lz4: jfsx_lz4_compress_batch writes what
+ * LZ4_compress_default(src, dst, len, bound) writes; jfsx_lz4_decompress_batch
+ * decodes as LZ4_decompress_safe(src, dst, len, cap) does (status
+ * JFSX_EFORMAT where it returns < 0).  One zblk per block: compress needs
+ * dst_cap >= jfsx_lz4_bound(src_len) (JFSX_EINVAL otherwise), as
+ * cachedStore.upload's CompressBound-sized buffer; src_len <= 0x7E000000.
+ * mem = JFSX_MEM_DEVICE or JFSX_MEM_HOST.  The empty-input error of
+ * LZ4.Decompress ("decompress an empty input") is the caller's: a zero-length
+ * src decodes as LZ4_decompress_safe does (JFSX_EFORMAT). */
+typedef struct jfsx_zblk {
+    const void *src;
+    uint64_t src_len;
+    void *dst;
+    uint64_t dst_cap;
+    uint64_t out_len;  /* out: bytes written to dst                      */
+    int32_t status;    /* out: JFSX_OK / JFSX_EFORMAT (decompress)       */
+    int32_t reserved;
+} jfsx_zblk;
+/* LZ4_compressBound: n + n/255 + 16 (0 for n > 0x7E000000) */
+uint64_t jfsx_lz4_bound(uint64_t n);
+int jfsx_lz4_compress_batch(jfsx_ctx *ctx, int n, jfsx_zblk *blks, int mem);
+int jfsx_lz4_decompress_batch(jfsx_ctx *ctx, int n, jfsx_zblk *blks, int mem);
 
 /* header helper: returns wrapped-key length and offset/size of the nonce so a
  * caller can unwrap the key first (encrypt.go:197-205) */

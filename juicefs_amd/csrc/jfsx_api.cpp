@@ -709,6 +709,73 @@ int run_crc_host(jfsx_ctx *c, int n, jfsx_range *r, int mode) {
     return 0;
 }
 
+constexpr uint64_t kLz4MaxInput = 0x7E000000ull;  // LZ4_MAX_INPUT_SIZE
+uint64_t lz4_bound(uint64_t n) { return n > kLz4MaxInput ? 0 : n + n / 255 + 16; }
+
+// LZ4 stage (jfsx_lz4.hip): one wave per block.  Host-memory batches are
+// staged through the context's slot-0 staging buffer (inputs up, the
+// out_len bytes of each output down).
+int run_lz4(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, bool comp) {
+    if (n < 0 || (mem != JFSX_MEM_DEVICE && mem != JFSX_MEM_HOST)) return JFSX_EINVAL;
+    for (int i = 0; i < n; i++) {
+        if ((z[i].src_len && !z[i].src) || (z[i].dst_cap && !z[i].dst) || z[i].src_len > kLz4MaxInput ||
+            z[i].dst_cap > ((uint64_t)1 << 32))
+            return JFSX_EINVAL;
+        if (comp && z[i].dst_cap < lz4_bound(z[i].src_len)) return JFSX_EINVAL;
+    }
+    if (n == 0) return 0;
+    int rc;
+    Workspace &w = c->ws[0];
+    const size_t o_out = align256(sizeof(ZDev) * n), dbytes = o_out + align256(sizeof(ZOut) * n);
+    if ((rc = ensure_dev(c, &w.d, &w.dcap, dbytes))) return rc;
+    if ((rc = ensure_host(&w.h, &w.hcap, dbytes))) return rc;
+    hipStream_t s = c->stream;
+    ZDev *hz = (ZDev *)w.h;
+    std::vector<char *> sdst(n, nullptr);
+    if (mem == JFSX_MEM_HOST) {
+        size_t need = 0;
+        for (int i = 0; i < n; i++) need += align256(z[i].src_len) + align256(z[i].dst_cap);
+        if ((rc = ensure_dev(c, &w.stage, &w.scap, std::max<size_t>(need, 256)))) return rc;
+        size_t off = 0;
+        for (int i = 0; i < n; i++) {
+            char *in = w.stage + off;
+            off += align256(z[i].src_len);
+            sdst[i] = w.stage + off;
+            off += align256(z[i].dst_cap);
+            if (z[i].src_len) HIP_OK(hipMemcpyAsync(in, z[i].src, z[i].src_len, hipMemcpyHostToDevice, s));
+            hz[i] = ZDev{(const uint8_t *)in, (uint8_t *)sdst[i], z[i].src_len, z[i].dst_cap};
+        }
+    } else {
+        for (int i = 0; i < n; i++)
+            hz[i] = ZDev{(const uint8_t *)z[i].src, (uint8_t *)z[i].dst, z[i].src_len, z[i].dst_cap};
+    }
+    HIP_OK(hipMemcpyAsync(w.d, w.h, sizeof(ZDev) * n, hipMemcpyHostToDevice, s));
+    if (c->timing) HIP_OK(hipEventRecord(c->ev_k0[0], s));
+    if (comp)
+        launch_lz4_compress(s, n, (const ZDev *)w.d, (ZOut *)(w.d + o_out));
+    else
+        launch_lz4_decompress(s, n, (const ZDev *)w.d, (ZOut *)(w.d + o_out));
+    if (c->timing) HIP_OK(hipEventRecord(c->ev_k1[0], s));
+    HIP_OK(hipGetLastError());
+    ZOut *ho = (ZOut *)(w.h + o_out);
+    HIP_OK(hipMemcpyAsync(ho, w.d + o_out, sizeof(ZOut) * n, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    if (c->timing) {
+        float ms = 0;
+        HIP_OK(hipEventElapsedTime(&ms, c->ev_k0[0], c->ev_k1[0]));
+        c->ms_total += ms;
+        c->launches += 1;
+    }
+    for (int i = 0; i < n; i++) {
+        z[i].out_len = ho[i].out_len;
+        z[i].status = ho[i].status;
+        if (mem == JFSX_MEM_HOST && ho[i].out_len)
+            HIP_OK(hipMemcpyAsync(z[i].dst, sdst[i], ho[i].out_len, hipMemcpyDeviceToHost, s));
+    }
+    if (mem == JFSX_MEM_HOST) HIP_OK(hipStreamSynchronize(s));
+    return 0;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -896,6 +963,22 @@ int jfsx_crc32c_segments(jfsx_ctx *c, int n, jfsx_range *ranges, int mode, int m
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
     return mem == JFSX_MEM_HOST ? run_crc_host(c, n, ranges, mode) : run_crc(c, n, ranges, mode);
+}
+
+uint64_t jfsx_lz4_bound(uint64_t n) { return lz4_bound(n); }
+
+int jfsx_lz4_compress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
+    if (!c || (n > 0 && !blks)) return JFSX_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    return run_lz4(c, n, blks, mem, true);
+}
+
+int jfsx_lz4_decompress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
+    if (!c || (n > 0 && !blks)) return JFSX_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    return run_lz4(c, n, blks, mem, false);
 }
 
 int jfsx_checksum(jfsx_ctx *c, const void *data, uint64_t len, uint8_t *out) {

@@ -53,6 +53,14 @@ constexpr int kThreads = kWaves * 64;
 #ifndef JFSX_RKR
 #define JFSX_RKR 1
 #endif
+// Poly1305 limb sums with the addend in the first v_mad_u64_u32 (mad64, jfsx_chacha.hip).
+#ifndef JFSX_CPMAD
+#define JFSX_CPMAD 0
+#endif
+// ChaCha "d = rotl16(d ^ a)" as two SDWA word XORs instead of v_xor + v_alignbit.
+#ifndef JFSX_CPROT16
+#define JFSX_CPROT16 0
+#endif
 constexpr int kStreams = JFSX_STREAMS;        // independent segment streams per wave (ILP)
 constexpr int kSlotsPerTask = kWaves * kStreams;  // GHASH/Poly partial slots per task
 constexpr int kMaxTaskBytes = 4 << 20;
@@ -82,6 +90,19 @@ struct Task {
 #ifdef JFSX_ABLATE_TRACE
     uint32_t trace, pad;  // diagnostic builds: index in the planned order
 #endif
+};
+
+// LZ4 stage (jfsx_lz4.hip): one block per wave
+struct ZDev {
+    const uint8_t *src;
+    uint8_t *dst;
+    uint64_t len;  // input bytes
+    uint64_t cap;  // dst capacity
+};
+struct ZOut {
+    uint64_t out_len;
+    int32_t status;
+    int32_t pad;
 };
 
 struct BlkOut {        // written by finalize, copied back to the host
@@ -275,6 +296,8 @@ void launch_crc_finalize(hipStream_t s, int n, int crc_mode, const BlkDev *blks,
 void launch_gen_synthetic(hipStream_t s, uint8_t *dst, uint64_t len, uint64_t seed, uint64_t block);
 void launch_gen_synthetic_batch(hipStream_t s, uint8_t *dst, uint64_t stride, int n, const uint64_t *lens,
                                 uint64_t seed, uint64_t block0);
+void launch_lz4_compress(hipStream_t s, int n, const ZDev *blks, ZOut *outs);
+void launch_lz4_decompress(hipStream_t s, int n, const ZDev *blks, ZOut *outs);
 // batched RSA-OAEP unwrap (jfsx_rsa.hip): key = device jfsx_rsa::Key
 void async_detach(jfsx_ctx *c);  // jfsx_agg.cpp
 void launch_rsa_unwrap(hipStream_t s, const void *key, int n, const uint8_t *ct, uint32_t *mh, uint8_t *em,

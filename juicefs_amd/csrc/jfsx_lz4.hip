@@ -1,0 +1,412 @@
+// jfsx_lz4.hip -- LZ4 block compression / decompression (gfx950), the
+// compression stage of the compressed block path.
+//
+// Replaces, per block, LZ4.Compress = lz4.CompressDefault(src, dst) and
+// LZ4.Decompress = lz4.DecompressSafe(src, dst) (pkg/compress/compress.go:
+// 107-125, github.com/hungys/go-lz4 over the LZ4 C library), called by
+// cachedStore.upload before the object is put (pkg/chunk/cached_store.go:
+// 371-392: dst sized CompressBound(len)) and by cachedStore.load after the
+// object is read (:680-745).  Output bytes are those of LZ4_compress_default
+// (acceleration 1) and the accept/reject rules of LZ4_decompress_safe, as
+// restated in oracle/jfs_lz4.c and pinned there against liblz4.
+//
+// The greedy LZ4 parse is sequential per block, so a block is one wave and
+// the wave's 64 lanes work on the parse together (no MFMA, no cross-block
+// state; blocks shard like the AEAD blocks):
+//   * match search: the compressor probes positions ip, ip+1, ... with a step
+//     that grows by one every 64 misses.  Those positions depend only on the
+//     search start, so a wave evaluates 64 probes at once (lane j = probe
+//     k0 + j): hash, hash-table read, distance check, 4-byte compare.  Probes
+//     of the same batch that share a hash bucket see each other's table
+//     writes in probe order (13 ballots give each lane the lanes of its
+//     bucket); the first succeeding probe ends the search and only the probes
+//     before it write the table, last writer per bucket.
+//   * backward extension, match-length count, literal and 255-run copies:
+//     64 (or 256) bytes per step with a ballot for the first difference.
+//   * the 16 KiB hash table (4096 x u32 for inputs >= 64 KiB + 11 B, else
+//     8192 x u16) lives in LDS: 10 waves per CU.
+// The decompressor parses tokens from a 256-byte window of the input held in
+// the wave's VGPRs (one dword per lane, read back with v_readlane) and copies
+// literals / matches 64 bytes per step; a match reads only output written
+// before it (overlapping matches are expanded as out[op+i] = out[op-off+i%off]),
+// after the wave's earlier stores have completed (s_waitcnt vmcnt(0)).
+#include "jfsx_dev.h"
+
+namespace jfsx {
+
+namespace {
+
+constexpr uint32_t kMinMatch = 4, kMfLimit = 12, kLastLit = 5, kLimit64K = 65536 + kMfLimit - 1;
+
+typedef __attribute__((address_space(1))) const uint32_t gcu32;
+typedef __attribute__((address_space(1))) const uint8_t gcu8;
+typedef __attribute__((address_space(1))) uint8_t gu8;
+
+__device__ __forceinline__ uint32_t ld32a(const uint8_t *p) { return *(gcu32 *)p; }
+__device__ __forceinline__ uint32_t ld8(const uint8_t *p) { return *(gcu8 *)p; }
+__device__ __forceinline__ void st8(uint8_t *p, uint32_t v) { *(gu8 *)p = (uint8_t)v; }
+
+// 4 bytes at any address: two aligned dword loads, each holding at least one
+// of the requested bytes (so neither touches a page the bytes are not on)
+__device__ __forceinline__ uint32_t ld32u(const uint8_t *a) {
+    const uintptr_t x = (uintptr_t)a;
+    const uint8_t *b = (const uint8_t *)(x & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(x & 3);
+    const uint32_t w0 = ld32a(b), w1 = ld32a(sh ? b + 4 : b);
+    return __builtin_amdgcn_alignbyte(w1, w0, sh);
+}
+
+__device__ __forceinline__ uint32_t lz_hash(const uint8_t *p, bool small) {
+    const uint32_t w = ld32u(p);
+    if (small) return (w * 2654435761u) >> (32 - 13);
+    const uint64_t v = (uint64_t)w | ((uint64_t)ld8(p + 4) << 32);  // LZ4_hash5: the read's low 5 bytes
+    return (uint32_t)(((v << 24) * 889523592379ull) >> (64 - 12));
+}
+
+// offset of probe k from the search start: steps 1 (probes 0..64), then
+// (63 + t) >> 6 for probe t (LZ4_skipTrigger = 6)
+__device__ __forceinline__ uint32_t probe_off(uint32_t k) {
+    if (k == 0) return 0;
+    const uint32_t m = 62 + k, q = m >> 6, r = m & 63;
+    return 1 + 32 * q * (q - 1) + (r + 1) * q;
+}
+
+__device__ __forceinline__ uint64_t ballot(bool b) { return __ballot(b); }
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// lanes below / above this one
+__device__ __forceinline__ uint64_t lanes_below(uint32_t lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
+
+// dst[0, len) = src[0, len), 64 lanes x 4 bytes per step on dword-aligned
+// destination words (head and tail byte-wise); src and dst do not overlap
+__device__ void wave_copy(uint8_t *dst, const uint8_t *src, uint32_t len, uint32_t lane) {
+    uint32_t head = (uint32_t)(-(uintptr_t)dst & 3);
+    if (head > len) head = len;
+    if (lane < head) st8(dst + lane, ld8(src + lane));
+    uint32_t i = head;
+    for (; i + 256 <= len; i += 256) {
+        const uint32_t o = i + 4 * lane;
+        *(__attribute__((address_space(1))) uint32_t *)(dst + o) = ld32u(src + o);
+    }
+    for (uint32_t j = i + lane; j < len; j += 64) st8(dst + j, ld8(src + j));
+}
+
+__device__ void wave_fill255(uint8_t *dst, uint32_t cnt, uint32_t lane) {
+    for (uint32_t j = lane; j < cnt; j += 64) st8(dst + j, 255u);
+}
+
+// literal or match length continuation: (v - 15) as 255-runs plus the rest
+__device__ __forceinline__ uint32_t put_len(uint8_t *dst, uint32_t op, uint32_t v, uint32_t lane) {
+    const uint32_t runs = v / 255;
+    wave_fill255(dst + op, runs, lane);
+    if (lane == 0) st8(dst + op + runs, v % 255);
+    return op + runs + 1;
+}
+
+}  // namespace
+
+// One wave per block.  ZDev.len = input bytes, ZDev.cap >= LZ4_compressBound
+// (checked on the host); ZOut.out_len = compressed bytes.
+__global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ blks, ZOut *__restrict__ outs) {
+    __shared__ uint32_t T[4096];
+    uint16_t *T16 = reinterpret_cast<uint16_t *>(T);
+    const uint32_t lane = threadIdx.x;
+    const ZDev b = blks[blockIdx.x];
+    const uint8_t *src = b.src;
+    uint8_t *dst = b.dst;
+    const uint32_t n = uni((uint32_t)b.len);
+    const bool small = n < kLimit64K;
+    for (uint32_t i = lane; i < 4096; i += 64) T[i] = 0;
+    __syncthreads();
+#define TGET(h) (small ? (uint32_t)T16[(h)] : T[(h)])
+#define TPUT(h, v)                            \
+    do {                                      \
+        if (small) T16[(h)] = (uint16_t)(v); \
+        else T[(h)] = (v);                   \
+    } while (0)
+
+    uint32_t op = 0, anchor = 0;
+    if (n >= kMfLimit + 1) {
+        const uint32_t mflimit1 = n - kMfLimit + 1, matchlimit = n - kLastLit;
+        if (lane == 0) TPUT(lz_hash(src, small), 0u);
+        uint32_t ip = 1;
+        for (;;) {
+            // ---- find a match: 64 probes per step ----
+            uint32_t match = 0;
+            bool found = false;
+            {
+                const uint32_t q0 = ip;
+                for (uint32_t k0 = 0;; k0 += 64) {
+                    const uint32_t k = k0 + lane;
+                    const uint32_t p = q0 + probe_off(k);
+                    const bool valid = q0 + probe_off(k + 1) <= mflimit1;  // else this probe ends the search
+                    const uint32_t pc = valid ? p : q0;
+                    const uint32_t h = lz_hash(src + pc, small);
+                    uint64_t eq = ~0ull;
+#pragma unroll
+                    for (int bit = 0; bit < 13; bit++) {
+                        const bool hb = (h >> bit) & 1u;
+                        const uint64_t bl = ballot(hb);
+                        eq &= hb ? bl : ~bl;
+                    }
+                    const uint64_t vmask = ballot(valid);  // a prefix of the lanes
+                    const uint64_t below = lanes_below(lane);
+                    const uint64_t prev = eq & below & vmask;
+                    uint32_t mi = TGET(h);
+                    const uint32_t pl = __shfl(p, prev ? 63 - __builtin_clzll(prev) : lane, 64);
+                    if (prev) mi = pl;
+                    const bool ok = valid && (small || mi + 65535u >= p) && ld32u(src + mi) == ld32u(src + pc);
+                    const uint64_t okm = ballot(ok);
+                    const uint64_t ex = okm ? ((okm & (0ull - okm)) << 1) - 1ull : vmask;  // probes that ran
+                    const bool writer = ((ex >> lane) & 1ull) && !(eq & ex & ~below & ~(1ull << lane));
+                    if (writer) TPUT(h, p);
+                    if (okm) {
+                        const int j = __builtin_ctzll(okm);
+                        ip = uni(__builtin_amdgcn_readlane(p, j));
+                        match = uni(__builtin_amdgcn_readlane(mi, j));
+                        found = true;
+                        break;
+                    }
+                    if (vmask != ~0ull) break;
+                }
+            }
+            if (!found) break;
+            // ---- catch up: extend the match backwards ----
+            {
+                const uint32_t lim = min(ip - anchor, match);
+                uint32_t back = 0;
+                for (;;) {
+                    const uint32_t t = back + lane;
+                    const bool same = t < lim && ld8(src + ip - 1 - t) == ld8(src + match - 1 - t);
+                    const uint64_t stop = ballot(!same);
+                    if (stop) {
+                        back += __builtin_ctzll(stop);
+                        break;
+                    }
+                    back += 64;
+                }
+                back = uni(back);
+                ip -= back;
+                match -= back;
+            }
+            // ---- literals ----
+            uint32_t tokpos = op, tok;
+            {
+                const uint32_t ll = ip - anchor;
+                op++;
+                if (ll >= 15) {
+                    tok = 15u << 4;
+                    op = put_len(dst, op, ll - 15, lane);
+                } else {
+                    tok = ll << 4;
+                }
+                wave_copy(dst + op, src + anchor, ll, lane);
+                op += ll;
+            }
+            // ---- match, then as long as the next position matches at once ----
+            for (;;) {
+                const uint32_t off = ip - match;
+                if (lane == 0) {
+                    st8(dst + op, off & 255u);
+                    st8(dst + op + 1, off >> 8);
+                }
+                op += 2;
+                // match length beyond MINMATCH: first difference, 4 bytes per lane
+                const uint32_t a = ip + kMinMatch, m2 = match + kMinMatch;
+                const uint32_t avail = matchlimit > a ? matchlimit - a : 0u;
+                uint32_t mc = 0;
+                for (;;) {
+                    if (mc >= avail) {
+                        mc = avail;
+                        break;
+                    }
+                    const uint32_t t = mc + 4 * lane;
+                    uint32_t stop = 0;
+                    if (t < avail) {
+                        const uint32_t x = ld32u(src + a + t) ^ ld32u(src + m2 + t);
+                        stop = min(x ? (uint32_t)__builtin_ctz(x) >> 3 : 4u, avail - t);
+                    }
+                    const uint64_t sm = ballot(stop < 4);
+                    if (sm) {
+                        const int L = __builtin_ctzll(sm);
+                        mc += 4 * L + __builtin_amdgcn_readlane(stop, L);
+                        break;
+                    }
+                    mc += 256;
+                }
+                mc = uni(mc);
+                ip += mc + kMinMatch;
+                if (mc >= 15) {
+                    tok += 15;
+                    op = put_len(dst, op, mc - 15, lane);
+                } else {
+                    tok += mc;
+                }
+                if (lane == 0) st8(dst + tokpos, tok);
+                anchor = ip;
+                if (ip >= mflimit1) break;
+                // fill the table at ip - 2, then test ip itself
+                if (lane == 0) TPUT(lz_hash(src + ip - 2, small), ip - 2);
+                const uint32_t h = uni(lz_hash(src + ip, small));
+                const uint32_t mi = uni(TGET(h));
+                if (lane == 0) TPUT(h, ip);
+                if ((small || mi + 65535u >= ip) && ld32u(src + mi) == ld32u(src + ip)) {
+                    tokpos = op++;
+                    tok = 0;
+                    match = mi;
+                    continue;
+                }
+                break;
+            }
+            if (anchor >= mflimit1) break;
+            ip++;
+        }
+    }
+    // ---- last literals ----
+    {
+        const uint32_t run = n - anchor;
+        const uint32_t tokpos = op++;
+        if (run >= 15) {
+            if (lane == 0) st8(dst + tokpos, 15u << 4);
+            op = put_len(dst, op, run - 15, lane);
+        } else if (lane == 0) {
+            st8(dst + tokpos, run << 4);
+        }
+        wave_copy(dst + op, src + anchor, run, lane);
+        op += run;
+    }
+#undef TGET
+#undef TPUT
+    if (lane == 0) {
+        outs[blockIdx.x].out_len = op;
+        outs[blockIdx.x].status = JFSX_OK;
+    }
+}
+
+namespace {
+
+// 256-byte window of the compressed input in the wave's VGPRs
+struct Win {
+    const uint8_t *src;
+    uint32_t n;
+    uint32_t w0;   // window start (multiple of 4, relative to src's dword-aligned base)
+    uint32_t w;    // this lane's dword
+    uintptr_t al;  // src rounded down to 4
+    uint32_t sh;   // src - al
+};
+
+__device__ __forceinline__ void win_load(Win &W, uint32_t pos, uint32_t lane) {
+    // dword d of the aligned image covers src bytes [4d - sh, 4d - sh + 4)
+    W.w0 = (pos + W.sh) & ~3u;
+    const uint32_t o = W.w0 + 4 * lane;  // aligned-image offset
+    const bool in = o < W.n + W.sh;        // the dword holds at least one input byte
+    W.w = in ? ld32a((const uint8_t *)(W.al + o)) : 0u;
+}
+
+__device__ __forceinline__ uint32_t win_byte(Win &W, uint32_t pos, uint32_t lane) {
+    const uint32_t x = pos + W.sh;
+    if (x - W.w0 >= 256u) win_load(W, pos, lane);
+    const uint32_t r = x - W.w0;
+    return (__builtin_amdgcn_readlane(W.w, r >> 2) >> (8 * (r & 3))) & 255u;
+}
+
+}  // namespace
+
+// One wave per block.  ZDev.len = compressed bytes, ZDev.cap = dst capacity;
+// ZOut.out_len = decoded bytes; status JFSX_EFORMAT for a malformed stream.
+__global__ __launch_bounds__(64) void lz4_decompress_k(const ZDev *__restrict__ blks, ZOut *__restrict__ outs) {
+    const uint32_t lane = threadIdx.x;
+    const ZDev b = blks[blockIdx.x];
+    const uint8_t *src = b.src;
+    uint8_t *dst = b.dst;
+    const uint32_t n = uni((uint32_t)b.len);
+    const int64_t cap = (int64_t)b.cap;
+    int64_t op = 0;
+    bool bad = false;
+    if (cap == 0) {
+        bad = !(n == 1 && ld8(src) == 0);
+    } else if (n == 0) {
+        bad = true;
+    } else {
+        Win W;
+        W.src = src;
+        W.n = n;
+        W.al = (uintptr_t)src & ~(uintptr_t)3;
+        W.sh = (uint32_t)((uintptr_t)src & 3);
+        win_load(W, 0, lane);
+        int64_t ip = 0, fenced = 0;  // dst bytes [0, fenced) are visible to this wave's loads
+        const int64_t ni = n;
+        for (;;) {
+            if (ip >= ni) { bad = true; break; }
+            const uint32_t token = win_byte(W, (uint32_t)ip++, lane);
+            int64_t len = token >> 4;
+            if (len == 15) {
+                uint32_t s;
+                do {
+                    if (ip >= ni - 15) { bad = true; break; }
+                    s = win_byte(W, (uint32_t)ip++, lane);
+                    len += s;
+                } while (s == 255);
+                if (bad) break;
+            }
+            if (cap - op < len || ni - ip < len) { bad = true; break; }
+            if (op + len > cap - (int64_t)kMfLimit || ip + len > ni - (2 + 1 + (int64_t)kLastLit)) {
+                // the last sequence: it must end the input exactly
+                if (ip + len != ni || op + len > cap) { bad = true; break; }
+                wave_copy(dst + op, src + ip, (uint32_t)len, lane);
+                op += len;
+                break;
+            }
+            wave_copy(dst + op, src + ip, (uint32_t)len, lane);
+            ip += len;
+            op += len;
+            const uint32_t off = win_byte(W, (uint32_t)ip, lane) | (win_byte(W, (uint32_t)ip + 1, lane) << 8);
+            ip += 2;
+            if ((int64_t)off > op) { bad = true; break; }
+            int64_t ml = token & 15;
+            if (ml == 15) {
+                uint32_t s;
+                do {
+                    if (ip > ni - (int64_t)kLastLit) { bad = true; break; }
+                    s = win_byte(W, (uint32_t)ip++, lane);
+                    ml += s;
+                } while (s == 255);
+                if (bad) break;
+            }
+            ml += kMinMatch;
+            if (cap - op < ml || op + ml > cap - (int64_t)kLastLit) { bad = true; break; }
+            uint8_t *o = dst + op;
+            if (off == 0) {
+                // an offset of 0 copies the bytes being written: LZ4 1.9 zero-fills them
+                for (uint32_t j = lane; j < (uint32_t)ml; j += 64) st8(o + j, 0u);
+            } else {
+                const int64_t need = op - off + (ml < (int64_t)off ? ml : (int64_t)off);  // source end
+                if (need > fenced) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    fenced = op;
+                }
+                const uint8_t *m = o - off;
+                if (ml <= (int64_t)off)
+                    wave_copy(o, m, (uint32_t)ml, lane);  // disjoint
+                else  // overlapping: the first off bytes repeat
+                    for (uint32_t j = lane; j < (uint32_t)ml; j += 64) st8(o + j, ld8(m + j % off));
+            }
+            op += ml;
+        }
+    }
+    if (lane == 0) {
+        outs[blockIdx.x].out_len = bad ? 0 : (uint64_t)op;
+        outs[blockIdx.x].status = bad ? JFSX_EFORMAT : JFSX_OK;
+    }
+}
+
+void launch_lz4_compress(hipStream_t s, int n, const ZDev *blks, ZOut *outs) {
+    if (n > 0) hipLaunchKernelGGL(lz4_compress_k, dim3(n), dim3(64), 0, s, blks, outs);
+}
+
+void launch_lz4_decompress(hipStream_t s, int n, const ZDev *blks, ZOut *outs) {
+    if (n > 0) hipLaunchKernelGGL(lz4_decompress_k, dim3(n), dim3(64), 0, s, blks, outs);
+}
+
+}  // namespace jfsx

@@ -21,6 +21,7 @@ CTX_BITSLICE = 1  # context flag: AES-GCM keystream from the bitsliced AES (VALU
 MEM_DEVICE, MEM_HOST = 0, 1
 OK, ETAG, ECRC = 0, 1, 2
 EOF = 3  # jfsx_cache_verify: short read
+EFORMAT = 4  # malformed LZ4 block (lz4.DecompressSafe error)
 EINVAL, ENODEV, EIO, ENOMEM, EMISFORMED, EAGAIN = -22, -19, -5, -12, -74, -11
 SEG = 32 << 10
 
@@ -37,7 +38,7 @@ EXPORTS = [
     "jfsx_agg_new", "jfsx_agg_free", "jfsx_agg_seal", "jfsx_agg_open", "jfsx_agg_crc32c", "jfsx_agg_stats",
     "jfsx_gen_synthetic_batch", "jfsx_mctx_open", "jfsx_mctx_close", "jfsx_mctx_ndev", "jfsx_mctx_ctx",
     "jfsx_mctx_seal_batch", "jfsx_mctx_open_batch", "jfsx_mctx_crc32c_segments", "jfsx_agg_new_mctx",
-    "jfsx_agg_dev_batches",
+    "jfsx_agg_dev_batches", "jfsx_lz4_bound", "jfsx_lz4_compress_batch", "jfsx_lz4_decompress_batch",
 ]
 
 
@@ -61,6 +62,14 @@ class jfsx_range(ctypes.Structure):
         ("data", ctypes.c_void_p), ("len", ctypes.c_uint64), ("crc", ctypes.c_void_p),
         ("status", ctypes.c_int32), ("bad_seg", ctypes.c_int32), ("got", ctypes.c_uint32),
         ("expect", ctypes.c_uint32),
+    ]
+
+
+class jfsx_zblk(ctypes.Structure):
+    _fields_ = [
+        ("src", ctypes.c_void_p), ("src_len", ctypes.c_uint64), ("dst", ctypes.c_void_p),
+        ("dst_cap", ctypes.c_uint64), ("out_len", ctypes.c_uint64), ("status", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
     ]
 
 
@@ -133,6 +142,9 @@ def load_library(path=LIB_PATH):
             "jfsx_mctx_crc32c_segments": (I, [P, I, ctypes.POINTER(jfsx_range), I, I]),
             "jfsx_agg_new_mctx": (I, [P, I, U64, U32, PP]),
             "jfsx_agg_dev_batches": (I, [P, I, ctypes.POINTER(U64)]),
+            "jfsx_lz4_bound": (U64, [U64]),
+            "jfsx_lz4_compress_batch": (I, [P, I, ctypes.POINTER(jfsx_zblk), I]),
+            "jfsx_lz4_decompress_batch": (I, [P, I, ctypes.POINTER(jfsx_zblk), I]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -175,6 +187,11 @@ def gen_key(seed, block):
     nonce = np.empty(12, np.uint8)
     load_library().jfsx_gen_key(seed, block, key.ctypes.data, nonce.ctypes.data)
     return key.tobytes(), nonce.tobytes()
+
+
+def lz4_bound(n):
+    """LZ4_compressBound (compress.go:111 CompressBound)."""
+    return load_library().jfsx_lz4_bound(n)
 
 
 def device_count():
@@ -312,6 +329,40 @@ class Engine:
 
     def crc32c_segments(self, ranges, n, mode=CRC_GEN, mem=MEM_DEVICE):
         self._check(self.L.jfsx_crc32c_segments(self.ctx, n, ranges, mode, mem), "jfsx_crc32c_segments")
+
+    # -- LZ4 stage (jfsx_lz4_*) -------------------------------------------
+    @staticmethod
+    def make_zblocks(specs):
+        """specs: iterable of (src_ptr, src_len, dst_ptr, dst_cap)."""
+        specs = list(specs)
+        arr = (jfsx_zblk * max(len(specs), 1))()
+        for i, (sp, sl, dp, dc) in enumerate(specs):
+            arr[i].src, arr[i].src_len, arr[i].dst, arr[i].dst_cap = sp, sl, dp, dc
+        return arr, len(specs)
+
+    def lz4_compress_batch(self, zblks, n, mem=MEM_DEVICE):
+        self._check(self.L.jfsx_lz4_compress_batch(self.ctx, n, zblks, mem), "jfsx_lz4_compress_batch")
+
+    def lz4_decompress_batch(self, zblks, n, mem=MEM_DEVICE):
+        self._check(self.L.jfsx_lz4_decompress_batch(self.ctx, n, zblks, mem), "jfsx_lz4_decompress_batch")
+
+    def lz4_compress(self, datas):
+        """Host buffers in, list of compressed bytes out (one GPU batch)."""
+        srcs = [_u8(d) for d in datas]
+        dsts = [np.empty(max(int(lz4_bound(s.size)), 1), np.uint8) for s in srcs]
+        arr, n = self.make_zblocks((s.ctypes.data, s.size, d.ctypes.data, int(lz4_bound(s.size)))
+                                   for s, d in zip(srcs, dsts))
+        self.lz4_compress_batch(arr, n, MEM_HOST)
+        return [d[:arr[i].out_len].tobytes() for i, d in enumerate(dsts)]
+
+    def lz4_decompress(self, datas, caps):
+        """Host buffers in; list of (status, bytes) out, decoded into dst of caps[i] bytes."""
+        srcs = [_u8(d) for d in datas]
+        dsts = [np.empty(max(int(c), 1), np.uint8) for c in caps]
+        arr, n = self.make_zblocks((s.ctypes.data, s.size, d.ctypes.data, int(c))
+                                   for s, d, c in zip(srcs, dsts, caps))
+        self.lz4_decompress_batch(arr, n, MEM_HOST)
+        return [(arr[i].status, d[:arr[i].out_len].tobytes()) for i, d in enumerate(dsts)]
 
     # -- asynchronous batches (jfsx_*_async + jfsx_wait) ------------------
     def _ticket(self, fn, what, *args):

@@ -60,6 +60,9 @@ def lib():
             "orc_data_encrypt": (I64, [I, P, P, P, I, P, U64, P]),
             "orc_data_decrypt": (I64, [I, P, P, I64, P]),
             "orc_bench_seal_crc": (ctypes.c_double, [I, I, U64, U64, U64, P]),
+            "orc_lz4_bound": (I, [I]),
+            "orc_lz4_compress": (I, [P, I, P, I]),
+            "orc_lz4_decompress": (I, [P, I, P, I]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -247,3 +250,26 @@ def bench_seal_crc_evp(algo, nthreads, nblocks, blen, seed):
     dg = ctypes.c_uint32()
     secs = lib().orc_bench_seal_crc_evp(algo, nthreads, nblocks, blen, seed, ctypes.byref(dg))
     return secs, dg.value
+
+
+# -- LZ4 block codec (oracle/jfs_lz4.c; compress.go:107-125) ------------------
+def lz4_bound(n):
+    return lib().orc_lz4_bound(n)
+
+
+def lz4_compress(data):
+    """LZ4_compress_default(data) as bytes."""
+    src = _np(data)
+    cap = lz4_bound(src.size)
+    dst = np.empty(max(cap, 1), np.uint8)
+    r = lib().orc_lz4_compress(src.ctypes.data, src.size, dst.ctypes.data, cap)
+    assert r > 0
+    return dst[:r].tobytes()
+
+
+def lz4_decompress(data, cap):
+    """LZ4_decompress_safe(data, cap): (rc, bytes); rc < 0 for a malformed block."""
+    src = _np(data)
+    dst = np.empty(max(cap, 1), np.uint8)
+    r = lib().orc_lz4_decompress(src.ctypes.data if src.size else None, src.size, dst.ctypes.data, cap)
+    return r, (dst[:r].tobytes() if r > 0 else b"")

@@ -104,3 +104,40 @@ def test_write_cache_file_layout(tmp_path):
     assert raw == d + orc.checksum(d)
     chunk.write_cache_file(p, d, chunk.CsNone)
     assert open(p, "rb").read() == d
+
+
+# ---- compress stage around the block store (cached_store.go:371-392, 673-745) ----
+def test_upload_load_blocks_lz4_through_encrypted_store():
+    from juicefs_amd import compress as C
+    from juicefs_amd import encrypt as EN
+    from tests import lz4_data
+    priv = EN.GenerateRsaKey(2048)
+    enc = EN.NewDataEncryptor(EN.NewRSAEncryptor(priv), EN.CHACHA20_RSA)
+    store = EN.NewEncrypted(EN.MemStorage(), enc)
+    lz = C.NewCompressor("lz4")
+    blocks = [lz4_data.sample(k, n, seed=i) for i, (k, n) in
+              enumerate([("text", 4 << 20), ("random", 1 << 20), ("zeros", 70000), ("runs", 12345), ("text", 5)])]
+    keys = ["chunks/0/0/%d_0_%d" % (i, len(b)) for i, b in enumerate(blocks)]
+    outs = C.upload_blocks(store, keys, blocks, lz)
+    from oracle import oracle as orc
+    assert outs == [orc.lz4_compress(b) for b in blocks]
+    assert len(outs[0]) < len(blocks[0]) // 2 and len(outs[2]) < 1000
+    assert C.load_blocks(store, keys, [len(b) for b in blocks], lz) == blocks
+    # a block whose object decodes short of its length: "read %s fully"
+    store.Put(keys[3], orc.lz4_compress(blocks[3][:-1]))
+    import pytest
+    with pytest.raises(C.CompressError, match="read chunks/0/0/3_0_12345 fully"):
+        C.load_blocks(store, keys[3:4], [len(blocks[3])], lz)
+
+
+def test_lz4_compressor_single_calls():
+    from juicefs_amd import compress as C
+    lz = C.NewCompressor("lz4")
+    src = b"abcabcabcabc" * 1000
+    dst = bytearray(lz.CompressBound(len(src)))
+    n = lz.Compress(dst, src)
+    page = bytearray(len(src))
+    assert lz.Decompress(page, bytes(dst[:n])) == len(src) and bytes(page) == src
+    import pytest
+    with pytest.raises(C.CompressError, match="lz4: malformed block"):
+        lz.Decompress(bytearray(len(src)), bytes(dst[:n - 3]))

@@ -85,3 +85,33 @@ def test_parse_pem_without_password_fixture():
     e1, e2 = enc.NewRSAEncryptor(k1), enc.NewRSAEncryptor(k2)
     secret = bytes(32)
     assert e2.Decrypt(e1.Encrypt(secret)) == secret
+
+
+# ---- pkg/compress/compress.go mirror (host logic; no GPU calls) ----------
+def test_new_compressor_names():
+    from juicefs_amd import compress as C
+    assert isinstance(C.NewCompressor("LZ4"), C.LZ4)
+    assert isinstance(C.NewCompressor("zstd"), C.ZStandard)
+    assert isinstance(C.NewCompressor(""), C.noOp) and isinstance(C.NewCompressor("none"), C.noOp)
+    assert C.NewCompressor("gzip") is None
+    assert [C.NewCompressor(a).Name() for a in ("lz4", "zstd", "none")] == ["LZ4", "Zstd", "Noop"]
+
+
+def test_compress_bounds_and_noop_errors():
+    import pytest
+    from juicefs_amd import compress as C
+    lz = C.NewCompressor("lz4")
+    for n in (0, 1, 254, 255, 4 << 20):
+        assert lz.CompressBound(n) == n + n // 255 + 16  # LZ4_COMPRESSBOUND
+    assert C.ZStandard().CompressBound(4 << 20) == (4 << 20) + (4 << 12)
+    assert C.ZStandard().CompressBound(1000) == 1000 + 3 + ((128 << 10) - 1000) // 2048
+    nop = C.noOp()
+    assert nop.CompressBound(77) == 77
+    buf = bytearray(3)
+    with pytest.raises(C.CompressError, match="buffer too short: 3 < 4"):
+        nop.Compress(buf, b"abcd")
+    assert nop.Decompress(bytearray(4), b"abcd") == 4
+    with pytest.raises(C.CompressError, match="decompress an empty input"):
+        lz.Decompress(bytearray(10), b"")
+    with pytest.raises(NotImplementedError):
+        C.ZStandard().Compress(bytearray(10), b"x")
