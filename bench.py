@@ -37,7 +37,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--blocks", type=int, default=16384, help="4 MiB blocks per GPU (16384 = 64 GiB)")
     ap.add_argument("--block-bytes", type=int, default=BLOCK)
-    ap.add_argument("--mode", choices=["seal", "open", "crc", "decrypt", "agg"], default="seal",
+    ap.add_argument("--mode", choices=["seal", "open", "crc", "decrypt", "agg", "lz4", "unlz4"], default="seal",
                     help="decrypt = dataEncryptor.Decrypt end to end: batched RSA-OAEP key unwrap + Open + CRC verify; "
                          "agg = one-block Seal calls from --threads threads on pinned host blocks, through the "
                          "aggregator (jfsx_agg) and, for comparison, as direct one-block batches")
@@ -61,6 +61,8 @@ def parse():
                     help="place blocks back to back (256-B aligned) instead of one per --block-bytes slot")
     ap.add_argument("--aes", choices=["ttable", "bitslice"], default="ttable",
                     help="AES-GCM keystream kernel: T-table AES in LDS, or bitsliced AES on the VALU")
+    ap.add_argument("--lz4-data", choices=["text", "random"], default="text",
+                    help="lz4/unlz4 modes (SURVEY 8f-4): word text (compressible) or SplitMix64 bytes")
     ap.add_argument("--dry-run", action="store_true",
                     help="test hook: the launcher, process group, shard layout, barrier and max-over-ranks timing "
                          "with no engine (no GPU); prints the JSON line with value null")
@@ -193,6 +195,8 @@ def main():
     eng = E.Engine(local, E.CTX_BITSLICE if args.aes == "bitslice" else 0)
     if args.mode == "agg":
         return agg_bench(args, world, rank, local, dist, eng)
+    if args.mode in ("lz4", "unlz4"):
+        return lz4_bench(args, world, rank, local, dist, eng)
     if args.mem == "host":
         return host_ingest(args, world, rank, local, dist, eng)
     nb, L = args.blocks, args.block_bytes
@@ -576,6 +580,138 @@ def agg_bench(args, world, rank, local, dist, eng):
             "roofline": None, "cpu_baseline": None, "verified_blocks": verified}), flush=True)
     for h in (hin, hout, hcrc):
         eng.free_pinned(h)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def _text_pool(nbytes, seed):
+    """Word text (zipf-distributed words of a 300-word vocabulary): the
+    compressible synthetic input of the lz4 modes."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    nw = 300
+    lens = rng.integers(1, 10, nw)
+    tab = np.full((nw, 11), 32, np.uint8)
+    for i in range(nw):
+        tab[i, :lens[i]] = rng.integers(97, 123, lens[i], dtype=np.uint8)
+    idx = rng.zipf(1.3, nbytes // 2 + 8) % nw
+    L = lens[idx] + 1
+    k = int(np.searchsorted(np.cumsum(L), nbytes)) + 1
+    idx, L = idx[:k], L[:k]
+    off = np.arange(int(L.sum())) - np.repeat(np.cumsum(L) - L, L)
+    return tab[np.repeat(idx, L), off][:nbytes]
+
+
+def lz4_cpu_baseline(blocks, L):
+    """LZ4_compress_default / LZ4_decompress_safe of the system LZ4 C library
+    (the library hungys/go-lz4 wraps) over a bounded sample, one thread per
+    core (ctypes releases the GIL)."""
+    import ctypes
+    from concurrent.futures import ThreadPoolExecutor
+    lib = ctypes.CDLL("liblz4.so.1")
+    threads, note = host_cores()
+    cap = lib.LZ4_compressBound(L)
+    outs = [ctypes.create_string_buffer(cap) for _ in range(threads)]
+    sizes = [0] * len(blocks)
+
+    def comp(i):
+        sizes[i] = lib.LZ4_compress_default(blocks[i], outs[i % threads], L, cap)
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(comp, range(min(threads, len(blocks)))))
+        t0 = time.perf_counter()
+        list(ex.map(comp, range(len(blocks))))
+        el = time.perf_counter() - t0
+    return {"value": round(len(blocks) * L / el / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": "%d x 4 MiB blocks, LZ4_compress_default of the system liblz4 %d (the LZ4 C library "
+                      "github.com/hungys/go-lz4 binds), %d threads (%s)" % (len(blocks), lib.LZ4_versionNumber(),
+                                                                          threads, note)}
+
+
+def lz4_bench(args, world, rank, local, dist, eng):
+    """SURVEY 8f-4 / cachedStore.upload's Compress (cached_store.go:387) and
+    load's Decompress (:738): a device-resident batch of 4 MiB blocks through
+    the LZ4 stage.  value = uncompressed GB/s."""
+    import numpy as np
+    from juicefs_amd import engine as E
+    nb = args.blocks if args.blocks != 16384 else 1024
+    L = args.block_bytes
+    base = rank * nb
+    bound = int(E.lz4_bound(L))
+    src = eng.alloc(nb * L)
+    cmp_ = eng.alloc(nb * bound)
+    if args.lz4_data == "text":
+        pool = _text_pool(16 << 20, SEED + rank)
+        for b in range(nb):
+            o = ((base + b) * 2654435761) % (pool.size - L)
+            src.upload(pool[o:o + L], b * L)
+    else:
+        eng.gen_synthetic_batch(src, L, [L] * nb, SEED, base)
+    carr, n = eng.make_zblocks((src.ptr + b * L, L, cmp_.ptr + b * bound, bound) for b in range(nb))
+    eng.lz4_compress_batch(carr, n, E.MEM_DEVICE)
+    clens = [carr[b].out_len for b in range(nb)]
+    if args.mode == "lz4":
+        def step():
+            eng.lz4_compress_batch(carr, n, E.MEM_DEVICE)
+        algo_bytes = nb * L + sum(clens)
+    else:
+        out = eng.alloc(nb * L)
+        darr, _ = eng.make_zblocks((cmp_.ptr + b * bound, clens[b], out.ptr + b * L, L) for b in range(nb))
+
+        def step():
+            eng.lz4_decompress_batch(darr, n, E.MEM_DEVICE)
+        algo_bytes = nb * L + sum(clens)
+    for _ in range(args.warmup):
+        step()
+    eng.sync()
+    eng.kernel_time(reset=True)
+    eng.set_timing(True)
+    barrier(dist)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    eng.sync()
+    barrier(dist)
+    el = max_over_ranks(dist, time.perf_counter() - t0, local)
+    eng.set_timing(False)
+    k_ms, k_n = eng.kernel_time(reset=True)
+    k_avg = k_ms / max(k_n, 1)
+    # spot check against the oracle (checker only)
+    verified = 0
+    if args.verify:
+        from oracle import oracle as orc
+        for b in range(0, nb, max(1, nb // args.verify))[:args.verify]:
+            p = src.download(L, b * L).tobytes()
+            c = cmp_.download(clens[b], b * bound).tobytes()
+            if c != orc.lz4_compress(p):
+                raise SystemExit("bench: block %d compresses differently from the oracle" % b)
+            if args.mode == "unlz4":
+                if darr[b].status != E.OK or out.download(L, b * L).tobytes() != p:
+                    raise SystemExit("bench: block %d does not decode" % b)
+            verified += 1
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu and args.mode == "lz4":
+        sample = [src.download(L, b * L).tobytes() for b in range(min(nb, 256))]
+        cpu = lz4_cpu_baseline(sample, L)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "LZ4 %s GB/s (uncompressed bytes), 4 MiB blocks" % (
+                "compressed" if args.mode == "lz4" else "decompressed"),
+            "value": round(world * nb * L * args.steps / el / 1e9, 2), "unit": "GB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (%s), device-resident" % (
+                "zipf word text, 4 MiB windows of a 16 MiB pool" if args.lz4_data == "text" else "SplitMix64 blocks"),
+            "config": {"workload": "%s GiB device-resident batch of 4 MiB blocks per GPU, LZ4 %s" % (
+                round(nb * L / 2**30, 3), "compress" if args.mode == "lz4" else "decompress"),
+                "blocks_per_gpu": nb, "block_bytes": L, "mode": args.mode, "data": args.lz4_data,
+                "ratio": round(sum(clens) / (nb * L), 4), "parallelism": "block-sharded x%d, no collective" % world},
+            "roofline": {"bound": "hbm", "achieved": round(algo_bytes / (k_avg / 1e3) / 1e9, 1) if k_n else None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(algo_bytes / (k_avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if k_n else None,
+                         "traffic": None, "kernel": "lz4_compress_k" if args.mode == "lz4" else "lz4_decompress_k",
+                         "kernel_avg_ms": round(k_avg, 3), "algorithmic_bytes_per_launch": algo_bytes},
+            "cpu_baseline": cpu, "verified_blocks": verified}), flush=True)
     eng.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -64,47 +64,29 @@ __device__ __forceinline__ P5 p_mul(const P5 &a, const P5 &b) {
 // and the top carry folds back into limb 0 times 5 (d4 has no wrapped
 // products: d4 < 2^54.4, 5 * (d4 >> 26) < 2^31).  Output limbs < 2^26 except
 // l[1] < 2^26 + 2^6.
-#if JFSX_CPMAD
-// d = a * b + c in one v_mad_u64_u32 whose 64-bit addend is c itself.  Written
-// out because LLVM reassociates a sum of products plus an addend into
-// "products from 0, then a v_lshl_add_u64 of the addend" (one extra 64-bit op
-// per limb); b is wave-uniform (an SGPR operand).
-__device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
-    uint64_t d, co;  // co: the unused carry-out SGPR pair
-    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(co) : "v"(a), "s"(b), "v"(c));
-    return d;
-}
-#define MADF(x, y, z) mad64((x), (y), (z))
-#else
-#define MADF(x, y, z) ((uint64_t)(x) * (y) + (z))
-#endif
-#if JFSX_CPMAD == 2
-#define MADC(x, y, z) mad64((x), (y), (z))
-#else
 #define MADC(x, y, z) ((uint64_t)(x) * (y) + (z))
-#endif
 
 __device__ __forceinline__ P5 p_mul_add(const P5 &a, const P5 &b, const uint32_t (&sb)[5], const P5 &m) {
     typedef uint64_t u64;
     P5 r;
     u64 d = MADC(a.l[4], sb[1], MADC(a.l[3], sb[2], MADC(a.l[2], sb[3], MADC(a.l[1], sb[4],
-            MADF(a.l[0], b.l[0], (u64)m.l[0])))));
+            MADC(a.l[0], b.l[0], (u64)m.l[0])))));
     r.l[0] = (uint32_t)d & M26;
     uint32_t c = (uint32_t)(d >> 26);
     d = MADC(a.l[4], sb[2], MADC(a.l[3], sb[3], MADC(a.l[2], sb[4], MADC(a.l[1], b.l[0],
-        MADF(a.l[0], b.l[1], (u64)(c + m.l[1]))))));
+        MADC(a.l[0], b.l[1], (u64)(c + m.l[1]))))));
     r.l[1] = (uint32_t)d & M26;
     c = (uint32_t)(d >> 26);
     d = MADC(a.l[4], sb[3], MADC(a.l[3], sb[4], MADC(a.l[2], b.l[0], MADC(a.l[1], b.l[1],
-        MADF(a.l[0], b.l[2], (u64)(c + m.l[2]))))));
+        MADC(a.l[0], b.l[2], (u64)(c + m.l[2]))))));
     r.l[2] = (uint32_t)d & M26;
     c = (uint32_t)(d >> 26);
     d = MADC(a.l[4], sb[4], MADC(a.l[3], b.l[0], MADC(a.l[2], b.l[1], MADC(a.l[1], b.l[2],
-        MADF(a.l[0], b.l[3], (u64)(c + m.l[3]))))));
+        MADC(a.l[0], b.l[3], (u64)(c + m.l[3]))))));
     r.l[3] = (uint32_t)d & M26;
     c = (uint32_t)(d >> 26);
     d = MADC(a.l[4], b.l[0], MADC(a.l[3], b.l[1], MADC(a.l[2], b.l[2], MADC(a.l[1], b.l[3],
-        MADF(a.l[0], b.l[4], (u64)(c + m.l[4]))))));
+        MADC(a.l[0], b.l[4], (u64)(c + m.l[4]))))));
     r.l[4] = (uint32_t)d & M26;
     c = (uint32_t)(d >> 26);
     const uint32_t t = r.l[0] + c * 5u;
@@ -178,21 +160,7 @@ __device__ __forceinline__ P5 p_wave_sum(P5 a) {
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
 
-#if JFSX_CPROT16
-// rotl16(d ^ a): the high word takes the low words' XOR and the low word the
-// high words' (two SDWA v_xor_b32, word selects on both sources)
-__device__ __forceinline__ uint32_t xor_rot16(uint32_t d, uint32_t a) {
-    uint32_t t;
-    asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_0\n\t"
-        "v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1"
-        : "=&v"(t)
-        : "v"(d), "v"(a));
-    return t;
-}
-#define XR16(d, a) xor_rot16((d), (a))
-#else
 #define XR16(d, a) rotl((d) ^ (a), 16)
-#endif
 
 #define CP_QR(a, b, c, d)          \
     a += b; d = XR16(d, a);        \

@@ -53,14 +53,6 @@ constexpr int kThreads = kWaves * 64;
 #ifndef JFSX_RKR
 #define JFSX_RKR 1
 #endif
-// Poly1305 limb sums with the addend in the first v_mad_u64_u32 (mad64, jfsx_chacha.hip).
-#ifndef JFSX_CPMAD
-#define JFSX_CPMAD 0
-#endif
-// ChaCha "d = rotl16(d ^ a)" as two SDWA word XORs instead of v_xor + v_alignbit.
-#ifndef JFSX_CPROT16
-#define JFSX_CPROT16 0
-#endif
 constexpr int kStreams = JFSX_STREAMS;        // independent segment streams per wave (ILP)
 constexpr int kSlotsPerTask = kWaves * kStreams;  // GHASH/Poly partial slots per task
 constexpr int kMaxTaskBytes = 4 << 20;
