@@ -634,7 +634,7 @@ def lz4_bench(args, world, rank, local, dist, eng):
     the LZ4 stage.  value = uncompressed GB/s."""
     import numpy as np
     from juicefs_amd import engine as E
-    nb = args.blocks if args.blocks != 16384 else 1024
+    nb = args.blocks
     L = args.block_bytes
     base = rank * nb
     bound = int(E.lz4_bound(L))

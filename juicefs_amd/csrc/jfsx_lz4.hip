@@ -105,6 +105,108 @@ __device__ __forceinline__ uint32_t put_len(uint8_t *dst, uint32_t op, uint32_t 
 
 }  // namespace
 
+namespace {
+
+// 256 bytes of the input in the wave's VGPRs: lane L holds the aligned dword
+// at A0 + 4L (zero past the block end).  Reads inside it cost a v_readlane
+// (uniform position) or a ds_bpermute (per-lane position), not a memory trip.
+struct IWin {
+    uintptr_t A0;
+    uint32_t w;
+};
+
+__device__ __forceinline__ void iwin_load(IWin &W, const uint8_t *p, const uint8_t *send, uint32_t lane) {
+    W.A0 = (uintptr_t)p & ~(uintptr_t)3;
+    const uintptr_t a = W.A0 + 4 * lane;
+    W.w = a < (uintptr_t)send ? ld32a((const uint8_t *)a) : 0u;
+}
+// [p, p + len) inside the window (uniform)
+__device__ __forceinline__ bool iwin_has(const IWin &W, const uint8_t *p, uint32_t len) {
+    return (uintptr_t)p >= W.A0 && (uintptr_t)p + len <= W.A0 + 256;
+}
+// 4 bytes at p and the byte at p + 4, uniform p inside the window
+__device__ __forceinline__ uint32_t iwin_u32(const IWin &W, const uint8_t *p, uint32_t &b4) {
+    const uint32_t r = (uint32_t)((uintptr_t)p - W.A0), i = r >> 2, sh = r & 3;
+    const uint32_t d0 = __builtin_amdgcn_readlane(W.w, i), d1 = __builtin_amdgcn_readlane(W.w, i + 1);
+    b4 = (d1 >> (8 * sh)) & 255u;
+    return __builtin_amdgcn_alignbyte(d1, d0, sh);
+}
+// the same for a per-lane p (ds_bpermute)
+__device__ __forceinline__ uint32_t iwin_u32_lane(const IWin &W, const uint8_t *p, uint32_t &b4) {
+    const uint32_t r = (uint32_t)((uintptr_t)p - W.A0), i = r >> 2, sh = r & 3;
+    const uint32_t d0 = __shfl(W.w, (int)i, 64), d1 = __shfl(W.w, (int)(i + 1), 64);
+    b4 = (d1 >> (8 * sh)) & 255u;
+    return __builtin_amdgcn_alignbyte(d1, d0, sh);
+}
+
+__device__ __forceinline__ uint32_t hash_of(uint32_t w, uint32_t b4, bool small) {
+    if (small) return (w * 2654435761u) >> (32 - 13);
+    const uint64_t v = (uint64_t)w | ((uint64_t)b4 << 32);
+    return (uint32_t)(((v << 24) * 889523592379ull) >> (64 - 12));
+}
+
+// dst[0, len) = [p, p + len) of the window (len <= 256)
+__device__ __forceinline__ void iwin_copy(uint8_t *dst, const IWin &W, const uint8_t *p, uint32_t len, uint32_t lane) {
+    const uint32_t r = (uint32_t)((uintptr_t)p - W.A0);
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t j = lane + 64 * k, q = r + j;
+        const uint32_t d = __shfl(W.w, (int)((q >> 2) & 63), 64);
+        if (j < len) st8(dst + j, (d >> (8 * (q & 3))) & 255u);
+    }
+}
+
+// Match length beyond MINMATCH at (ip, match): LZ4_count(ip + 4, match + 4,
+// matchlimit).  Loads the window C at ip + 4 (input side) and, in the same
+// round of loads, the catch-up bytes before ip / match (limc <= 64 of them;
+// back = equal bytes found, 64 when all were equal).  Returns mc.
+__device__ uint32_t count_and_back(IWin &C, const uint8_t *src, const uint8_t *send, uint32_t ip, uint32_t match,
+                                   uint32_t matchlimit, uint32_t limc, uint32_t &back, uint32_t lane) {
+    const uint8_t *aa = src + ip + kMinMatch;
+    const uint32_t off = ip - match;
+    iwin_load(C, aa, send, lane);
+    const uint8_t *mp = (const uint8_t *)(C.A0 + 4 * lane) - off;
+    const uint32_t mw = ld32u(mp + 4 <= send ? mp : send - 4);
+    bool ceq = false;
+    if (lane < limc) ceq = ld8(src + ip - 1 - lane) == ld8(src + match - 1 - lane);
+    const uint64_t cst = ballot(!ceq);
+    back = cst ? (uint32_t)__builtin_ctzll(cst) : 64u;
+    const uintptr_t lim = (uintptr_t)src + matchlimit, a0 = (uintptr_t)aa;
+    const uint32_t x = C.w ^ mw;
+    uint32_t si = 4;
+#pragma unroll
+    for (int i = 3; i >= 0; i--) {
+        const uintptr_t ad = C.A0 + 4 * lane + i;
+        if (ad >= a0 && (ad >= lim || ((x >> (8 * i)) & 255u))) si = (uint32_t)i;
+    }
+    const uint64_t sm = ballot(si < 4);
+    if (sm) {
+        const int L = __builtin_ctzll(sm);
+        return uni((uint32_t)(C.A0 + 4 * L + __builtin_amdgcn_readlane(si, L) - a0));
+    }
+    // a long match: continue 256 bytes per step from the window's end
+    const uint32_t avail = (uintptr_t)lim > a0 ? (uint32_t)(lim - a0) : 0u;
+    uint32_t mc = (uint32_t)(C.A0 + 256 - a0);
+    const uint8_t *m2 = src + match + kMinMatch;
+    for (;;) {
+        if (mc >= avail) return avail;
+        const uint32_t t = mc + 4 * lane;
+        uint32_t stop = 0;
+        if (t < avail) {
+            const uint32_t y = ld32u(aa + t) ^ ld32u(m2 + t);
+            stop = min(y ? (uint32_t)__builtin_ctz(y) >> 3 : 4u, avail - t);
+        }
+        const uint64_t s2 = ballot(stop < 4);
+        if (s2) {
+            const int L = __builtin_ctzll(s2);
+            return uni(mc + 4 * L + __builtin_amdgcn_readlane(stop, L));
+        }
+        mc += 256;
+    }
+}
+
+}  // namespace
+
 // One wave per block.  ZDev.len = input bytes, ZDev.cap >= LZ4_compressBound
 // (checked on the host); ZOut.out_len = compressed bytes.
 __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ blks, ZOut *__restrict__ outs) {
@@ -115,6 +217,7 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
     const uint8_t *src = b.src;
     uint8_t *dst = b.dst;
     const uint32_t n = uni((uint32_t)b.len);
+    const uint8_t *send = src + n;
     const bool small = n < kLimit64K;
     for (uint32_t i = lane; i < 4096; i += 64) T[i] = 0;
     __syncthreads();
@@ -130,35 +233,67 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
         const uint32_t mflimit1 = n - kMfLimit + 1, matchlimit = n - kLastLit;
         if (lane == 0) TPUT(lz_hash(src, small), 0u);
         uint32_t ip = 1;
+        IWin W;  // input window; a search starts with it holding [anchor, anchor + 253)
+        W.A0 = 1;  // empty
+        W.w = 0;
         for (;;) {
             // ---- find a match: 64 probes per step ----
             uint32_t match = 0;
             bool found = false;
             {
                 const uint32_t q0 = ip;
+                if (!iwin_has(W, src + anchor, q0 - anchor + 72)) iwin_load(W, src + anchor, send, lane);
                 for (uint32_t k0 = 0;; k0 += 64) {
                     const uint32_t k = k0 + lane;
                     const uint32_t p = q0 + probe_off(k);
                     const bool valid = q0 + probe_off(k + 1) <= mflimit1;  // else this probe ends the search
                     const uint32_t pc = valid ? p : q0;
-                    const uint32_t h = lz_hash(src + pc, small);
-                    uint64_t eq = ~0ull;
-#pragma unroll
-                    for (int bit = 0; bit < 13; bit++) {
-                        const bool hb = (h >> bit) & 1u;
-                        const uint64_t bl = ballot(hb);
-                        eq &= hb ? bl : ~bl;
+                    const uint32_t pf = q0 + probe_off(k0), pl = q0 + probe_off(k0 + 63);
+                    uint32_t cur, b4;
+                    if (iwin_has(W, src + pf, pl - pf + 8)) {
+                        cur = iwin_u32_lane(W, src + pc, b4);
+                    } else {
+                        cur = ld32u(src + pc);
+                        b4 = small ? 0u : ld8(src + pc + 4);
                     }
+                    const uint32_t h = hash_of(cur, b4, small);
                     const uint64_t vmask = ballot(valid);  // a prefix of the lanes
-                    const uint64_t below = lanes_below(lane);
-                    const uint64_t prev = eq & below & vmask;
-                    uint32_t mi = TGET(h);
-                    const uint32_t pl = __shfl(p, prev ? 63 - __builtin_clzll(prev) : lane, 64);
-                    if (prev) mi = pl;
-                    const bool ok = valid && (small || mi + 65535u >= p) && ld32u(src + mi) == ld32u(src + pc);
-                    const uint64_t okm = ballot(ok);
-                    const uint64_t ex = okm ? ((okm & (0ull - okm)) << 1) - 1ull : vmask;  // probes that ran
-                    const bool writer = ((ex >> lane) & 1ull) && !(eq & ex & ~below & ~(1ull << lane));
+                    // probes against the table as it stood before this step
+                    const uint32_t mi0 = TGET(h);
+                    const bool ok0 = valid && (small || mi0 + 65535u >= p) && ld32u(src + mi0) == cur;
+                    const uint64_t okm0 = ballot(ok0);
+                    uint32_t mi = mi0;
+                    uint64_t okm;
+                    bool writer;
+                    if (okm0 & 1ull) {
+                        // the first probe matches: it alone ran, nothing shares its bucket
+                        okm = 1ull;
+                        writer = lane == 0;
+                    } else {
+                        // lanes of the same bucket (13 ballots over the hash bits)
+                        uint64_t eq = ~0ull;
+#pragma unroll
+                        for (int bit = 0; bit < 13; bit++) {
+                            const bool hb = (h >> bit) & 1u;
+                            const uint64_t bl = ballot(hb);
+                            eq &= hb ? bl : ~bl;
+                        }
+                        const uint64_t below = lanes_below(lane);
+                        const uint64_t prev = eq & below & vmask;
+                        okm = okm0;
+                        if (ballot(prev != 0ull)) {
+                            // a probe after another of its bucket reads that probe's position
+                            const uint32_t plv = __shfl(p, prev ? 63 - __builtin_clzll(prev) : lane, 64);
+                            bool ok = ok0;
+                            if (prev) {
+                                mi = plv;
+                                ok = valid && (small || mi + 65535u >= p) && ld32u(src + mi) == cur;
+                            }
+                            okm = ballot(ok);
+                        }
+                        const uint64_t ex = okm ? ((okm & (0ull - okm)) << 1) - 1ull : vmask;  // probes that ran
+                        writer = ((ex >> lane) & 1ull) && !(eq & ex & ~below & ~(1ull << lane));
+                    }
                     if (writer) TPUT(h, p);
                     if (okm) {
                         const int j = __builtin_ctzll(okm);
@@ -171,10 +306,17 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
                 }
             }
             if (!found) break;
-            // ---- catch up: extend the match backwards ----
-            {
+            // ---- catch-up and match length in one round of loads ----
+            // (bytes [ip', ip + 4) are equal after the catch-up, so the length
+            // counted from ip + 4 plus the catch-up distance is LZ4_count from ip' + 4)
+            IWin C;
+            uint32_t back;
+            const uint32_t limc = min(min(ip - anchor, match), 64u);
+            uint32_t mc = count_and_back(C, src, send, ip, match, matchlimit, limc, back, lane);
+            back = uni(back);
+            if (back == 64 && limc == 64) {
+                // a longer backward run: continue 64 bytes per step
                 const uint32_t lim = min(ip - anchor, match);
-                uint32_t back = 0;
                 for (;;) {
                     const uint32_t t = back + lane;
                     const bool same = t < lim && ld8(src + ip - 1 - t) == ld8(src + match - 1 - t);
@@ -186,9 +328,10 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
                     back += 64;
                 }
                 back = uni(back);
-                ip -= back;
-                match -= back;
             }
+            ip -= back;
+            match -= back;
+            mc += back;
             // ---- literals ----
             uint32_t tokpos = op, tok;
             {
@@ -200,7 +343,10 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
                 } else {
                     tok = ll << 4;
                 }
-                wave_copy(dst + op, src + anchor, ll, lane);
+                if (iwin_has(W, src + anchor, ll))
+                    iwin_copy(dst + op, W, src + anchor, ll, lane);
+                else
+                    wave_copy(dst + op, src + anchor, ll, lane);
                 op += ll;
             }
             // ---- match, then as long as the next position matches at once ----
@@ -211,30 +357,6 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
                     st8(dst + op + 1, off >> 8);
                 }
                 op += 2;
-                // match length beyond MINMATCH: first difference, 4 bytes per lane
-                const uint32_t a = ip + kMinMatch, m2 = match + kMinMatch;
-                const uint32_t avail = matchlimit > a ? matchlimit - a : 0u;
-                uint32_t mc = 0;
-                for (;;) {
-                    if (mc >= avail) {
-                        mc = avail;
-                        break;
-                    }
-                    const uint32_t t = mc + 4 * lane;
-                    uint32_t stop = 0;
-                    if (t < avail) {
-                        const uint32_t x = ld32u(src + a + t) ^ ld32u(src + m2 + t);
-                        stop = min(x ? (uint32_t)__builtin_ctz(x) >> 3 : 4u, avail - t);
-                    }
-                    const uint64_t sm = ballot(stop < 4);
-                    if (sm) {
-                        const int L = __builtin_ctzll(sm);
-                        mc += 4 * L + __builtin_amdgcn_readlane(stop, L);
-                        break;
-                    }
-                    mc += 256;
-                }
-                mc = uni(mc);
                 ip += mc + kMinMatch;
                 if (mc >= 15) {
                     tok += 15;
@@ -245,21 +367,35 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
                 if (lane == 0) st8(dst + tokpos, tok);
                 anchor = ip;
                 if (ip >= mflimit1) break;
-                // fill the table at ip - 2, then test ip itself
-                if (lane == 0) TPUT(lz_hash(src + ip - 2, small), ip - 2);
-                const uint32_t h = uni(lz_hash(src + ip, small));
+                // fill the table at ip - 2, then test ip itself (bytes from the
+                // count window when it holds them)
+                uint32_t wm2, bm2, w0, b0;
+                if (iwin_has(C, src + ip - 2, 10)) {
+                    wm2 = iwin_u32(C, src + ip - 2, bm2);
+                    w0 = iwin_u32(C, src + ip, b0);
+                } else {
+                    wm2 = uni(ld32u(src + ip - 2));
+                    bm2 = uni(ld8(src + ip + 2));
+                    w0 = uni(ld32u(src + ip));
+                    b0 = uni(ld8(src + ip + 4));
+                }
+                if (lane == 0) TPUT(hash_of(wm2, bm2, small), ip - 2);
+                const uint32_t h = uni(hash_of(w0, b0, small));
                 const uint32_t mi = uni(TGET(h));
                 if (lane == 0) TPUT(h, ip);
-                if ((small || mi + 65535u >= ip) && ld32u(src + mi) == ld32u(src + ip)) {
+                if ((small || mi + 65535u >= ip) && uni(ld32u(src + mi)) == w0) {
                     tokpos = op++;
                     tok = 0;
                     match = mi;
+                    uint32_t nb;
+                    mc = count_and_back(C, src, send, ip, match, matchlimit, 0u, nb, lane);
                     continue;
                 }
                 break;
             }
             if (anchor >= mflimit1) break;
             ip++;
+            W = C;  // the next search starts inside the count window
         }
     }
     // ---- last literals ----
@@ -286,7 +422,7 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
 namespace {
 
 // 256-byte window of the compressed input in the wave's VGPRs
-struct Win {
+struct DWin {
     const uint8_t *src;
     uint32_t n;
     uint32_t w0;   // window start (multiple of 4, relative to src's dword-aligned base)
@@ -295,7 +431,7 @@ struct Win {
     uint32_t sh;   // src - al
 };
 
-__device__ __forceinline__ void win_load(Win &W, uint32_t pos, uint32_t lane) {
+__device__ __forceinline__ void win_load(DWin &W, uint32_t pos, uint32_t lane) {
     // dword d of the aligned image covers src bytes [4d - sh, 4d - sh + 4)
     W.w0 = (pos + W.sh) & ~3u;
     const uint32_t o = W.w0 + 4 * lane;  // aligned-image offset
@@ -303,7 +439,21 @@ __device__ __forceinline__ void win_load(Win &W, uint32_t pos, uint32_t lane) {
     W.w = in ? ld32a((const uint8_t *)(W.al + o)) : 0u;
 }
 
-__device__ __forceinline__ uint32_t win_byte(Win &W, uint32_t pos, uint32_t lane) {
+// dst[0, len) = input [pos, pos + len) when the window holds it (else false)
+__device__ __forceinline__ bool win_copy(uint8_t *dst, const DWin &W, uint32_t pos, uint32_t len, uint32_t lane) {
+    const uint32_t x = pos + W.sh;
+    if (x < W.w0 || x + len > W.w0 + 256u) return false;
+    const uint32_t r = x - W.w0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t j = lane + 64 * k, q = r + j;
+        const uint32_t d = __shfl(W.w, (int)((q >> 2) & 63), 64);
+        if (j < len) st8(dst + j, (d >> (8 * (q & 3))) & 255u);
+    }
+    return true;
+}
+
+__device__ __forceinline__ uint32_t win_byte(DWin &W, uint32_t pos, uint32_t lane) {
     const uint32_t x = pos + W.sh;
     if (x - W.w0 >= 256u) win_load(W, pos, lane);
     const uint32_t r = x - W.w0;
@@ -314,13 +464,21 @@ __device__ __forceinline__ uint32_t win_byte(Win &W, uint32_t pos, uint32_t lane
 
 // One wave per block.  ZDev.len = compressed bytes, ZDev.cap = dst capacity;
 // ZOut.out_len = decoded bytes; status JFSX_EFORMAT for a malformed stream.
+constexpr uint32_t kDRing = 16384;  // decoder's LDS copy of the most recent output bytes
+
+// One wave per block.  ZDev.len = compressed bytes, ZDev.cap = dst capacity;
+// ZOut.out_len = decoded bytes; status JFSX_EFORMAT for a malformed stream.
+// Every output byte is also written to a 16 KiB LDS ring, so a match whose
+// source lies within it never waits for the wave's own global stores.
 __global__ __launch_bounds__(64) void lz4_decompress_k(const ZDev *__restrict__ blks, ZOut *__restrict__ outs) {
+    __shared__ uint8_t ring[kDRing];
     const uint32_t lane = threadIdx.x;
     const ZDev b = blks[blockIdx.x];
     const uint8_t *src = b.src;
     uint8_t *dst = b.dst;
     const uint32_t n = uni((uint32_t)b.len);
     const int64_t cap = (int64_t)b.cap;
+    constexpr uint32_t RM = kDRing - 1;
     int64_t op = 0;
     bool bad = false;
     if (cap == 0) {
@@ -328,7 +486,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_k(const ZDev *__restrict__ 
     } else if (n == 0) {
         bad = true;
     } else {
-        Win W;
+        DWin W;
         W.src = src;
         W.n = n;
         W.al = (uintptr_t)src & ~(uintptr_t)3;
@@ -336,6 +494,27 @@ __global__ __launch_bounds__(64) void lz4_decompress_k(const ZDev *__restrict__ 
         win_load(W, 0, lane);
         int64_t ip = 0, fenced = 0;  // dst bytes [0, fenced) are visible to this wave's loads
         const int64_t ni = n;
+        // literal run [ip, ip + len) -> output at op, and its last kDRing bytes -> ring
+        auto literals = [&](int64_t len) {
+            const uint32_t x = (uint32_t)ip + W.sh;
+            if (x >= W.w0 && x + (uint32_t)len <= W.w0 + 256u) {
+                const uint32_t r = x - W.w0;
+#pragma unroll
+                for (uint32_t k = 0; k < 4; k++) {
+                    const uint32_t j = lane + 64 * k, q = r + j;
+                    const uint32_t d = __shfl(W.w, (int)((q >> 2) & 63), 64);
+                    const uint32_t v = (d >> (8 * (q & 3))) & 255u;
+                    if (j < (uint32_t)len) {
+                        st8(dst + op + j, v);
+                        ring[(uint32_t)(op + j) & RM] = (uint8_t)v;
+                    }
+                }
+            } else {
+                wave_copy(dst + op, src + ip, (uint32_t)len, lane);
+                for (int64_t j = (len > (int64_t)kDRing ? len - kDRing : 0) + lane; j < len; j += 64)
+                    ring[(uint32_t)(op + j) & RM] = (uint8_t)ld8(src + ip + j);
+            }
+        };
         for (;;) {
             if (ip >= ni) { bad = true; break; }
             const uint32_t token = win_byte(W, (uint32_t)ip++, lane);
@@ -353,11 +532,12 @@ __global__ __launch_bounds__(64) void lz4_decompress_k(const ZDev *__restrict__ 
             if (op + len > cap - (int64_t)kMfLimit || ip + len > ni - (2 + 1 + (int64_t)kLastLit)) {
                 // the last sequence: it must end the input exactly
                 if (ip + len != ni || op + len > cap) { bad = true; break; }
-                wave_copy(dst + op, src + ip, (uint32_t)len, lane);
+                if (!win_copy(dst + op, W, (uint32_t)ip, (uint32_t)len, lane))
+                    wave_copy(dst + op, src + ip, (uint32_t)len, lane);
                 op += len;
                 break;
             }
-            wave_copy(dst + op, src + ip, (uint32_t)len, lane);
+            literals(len);
             ip += len;
             op += len;
             const uint32_t off = win_byte(W, (uint32_t)ip, lane) | (win_byte(W, (uint32_t)ip + 1, lane) << 8);
@@ -376,9 +556,49 @@ __global__ __launch_bounds__(64) void lz4_decompress_k(const ZDev *__restrict__ 
             ml += kMinMatch;
             if (cap - op < ml || op + ml > cap - (int64_t)kLastLit) { bad = true; break; }
             uint8_t *o = dst + op;
+            const uint32_t uop = (uint32_t)op, uml = (uint32_t)ml;
             if (off == 0) {
                 // an offset of 0 copies the bytes being written: LZ4 1.9 zero-fills them
-                for (uint32_t j = lane; j < (uint32_t)ml; j += 64) st8(o + j, 0u);
+                for (uint32_t j = lane; j < uml; j += 64) {
+                    st8(o + j, 0u);
+                    ring[(uop + j) & RM] = 0;
+                }
+            } else if (uml <= off && off + uml <= kDRing) {
+                // disjoint source in the ring (no write of this match reaches a
+                // slot a later read of it needs): the common case, no modulo
+                for (uint32_t j = lane; j < uml; j += 64) {
+                    const uint32_t v = ring[(uop - off + j) & RM];
+                    st8(o + j, v);
+                    ring[(uop + j) & RM] = (uint8_t)v;
+                }
+            } else if (off <= 64 && uml <= (1u << 24)) {
+                // short period: the off source bytes, read once, repeat.  j % off
+                // by a float reciprocal (j < 2^24: the quotient is off by at most one)
+                const float rcp = 1.0f / (float)off;
+                auto mod = [&](uint32_t j) {
+                    uint32_t q = (uint32_t)((float)j * rcp);
+                    int32_t r = (int32_t)(j - q * off);
+                    r += r < 0 ? (int32_t)off : 0;
+                    r -= r >= (int32_t)off ? (int32_t)off : 0;
+                    return (uint32_t)r;
+                };
+                const uint32_t pat = ring[(uop - off + mod(lane)) & RM];
+                for (uint32_t j0 = 0; j0 < uml; j0 += 64) {
+                    // every lane joins the ds_bpermute (a disabled source lane reads 0)
+                    const uint32_t j = j0 + lane;
+                    const uint32_t v = __shfl(pat, (int)mod(j), 64);
+                    if (j < uml) {
+                        st8(o + j, v);
+                        ring[(uop + j) & RM] = (uint8_t)v;
+                    }
+                }
+            } else if (off + uml <= kDRing) {
+                // overlapping, period > 64: the first off bytes repeat
+                for (uint32_t j = lane; j < uml; j += 64) {
+                    const uint32_t v = ring[(uop - off + (j < off ? j : j % off)) & RM];
+                    st8(o + j, v);
+                    ring[(uop + j) & RM] = (uint8_t)v;
+                }
             } else {
                 const int64_t need = op - off + (ml < (int64_t)off ? ml : (int64_t)off);  // source end
                 if (need > fenced) {
@@ -388,9 +608,11 @@ __global__ __launch_bounds__(64) void lz4_decompress_k(const ZDev *__restrict__ 
                 }
                 const uint8_t *m = o - off;
                 if (ml <= (int64_t)off)
-                    wave_copy(o, m, (uint32_t)ml, lane);  // disjoint
+                    wave_copy(o, m, uml, lane);  // disjoint
                 else  // overlapping: the first off bytes repeat
-                    for (uint32_t j = lane; j < (uint32_t)ml; j += 64) st8(o + j, ld8(m + j % off));
+                    for (uint32_t j = lane; j < uml; j += 64) st8(o + j, ld8(m + j % off));
+                for (uint32_t j = (uml > kDRing ? uml - kDRing : 0) + lane; j < uml; j += 64)
+                    ring[(uop + j) & RM] = (uint8_t)ld8(m + (j < off ? j : j % off));
             }
             op += ml;
         }
