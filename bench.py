@@ -603,29 +603,37 @@ def _text_pool(nbytes, seed):
     return tab[np.repeat(idx, L), off][:nbytes]
 
 
-def lz4_cpu_baseline(blocks, L):
-    """LZ4_compress_default / LZ4_decompress_safe of the system LZ4 C library
-    (the library hungys/go-lz4 wraps) over a bounded sample, one thread per
-    core (ctypes releases the GIL)."""
+def lz4_cpu_baseline(blocks, L, decompress=False):
+    """LZ4_compress_default (or LZ4_decompress_safe) of the system LZ4 C
+    library (the library hungys/go-lz4 wraps) over a bounded sample, one thread
+    per core (ctypes releases the GIL)."""
     import ctypes
     from concurrent.futures import ThreadPoolExecutor
     lib = ctypes.CDLL("liblz4.so.1")
     threads, note = host_cores()
     cap = lib.LZ4_compressBound(L)
-    outs = [ctypes.create_string_buffer(cap) for _ in range(threads)]
-    sizes = [0] * len(blocks)
+    outs = [ctypes.create_string_buffer(max(cap, L)) for _ in range(threads)]
+    comp = []
+    if decompress:
+        for b in blocks:
+            c = ctypes.create_string_buffer(cap)
+            r = lib.LZ4_compress_default(b, c, L, cap)
+            comp.append((c, r))
 
-    def comp(i):
-        sizes[i] = lib.LZ4_compress_default(blocks[i], outs[i % threads], L, cap)
+    def work(i):
+        if decompress:
+            c, r = comp[i]
+            return lib.LZ4_decompress_safe(c, outs[i % threads], r, L)
+        return lib.LZ4_compress_default(blocks[i], outs[i % threads], L, cap)
     with ThreadPoolExecutor(threads) as ex:
-        list(ex.map(comp, range(min(threads, len(blocks)))))
+        list(ex.map(work, range(min(threads, len(blocks)))))
         t0 = time.perf_counter()
-        list(ex.map(comp, range(len(blocks))))
+        list(ex.map(work, range(len(blocks))))
         el = time.perf_counter() - t0
     return {"value": round(len(blocks) * L / el / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": "%d x 4 MiB blocks, LZ4_compress_default of the system liblz4 %d (the LZ4 C library "
-                      "github.com/hungys/go-lz4 binds), %d threads (%s)" % (len(blocks), lib.LZ4_versionNumber(),
-                                                                          threads, note)}
+            "sample": "%d x 4 MiB blocks, %s of the system liblz4 %d (the LZ4 C library github.com/hungys/go-lz4 "
+                      "binds), %d threads (%s)" % (len(blocks), "LZ4_decompress_safe" if decompress else
+                                                    "LZ4_compress_default", lib.LZ4_versionNumber(), threads, note)}
 
 
 def lz4_bench(args, world, rank, local, dist, eng):
@@ -690,9 +698,9 @@ def lz4_bench(args, world, rank, local, dist, eng):
                     raise SystemExit("bench: block %d does not decode" % b)
             verified += 1
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu and args.mode == "lz4":
+    if rank == 0 and world == 1 and not args.no_cpu:
         sample = [src.download(L, b * L).tobytes() for b in range(min(nb, 256))]
-        cpu = lz4_cpu_baseline(sample, L)
+        cpu = lz4_cpu_baseline(sample, L, decompress=args.mode == "unlz4")
     if rank == 0:
         print(json.dumps({
             "metric": "LZ4 %s GB/s (uncompressed bytes), 4 MiB blocks" % (
