@@ -310,6 +310,13 @@ typedef struct jfsx_zblk {
 uint64_t jfsx_lz4_bound(uint64_t n);
 int jfsx_lz4_compress_batch(jfsx_ctx *ctx, int n, jfsx_zblk *blks, int mem);
 int jfsx_lz4_decompress_batch(jfsx_ctx *ctx, int n, jfsx_zblk *blks, int mem);
+/* the same per block, through the aggregator (one synchronous call per
+ * goroutine, as cachedStore.upload / load call Compress / Decompress), and
+ * over a multi-device context (JFSX_MEM_HOST) */
+int jfsx_agg_lz4_compress(jfsx_agg *agg, jfsx_zblk *blk, int mem);
+int jfsx_agg_lz4_decompress(jfsx_agg *agg, jfsx_zblk *blk, int mem);
+int jfsx_mctx_lz4_compress_batch(jfsx_mctx *m, int n, jfsx_zblk *blks, int mem);
+int jfsx_mctx_lz4_decompress_batch(jfsx_mctx *m, int n, jfsx_zblk *blks, int mem);
 
 /* header helper: returns wrapped-key length and offset/size of the nonce so a
  * caller can unwrap the key first (encrypt.go:197-205) */

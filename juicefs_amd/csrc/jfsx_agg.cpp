@@ -168,12 +168,13 @@ int jfsx_wait(jfsx_ctx *c, jfsx_ticket t, int timeout_ms) {
 
 namespace jfsx {
 
-enum AggOp { kSeal = 0, kOpen = 1, kCrc = 2 };
+enum AggOp { kSeal = 0, kOpen = 1, kCrc = 2, kLz4c = 3, kLz4d = 4 };
 
 struct Req {
     int op, algo, mode, mem;
     jfsx_blk *blk;
     jfsx_range *range;
+    jfsx_zblk *z;
     uint64_t bytes;
     Clock::time_point t0;
     int rc = 0;
@@ -187,6 +188,8 @@ using jfsx::Req;
 using jfsx::kSeal;
 using jfsx::kOpen;
 using jfsx::kCrc;
+using jfsx::kLz4c;
+using jfsx::kLz4d;
 
 struct jfsx_agg {
     std::vector<jfsx_ctx *> cs;  // one dispatcher thread per context (device)
@@ -202,9 +205,11 @@ struct jfsx_agg {
     std::vector<std::thread> ths;
 
     int call(jfsx_ctx *c, const std::vector<Req *> &b, size_t i0, size_t n, std::vector<jfsx_blk> &blks,
-             std::vector<jfsx_range> &rng) {
+             std::vector<jfsx_range> &rng, std::vector<jfsx_zblk> &zs) {
         const Req &h = *b[i0];
         if (h.op == kCrc) return jfsx_crc32c_segments(c, (int)n, rng.data() + i0, h.mode, h.mem);
+        if (h.op == kLz4c) return jfsx_lz4_compress_batch(c, (int)n, zs.data() + i0, h.mem);
+        if (h.op == kLz4d) return jfsx_lz4_decompress_batch(c, (int)n, zs.data() + i0, h.mem);
         if (h.op == kSeal) return jfsx_seal_batch(c, h.algo, (int)n, blks.data() + i0, h.mode, h.mem);
         return jfsx_open_batch(c, h.algo, (int)n, blks.data() + i0, h.mode, h.mem);
     }
@@ -216,22 +221,29 @@ struct jfsx_agg {
         const size_t n = b.size();
         std::vector<jfsx_blk> blks;
         std::vector<jfsx_range> rng;
-        if (b[0]->op == kCrc) {
+        std::vector<jfsx_zblk> zs;
+        const int op = b[0]->op;
+        if (op == kCrc) {
             rng.resize(n);
             for (size_t i = 0; i < n; i++) rng[i] = *b[i]->range;
+        } else if (op == kLz4c || op == kLz4d) {
+            zs.resize(n);
+            for (size_t i = 0; i < n; i++) zs[i] = *b[i]->z;
         } else {
             blks.resize(n);
             for (size_t i = 0; i < n; i++) blks[i] = *b[i]->blk;
         }
-        int rc = call(c, b, 0, n, blks, rng);
+        int rc = call(c, b, 0, n, blks, rng, zs);
         if (rc == JFSX_EINVAL && n > 1) {
-            for (size_t i = 0; i < n; i++) b[i]->rc = call(c, b, i, 1, blks, rng);
+            for (size_t i = 0; i < n; i++) b[i]->rc = call(c, b, i, 1, blks, rng, zs);
         } else {
             for (size_t i = 0; i < n; i++) b[i]->rc = rc;
         }
         for (size_t i = 0; i < n; i++) {
-            if (b[i]->op == kCrc)
+            if (op == kCrc)
                 *b[i]->range = rng[i];
+            else if (op == kLz4c || op == kLz4d)
+                *b[i]->z = zs[i];
             else
                 *b[i]->blk = blks[i];
         }
@@ -336,19 +348,31 @@ int jfsx_agg_dev_batches(jfsx_agg *a, int i, uint64_t *batches) {
 
 int jfsx_agg_seal(jfsx_agg *a, int algo, jfsx_blk *blk, int crc_mode, int mem) {
     if (!a || !blk || !valid_algo(algo) || !valid_mem(mem)) return JFSX_EINVAL;
-    Req r{kSeal, algo, crc_mode, mem, blk, nullptr, blk->len};
+    Req r{kSeal, algo, crc_mode, mem, blk, nullptr, nullptr, blk->len};
     return a->submit(r);
 }
 
 int jfsx_agg_open(jfsx_agg *a, int algo, jfsx_blk *blk, int crc_mode, int mem) {
     if (!a || !blk || !valid_algo(algo) || !valid_mem(mem)) return JFSX_EINVAL;
-    Req r{kOpen, algo, crc_mode, mem, blk, nullptr, blk->len};
+    Req r{kOpen, algo, crc_mode, mem, blk, nullptr, nullptr, blk->len};
     return a->submit(r);
 }
 
 int jfsx_agg_crc32c(jfsx_agg *a, jfsx_range *range, int mode, int mem) {
     if (!a || !range || !valid_mem(mem) || (mode != JFSX_CRC_GEN && mode != JFSX_CRC_VERIFY)) return JFSX_EINVAL;
-    Req r{kCrc, 0, mode, mem, nullptr, range, range->len};
+    Req r{kCrc, 0, mode, mem, nullptr, range, nullptr, range->len};
+    return a->submit(r);
+}
+
+int jfsx_agg_lz4_compress(jfsx_agg *a, jfsx_zblk *z, int mem) {
+    if (!a || !z || !valid_mem(mem)) return JFSX_EINVAL;
+    Req r{kLz4c, 0, 0, mem, nullptr, nullptr, z, z->src_len};
+    return a->submit(r);
+}
+
+int jfsx_agg_lz4_decompress(jfsx_agg *a, jfsx_zblk *z, int mem) {
+    if (!a || !z || !valid_mem(mem)) return JFSX_EINVAL;
+    Req r{kLz4d, 0, 0, mem, nullptr, nullptr, z, z->dst_cap};
     return a->submit(r);
 }
 
@@ -473,6 +497,22 @@ int jfsx_mctx_crc32c_segments(jfsx_mctx *m, int n, jfsx_range *ranges, int mode,
     return fan_out(cut, [&](int k, int b0, int b1) {
         return jfsx_crc32c_segments(m->cs[k], b1 - b0, ranges + b0, mode, mem);
     });
+}
+
+static int mctx_lz4(jfsx_mctx *m, bool comp, int n, jfsx_zblk *z, int mem) {
+    if (!m || n < 0 || (n && !z)) return JFSX_EINVAL;
+    if (mem != JFSX_MEM_HOST && !(mem == JFSX_MEM_DEVICE && m->cs.size() == 1)) return JFSX_EINVAL;
+    if (n == 0) return 0;
+    const std::vector<int> cut = split_runs(n, (int)m->cs.size(), [&](int i) { return z[i].src_len; });
+    return fan_out(cut, [&](int k, int b0, int b1) {
+        return comp ? jfsx_lz4_compress_batch(m->cs[k], b1 - b0, z + b0, mem)
+                    : jfsx_lz4_decompress_batch(m->cs[k], b1 - b0, z + b0, mem);
+    });
+}
+
+int jfsx_mctx_lz4_compress_batch(jfsx_mctx *m, int n, jfsx_zblk *blks, int mem) { return mctx_lz4(m, true, n, blks, mem); }
+int jfsx_mctx_lz4_decompress_batch(jfsx_mctx *m, int n, jfsx_zblk *blks, int mem) {
+    return mctx_lz4(m, false, n, blks, mem);
 }
 
 int jfsx_agg_new_mctx(jfsx_mctx *m, int max_blocks, uint64_t max_bytes, uint32_t window_us, jfsx_agg **out) {

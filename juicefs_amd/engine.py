@@ -39,6 +39,7 @@ EXPORTS = [
     "jfsx_gen_synthetic_batch", "jfsx_mctx_open", "jfsx_mctx_close", "jfsx_mctx_ndev", "jfsx_mctx_ctx",
     "jfsx_mctx_seal_batch", "jfsx_mctx_open_batch", "jfsx_mctx_crc32c_segments", "jfsx_agg_new_mctx",
     "jfsx_agg_dev_batches", "jfsx_lz4_bound", "jfsx_lz4_compress_batch", "jfsx_lz4_decompress_batch",
+    "jfsx_agg_lz4_compress", "jfsx_agg_lz4_decompress", "jfsx_mctx_lz4_compress_batch", "jfsx_mctx_lz4_decompress_batch",
 ]
 
 
@@ -145,6 +146,10 @@ def load_library(path=LIB_PATH):
             "jfsx_lz4_bound": (U64, [U64]),
             "jfsx_lz4_compress_batch": (I, [P, I, ctypes.POINTER(jfsx_zblk), I]),
             "jfsx_lz4_decompress_batch": (I, [P, I, ctypes.POINTER(jfsx_zblk), I]),
+            "jfsx_agg_lz4_compress": (I, [P, ctypes.POINTER(jfsx_zblk), I]),
+            "jfsx_agg_lz4_decompress": (I, [P, ctypes.POINTER(jfsx_zblk), I]),
+            "jfsx_mctx_lz4_compress_batch": (I, [P, I, ctypes.POINTER(jfsx_zblk), I]),
+            "jfsx_mctx_lz4_decompress_batch": (I, [P, I, ctypes.POINTER(jfsx_zblk), I]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -589,6 +594,12 @@ class MultiEngine:
     def crc32c_segments(self, ranges, n, mode=CRC_GEN, mem=MEM_HOST):
         self._check(self.L.jfsx_mctx_crc32c_segments(self.m, n, ranges, mode, mem), "jfsx_mctx_crc32c_segments")
 
+    def lz4_compress_batch(self, zblks, n, mem=MEM_HOST):
+        self._check(self.L.jfsx_mctx_lz4_compress_batch(self.m, n, zblks, mem), "jfsx_mctx_lz4_compress_batch")
+
+    def lz4_decompress_batch(self, zblks, n, mem=MEM_HOST):
+        self._check(self.L.jfsx_mctx_lz4_decompress_batch(self.m, n, zblks, mem), "jfsx_mctx_lz4_decompress_batch")
+
 
 class Aggregator:
     """jfsx_agg: per-block calls from many threads coalesced into batches
@@ -641,6 +652,13 @@ class Aggregator:
 
     def crc32c(self, rng, mode=CRC_VERIFY, mem=MEM_HOST):
         self.eng._check(self.L.jfsx_agg_crc32c(self.h, ctypes.byref(rng), mode, mem), "jfsx_agg_crc32c")
+
+    def lz4_compress(self, z, mem=MEM_HOST):
+        """z: a jfsx_zblk (out_len/status are written into it)."""
+        self.eng._check(self.L.jfsx_agg_lz4_compress(self.h, ctypes.byref(z), mem), "jfsx_agg_lz4_compress")
+
+    def lz4_decompress(self, z, mem=MEM_HOST):
+        self.eng._check(self.L.jfsx_agg_lz4_decompress(self.h, ctypes.byref(z), mem), "jfsx_agg_lz4_decompress")
 
     def stats(self):
         """(calls, batches, blocks carried by those batches)"""

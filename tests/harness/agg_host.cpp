@@ -15,7 +15,7 @@
 namespace {
 std::mutex h_mu;
 std::vector<int> h_sizes;   // blocks per batch, in issue order
-std::vector<int> h_ops;     // 0 seal, 1 open, 2 crc
+std::vector<int> h_ops;     // 0 seal, 1 open, 2 crc, 3 lz4 compress, 4 lz4 decompress
 std::vector<int> h_modes;
 std::vector<intptr_t> h_ctxs;  // context of each batch
 std::vector<uint64_t> h_first;  // len of the first block of each batch
@@ -68,6 +68,28 @@ int jfsx_open_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *b, int crc_mode, int
 int jfsx_crc32c_segments(jfsx_ctx *c, int n, jfsx_range *r, int mode, int mem) {
     stub(c, 2, n, mode, n ? r[0].len : 0);
     for (int i = 0; i < n; i++) r[i].status = r[i].len % 7 == 3 ? JFSX_ECRC : JFSX_OK;
+    return 0;
+}
+
+// fake LZ4: out_len = src_len / 2 + 1 (compress), dst_cap (decompress);
+// src_len == 7 -> JFSX_EFORMAT; dst_cap == 1 -> EINVAL (the batch is retried alone)
+int jfsx_lz4_compress_batch(jfsx_ctx *c, int n, jfsx_zblk *z, int mem) {
+    for (int i = 0; i < n; i++)
+        if (z[i].dst_cap == 1) return JFSX_EINVAL;
+    stub(c, 3, n, 0, n ? z[0].src_len : 0);
+    for (int i = 0; i < n; i++) {
+        z[i].out_len = z[i].src_len / 2 + 1;
+        z[i].status = JFSX_OK;
+    }
+    return 0;
+}
+
+int jfsx_lz4_decompress_batch(jfsx_ctx *c, int n, jfsx_zblk *z, int mem) {
+    stub(c, 4, n, 0, n ? z[0].src_len : 0);
+    for (int i = 0; i < n; i++) {
+        z[i].status = z[i].src_len == 7 ? JFSX_EFORMAT : JFSX_OK;
+        z[i].out_len = z[i].status ? 0 : z[i].dst_cap;
+    }
     return 0;
 }
 

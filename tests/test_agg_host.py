@@ -52,6 +52,9 @@ def H(tmp_path_factory):
         ("jfsx_mctx_crc32c_segments", I, [P, I, ctypes.POINTER(E.jfsx_range), I, I]),
         ("jfsx_agg_new_mctx", I, [P, I, U64, U32, ctypes.POINTER(P)]),
         ("jfsx_agg_dev_batches", I, [P, I, ctypes.POINTER(U64)]),
+        ("jfsx_agg_lz4_compress", I, [P, ctypes.POINTER(E.jfsx_zblk), I]),
+        ("jfsx_agg_lz4_decompress", I, [P, ctypes.POINTER(E.jfsx_zblk), I]),
+        ("jfsx_mctx_lz4_compress_batch", I, [P, I, ctypes.POINTER(E.jfsx_zblk), I]),
     ]:
         f = getattr(L, name)
         f.restype, f.argtypes = res, args
@@ -375,3 +378,59 @@ def test_agg_over_devices_spreads_batches(H):
     assert {d for d, _ in batch_devs(H)} == {0, 1, 2, 3}
     H.jfsx_agg_free(h)
     H.jfsx_mctx_close(m)
+
+
+def test_lz4_calls_from_many_threads_batch_and_isolate_errors(H):
+    """Per-block Compress / Decompress calls (cachedStore.upload / load,
+    cached_store.go:387, :738) from many goroutines come out as few lz4
+    batches, never mixed with AEAD or the other direction; a request the
+    engine rejects (EINVAL) fails alone, a malformed block only flags itself."""
+    H.harness_reset(3000)
+    agg = ctypes.c_void_p()
+    assert H.jfsx_agg_new(FAKE_CTX, 0, 0, 2000, ctypes.byref(agg)) == 0
+    T = 48
+    zs = [E.jfsx_zblk() for _ in range(T)]
+    rcs = [None] * T
+    for i, z in enumerate(zs):
+        z.src_len = 1000 + i if i != 13 else 7
+        z.dst_cap = 5000 if i not in (28, 29) else 1  # 28: a compress the engine rejects
+
+    def worker(i):
+        f = H.jfsx_agg_lz4_compress if i % 2 == 0 else H.jfsx_agg_lz4_decompress
+        rcs[i] = f(agg, ctypes.byref(zs[i]), E.MEM_HOST)
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(T)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for i, z in enumerate(zs):
+        if i % 2 == 0:
+            assert rcs[i] == (E.EINVAL if i == 28 else 0)
+            if i != 28:
+                assert z.out_len == z.src_len // 2 + 1 and z.status == E.OK
+        else:
+            assert rcs[i] == 0, i  # a decompress with dst_cap 1 is no argument error
+            assert z.status == (E.EFORMAT if i == 13 else E.OK)
+    sizes, ops, modes = (ctypes.c_int * 256)(), (ctypes.c_int * 256)(), (ctypes.c_int * 256)()
+    nb = H.harness_batches(sizes, ops, modes, 256)
+    assert set(ops[:nb]) == {3, 4}
+    # coalesced (the rejected request's batch is re-run one request at a time)
+    assert nb < T * 2 // 3
+    assert H.jfsx_agg_free(agg) == 0
+
+
+def test_mctx_lz4_split_over_devices(H):
+    H.harness_reset(0)
+    H.harness_set_ndev(4)
+    m = ctypes.c_void_p()
+    assert H.jfsx_mctx_open(0, 0, ctypes.byref(m)) == 0
+    n = 10
+    zs = (E.jfsx_zblk * n)()
+    for i in range(n):
+        zs[i].src_len, zs[i].dst_cap = 4096 * (i + 1), 9000 * (i + 1)
+    assert H.jfsx_mctx_lz4_compress_batch(m, n, zs, E.MEM_HOST) == 0
+    assert all(zs[i].out_len == zs[i].src_len // 2 + 1 for i in range(n))
+    dev, first = (ctypes.c_int * 16)(), (ctypes.c_uint64 * 16)()
+    nb = H.harness_batch_devs(dev, first, 16)
+    assert sorted(dev[:nb]) == [0, 1, 2, 3]
+    assert H.jfsx_mctx_close(m) == 0

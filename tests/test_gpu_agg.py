@@ -222,3 +222,41 @@ def test_multi_device_context_host_batch(algo):
             assert sum(agg.dev_batches()) >= 1
     finally:
         m.close()
+
+
+def test_lz4_per_block_calls_through_the_aggregator():
+    """cachedStore.upload / load call Compress / Decompress once per block
+    from many goroutines: through jfsx_agg they become batches, each caller
+    gets its own bytes (bit-exact to the oracle)."""
+    import threading
+    from tests import lz4_data
+    eng = E.Engine(0)
+    try:
+        T = 24
+        srcs = [np.frombuffer(lz4_data.sample(lz4_data.KINDS[i % 6], 50000 + 997 * i, seed=i), np.uint8)
+                for i in range(T)]
+        outs = [np.zeros(int(E.lz4_bound(s.size)), np.uint8) for s in srcs]
+        backs = [np.zeros(s.size, np.uint8) for s in srcs]
+        zc = [E.jfsx_zblk() for _ in range(T)]
+        zd = [E.jfsx_zblk() for _ in range(T)]
+        with E.Aggregator(eng, window_us=3000) as agg:
+            def worker(i):
+                z = zc[i]
+                z.src, z.src_len, z.dst, z.dst_cap = srcs[i].ctypes.data, srcs[i].size, outs[i].ctypes.data, outs[i].size
+                agg.lz4_compress(z)
+                d = zd[i]
+                d.src, d.src_len, d.dst, d.dst_cap = outs[i].ctypes.data, z.out_len, backs[i].ctypes.data, backs[i].size
+                agg.lz4_decompress(d)
+            th = [threading.Thread(target=worker, args=(i,)) for i in range(T)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            calls, batches, blocks = agg.stats()
+        for i in range(T):
+            assert zc[i].status == E.OK and zd[i].status == E.OK
+            assert outs[i][:zc[i].out_len].tobytes() == orc.lz4_compress(srcs[i])
+            assert zd[i].out_len == srcs[i].size and backs[i].tobytes() == srcs[i].tobytes()
+        assert calls == 2 * T and batches < calls
+    finally:
+        eng.close()
