@@ -10,6 +10,8 @@
  *   §4 checksum()            -> jfsx_checksum
  *      cacheFile.ReadAt      -> jfsx_checksum of rb, compared with the stored
  *                               CRCs; and jfsx_cache_verify for the level logic
+ *   §5 LZ4.Compress/Decompress (cachedStore.upload / load) -> jfsx_agg_lz4_*
+ *                               from many threads, zblk descriptors in C memory
  *
  * Built in-tree by tests/harness/Makefile (from __graft_entry__.build());
  * run by tests/test_shim_sequence.py on the GPU box.  Exit 0 = all equal. */
@@ -20,6 +22,7 @@
 
 #include "../../include/jfsx.h"
 #include "../../oracle/jfs_oracle.c"
+#include "../../oracle/jfs_lz4.c"
 
 #define CHECK(c)                                                               \
     do {                                                                       \
@@ -192,6 +195,65 @@ static void cache_checksums(jfsx_ctx *ctx) {
     }
 }
 
+/* §5: one Compress then one Decompress per block and thread, as the upload
+ * and load goroutines make them; text-like and incompressible blocks */
+typedef struct {
+    jfsx_agg *agg;
+    uint8_t *src, *cmp, *back;
+    uint64_t n, cap;
+    int bad;
+} lz4_arg;
+
+static void *lz4_worker(void *vp) {
+    lz4_arg *a = (lz4_arg *)vp;
+    jfsx_zblk *z = (jfsx_zblk *)calloc(1, sizeof(jfsx_zblk));
+    z->src = a->src, z->src_len = a->n, z->dst = a->cmp, z->dst_cap = a->cap;
+    if (jfsx_agg_lz4_compress(a->agg, z, JFSX_MEM_HOST) || z->status) a->bad = 1;
+    const uint64_t cl = z->out_len;
+    z->src = a->cmp, z->src_len = cl, z->dst = a->back, z->dst_cap = a->n;
+    if (jfsx_agg_lz4_decompress(a->agg, z, JFSX_MEM_HOST) || z->status || z->out_len != a->n) a->bad = 1;
+    a->cap = cl;  /* compressed length, for the oracle check */
+    free(z);
+    return NULL;
+}
+
+static void lz4_stage(jfsx_ctx *ctx) {
+    enum { T = 12 };
+    jfsx_agg *agg = NULL;
+    CHECK(jfsx_agg_new(ctx, 0, 0, 1000, &agg) == 0);
+    lz4_arg a[T];
+    pthread_t th[T];
+    for (int t = 0; t < T; t++) {
+        const uint64_t n = 20000 + 77777 * (uint64_t)t;
+        memset(&a[t], 0, sizeof(a[t]));
+        a[t].agg = agg, a[t].n = n, a[t].cap = jfsx_lz4_bound(n);
+        a[t].src = (uint8_t *)malloc(n), a[t].cmp = (uint8_t *)malloc(a[t].cap), a[t].back = (uint8_t *)malloc(n);
+        if (t % 3 == 2) {
+            orc_gen_block(SEED, 500 + t, a[t].src, n);
+        } else {
+            /* words of a small vocabulary from an LCG */
+            uint32_t x = 12345u + t;
+            for (uint64_t i = 0; i < n; i++) {
+                x = x * 1103515245u + 12345u;
+                a[t].src[i] = (x >> 16) % 11 == 0 ? ' ' : (uint8_t)('a' + ((x >> 20) % (t % 3 ? 6 : 26)));
+            }
+        }
+        CHECK(pthread_create(&th[t], NULL, lz4_worker, &a[t]) == 0);
+    }
+    for (int t = 0; t < T; t++) {
+        CHECK(pthread_join(th[t], NULL) == 0);
+        CHECK(a[t].bad == 0);
+        uint8_t *ref = (uint8_t *)malloc(orc_lz4_bound((int)a[t].n));
+        const int rl = orc_lz4_compress(a[t].src, (int)a[t].n, ref, orc_lz4_bound((int)a[t].n));
+        CHECK((uint64_t)rl == a[t].cap && memcmp(ref, a[t].cmp, (size_t)rl) == 0);
+        CHECK(memcmp(a[t].back, a[t].src, a[t].n) == 0);
+        free(ref), free(a[t].src), free(a[t].cmp), free(a[t].back);
+    }
+    uint64_t calls, batches, blocks;
+    CHECK(jfsx_agg_stats(agg, &calls, &batches, &blocks) == 0 && calls == 2 * T && batches < calls);
+    CHECK(jfsx_agg_free(agg) == 0);
+}
+
 int main(void) {
     CHECK(jfsx_abi_version() == JFSX_ABI_VERSION);
     int nd = 0;
@@ -206,6 +268,7 @@ int main(void) {
         aggregated(ctx, m, algo);
     }
     cache_checksums(ctx);
+    lz4_stage(ctx);
     CHECK(jfsx_mctx_close(m) == 0);
     CHECK(jfsx_ctx_close(ctx) == 0);
     printf("shim sequence ok (%d device%s)\n", nd, nd == 1 ? "" : "s");
