@@ -719,7 +719,7 @@ int run_lz4(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, bool comp) {
     if (n < 0 || (mem != JFSX_MEM_DEVICE && mem != JFSX_MEM_HOST)) return JFSX_EINVAL;
     for (int i = 0; i < n; i++) {
         if ((z[i].src_len && !z[i].src) || (z[i].dst_cap && !z[i].dst) || z[i].src_len > kLz4MaxInput ||
-            z[i].dst_cap > ((uint64_t)1 << 32))
+            z[i].dst_cap >= ((uint64_t)1 << 32))
             return JFSX_EINVAL;
         if (comp && z[i].dst_cap < lz4_bound(z[i].src_len)) return JFSX_EINVAL;
     }

@@ -107,33 +107,41 @@ __device__ __forceinline__ uint32_t put_len(uint8_t *dst, uint32_t op, uint32_t 
 
 namespace {
 
-// 256 bytes of the input in the wave's VGPRs: lane L holds the aligned dword
-// at A0 + 4L (zero past the block end).  Reads inside it cost a v_readlane
+// The block as an aligned image: input byte pos sits at image offset pos + sh
+// of al = src rounded down to 4 (all offsets 32-bit scalars).
+struct Img {
+    const uint8_t *al;
+    uint32_t sh, n;
+};
+
+// 256 bytes of the input in the wave's VGPRs: lane L holds the image dword at
+// w0 + 4L (zero past the block end).  Reads inside it cost a v_readlane
 // (uniform position) or a ds_bpermute (per-lane position), not a memory trip.
 struct IWin {
-    uintptr_t A0;
+    uint32_t w0;
     uint32_t w;
 };
 
-__device__ __forceinline__ void iwin_load(IWin &W, const uint8_t *p, const uint8_t *send, uint32_t lane) {
-    W.A0 = (uintptr_t)p & ~(uintptr_t)3;
-    const uintptr_t a = W.A0 + 4 * lane;
-    W.w = a < (uintptr_t)send ? ld32a((const uint8_t *)a) : 0u;
+__device__ __forceinline__ void iwin_load(IWin &W, const Img &I, uint32_t pos, uint32_t lane) {
+    W.w0 = (pos + I.sh) & ~3u;
+    const uint32_t o = W.w0 + 4 * lane;
+    W.w = o < I.n + I.sh ? ld32a(I.al + o) : 0u;
 }
-// [p, p + len) inside the window (uniform)
-__device__ __forceinline__ bool iwin_has(const IWin &W, const uint8_t *p, uint32_t len) {
-    return (uintptr_t)p >= W.A0 && (uintptr_t)p + len <= W.A0 + 256;
+// [pos, pos + len) inside the window (uniform)
+__device__ __forceinline__ bool iwin_has(const IWin &W, const Img &I, uint32_t pos, uint32_t len) {
+    const uint32_t x = pos + I.sh;
+    return x >= W.w0 && x + len <= W.w0 + 256u;
 }
-// 4 bytes at p and the byte at p + 4, uniform p inside the window
-__device__ __forceinline__ uint32_t iwin_u32(const IWin &W, const uint8_t *p, uint32_t &b4) {
-    const uint32_t r = (uint32_t)((uintptr_t)p - W.A0), i = r >> 2, sh = r & 3;
+// 4 bytes at pos and the byte at pos + 4, uniform pos inside the window
+__device__ __forceinline__ uint32_t iwin_u32(const IWin &W, const Img &I, uint32_t pos, uint32_t &b4) {
+    const uint32_t r = pos + I.sh - W.w0, i = r >> 2, sh = r & 3;
     const uint32_t d0 = __builtin_amdgcn_readlane(W.w, i), d1 = __builtin_amdgcn_readlane(W.w, i + 1);
     b4 = (d1 >> (8 * sh)) & 255u;
     return __builtin_amdgcn_alignbyte(d1, d0, sh);
 }
-// the same for a per-lane p (ds_bpermute)
-__device__ __forceinline__ uint32_t iwin_u32_lane(const IWin &W, const uint8_t *p, uint32_t &b4) {
-    const uint32_t r = (uint32_t)((uintptr_t)p - W.A0), i = r >> 2, sh = r & 3;
+// the same for a per-lane pos (ds_bpermute)
+__device__ __forceinline__ uint32_t iwin_u32_lane(const IWin &W, const Img &I, uint32_t pos, uint32_t &b4) {
+    const uint32_t r = pos + I.sh - W.w0, i = r >> 2, sh = r & 3;
     const uint32_t d0 = __shfl(W.w, (int)i, 64), d1 = __shfl(W.w, (int)(i + 1), 64);
     b4 = (d1 >> (8 * sh)) & 255u;
     return __builtin_amdgcn_alignbyte(d1, d0, sh);
@@ -145,9 +153,10 @@ __device__ __forceinline__ uint32_t hash_of(uint32_t w, uint32_t b4, bool small)
     return (uint32_t)(((v << 24) * 889523592379ull) >> (64 - 12));
 }
 
-// dst[0, len) = [p, p + len) of the window (len <= 256)
-__device__ __forceinline__ void iwin_copy(uint8_t *dst, const IWin &W, const uint8_t *p, uint32_t len, uint32_t lane) {
-    const uint32_t r = (uint32_t)((uintptr_t)p - W.A0);
+// dst[0, len) = input [pos, pos + len) from the window (len <= 256)
+__device__ __forceinline__ void iwin_copy(uint8_t *dst, const IWin &W, const Img &I, uint32_t pos, uint32_t len,
+                                          uint32_t lane) {
+    const uint32_t r = pos + I.sh - W.w0;
 #pragma unroll
     for (uint32_t k = 0; k < 4; k++) {
         const uint32_t j = lane + 64 * k, q = r + j;
@@ -160,40 +169,39 @@ __device__ __forceinline__ void iwin_copy(uint8_t *dst, const IWin &W, const uin
 // matchlimit).  Loads the window C at ip + 4 (input side) and, in the same
 // round of loads, the catch-up bytes before ip / match (limc <= 64 of them;
 // back = equal bytes found, 64 when all were equal).  Returns mc.
-__device__ uint32_t count_and_back(IWin &C, const uint8_t *src, const uint8_t *send, uint32_t ip, uint32_t match,
+__device__ uint32_t count_and_back(IWin &C, const Img &I, const uint8_t *src, uint32_t ip, uint32_t match,
                                    uint32_t matchlimit, uint32_t limc, uint32_t &back, uint32_t lane) {
-    const uint8_t *aa = src + ip + kMinMatch;
-    const uint32_t off = ip - match;
-    iwin_load(C, aa, send, lane);
-    const uint8_t *mp = (const uint8_t *)(C.A0 + 4 * lane) - off;
-    const uint32_t mw = ld32u(mp + 4 <= send ? mp : send - 4);
+    const uint32_t aa = ip + kMinMatch, off = ip - match;
+    iwin_load(C, I, aa, lane);
+    const uint32_t lp = C.w0 + 4 * lane - I.sh;  // input position of this lane's first window byte (may wrap below 0 on lane 0)
+    const uint32_t mp = lp - off;
+    const uint32_t mw = ld32u(src + (mp + 4 <= I.n ? mp : I.n - 4));
     bool ceq = false;
     if (lane < limc) ceq = ld8(src + ip - 1 - lane) == ld8(src + match - 1 - lane);
     const uint64_t cst = ballot(!ceq);
     back = cst ? (uint32_t)__builtin_ctzll(cst) : 64u;
-    const uintptr_t lim = (uintptr_t)src + matchlimit, a0 = (uintptr_t)aa;
     const uint32_t x = C.w ^ mw;
     uint32_t si = 4;
 #pragma unroll
     for (int i = 3; i >= 0; i--) {
-        const uintptr_t ad = C.A0 + 4 * lane + i;
-        if (ad >= a0 && (ad >= lim || ((x >> (8 * i)) & 255u))) si = (uint32_t)i;
+        const int32_t ad = (int32_t)(lp + i);  // input position (signed: lane 0 may start before byte 0)
+        if (ad >= (int32_t)aa && ((uint32_t)ad >= matchlimit || ((x >> (8 * i)) & 255u))) si = (uint32_t)i;
     }
     const uint64_t sm = ballot(si < 4);
     if (sm) {
         const int L = __builtin_ctzll(sm);
-        return uni((uint32_t)(C.A0 + 4 * L + __builtin_amdgcn_readlane(si, L) - a0));
+        return uni(C.w0 + 4 * L - I.sh + __builtin_amdgcn_readlane(si, L) - aa);
     }
     // a long match: continue 256 bytes per step from the window's end
-    const uint32_t avail = (uintptr_t)lim > a0 ? (uint32_t)(lim - a0) : 0u;
-    uint32_t mc = (uint32_t)(C.A0 + 256 - a0);
-    const uint8_t *m2 = src + match + kMinMatch;
+    const uint32_t avail = matchlimit > aa ? matchlimit - aa : 0u;
+    uint32_t mc = C.w0 + 256 - I.sh - aa;
+    const uint8_t *a2 = src + aa, *m2 = src + match + kMinMatch;
     for (;;) {
         if (mc >= avail) return avail;
         const uint32_t t = mc + 4 * lane;
         uint32_t stop = 0;
         if (t < avail) {
-            const uint32_t y = ld32u(aa + t) ^ ld32u(m2 + t);
+            const uint32_t y = ld32u(a2 + t) ^ ld32u(m2 + t);
             stop = min(y ? (uint32_t)__builtin_ctz(y) >> 3 : 4u, avail - t);
         }
         const uint64_t s2 = ballot(stop < 4);
@@ -217,7 +225,7 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
     const uint8_t *src = b.src;
     uint8_t *dst = b.dst;
     const uint32_t n = uni((uint32_t)b.len);
-    const uint8_t *send = src + n;
+    const Img I{(const uint8_t *)((uintptr_t)src & ~(uintptr_t)3), (uint32_t)((uintptr_t)src & 3), n};
     const bool small = n < kLimit64K;
     for (uint32_t i = lane; i < 4096; i += 64) T[i] = 0;
     __syncthreads();
@@ -234,7 +242,7 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
         if (lane == 0) TPUT(lz_hash(src, small), 0u);
         uint32_t ip = 1;
         IWin W;  // input window; a search starts with it holding [anchor, anchor + 253)
-        W.A0 = 1;  // empty
+        W.w0 = 0xfffff000u;  // empty
         W.w = 0;
         for (;;) {
             // ---- find a match: 64 probes per step ----
@@ -242,7 +250,7 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
             bool found = false;
             {
                 const uint32_t q0 = ip;
-                if (!iwin_has(W, src + anchor, q0 - anchor + 72)) iwin_load(W, src + anchor, send, lane);
+                if (!iwin_has(W, I, anchor, q0 - anchor + 72)) iwin_load(W, I, anchor, lane);
                 for (uint32_t k0 = 0;; k0 += 64) {
                     const uint32_t k = k0 + lane;
                     const uint32_t p = q0 + probe_off(k);
@@ -250,8 +258,8 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
                     const uint32_t pc = valid ? p : q0;
                     const uint32_t pf = q0 + probe_off(k0), pl = q0 + probe_off(k0 + 63);
                     uint32_t cur, b4;
-                    if (iwin_has(W, src + pf, pl - pf + 8)) {
-                        cur = iwin_u32_lane(W, src + pc, b4);
+                    if (iwin_has(W, I, pf, pl - pf + 8)) {
+                        cur = iwin_u32_lane(W, I, pc, b4);
                     } else {
                         cur = ld32u(src + pc);
                         b4 = small ? 0u : ld8(src + pc + 4);
@@ -312,7 +320,7 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
             IWin C;
             uint32_t back;
             const uint32_t limc = min(min(ip - anchor, match), 64u);
-            uint32_t mc = count_and_back(C, src, send, ip, match, matchlimit, limc, back, lane);
+            uint32_t mc = count_and_back(C, I, src, ip, match, matchlimit, limc, back, lane);
             back = uni(back);
             if (back == 64 && limc == 64) {
                 // a longer backward run: continue 64 bytes per step
@@ -343,8 +351,8 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
                 } else {
                     tok = ll << 4;
                 }
-                if (iwin_has(W, src + anchor, ll))
-                    iwin_copy(dst + op, W, src + anchor, ll, lane);
+                if (iwin_has(W, I, anchor, ll))
+                    iwin_copy(dst + op, W, I, anchor, ll, lane);
                 else
                     wave_copy(dst + op, src + anchor, ll, lane);
                 op += ll;
@@ -370,9 +378,9 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
                 // fill the table at ip - 2, then test ip itself (bytes from the
                 // count window when it holds them)
                 uint32_t wm2, bm2, w0, b0;
-                if (iwin_has(C, src + ip - 2, 10)) {
-                    wm2 = iwin_u32(C, src + ip - 2, bm2);
-                    w0 = iwin_u32(C, src + ip, b0);
+                if (iwin_has(C, I, ip - 2, 10)) {
+                    wm2 = iwin_u32(C, I, ip - 2, bm2);
+                    w0 = iwin_u32(C, I, ip, b0);
                 } else {
                     wm2 = uni(ld32u(src + ip - 2));
                     bm2 = uni(ld8(src + ip + 2));
@@ -388,7 +396,7 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
                     tok = 0;
                     match = mi;
                     uint32_t nb;
-                    mc = count_and_back(C, src, send, ip, match, matchlimit, 0u, nb, lane);
+                    mc = count_and_back(C, I, src, ip, match, matchlimit, 0u, nb, lane);
                     continue;
                 }
                 break;
@@ -462,14 +470,15 @@ __device__ __forceinline__ uint32_t win_byte(DWin &W, uint32_t pos, uint32_t lan
 
 }  // namespace
 
-// One wave per block.  ZDev.len = compressed bytes, ZDev.cap = dst capacity;
-// ZOut.out_len = decoded bytes; status JFSX_EFORMAT for a malformed stream.
 constexpr uint32_t kDRing = 16384;  // decoder's LDS copy of the most recent output bytes
 
-// One wave per block.  ZDev.len = compressed bytes, ZDev.cap = dst capacity;
-// ZOut.out_len = decoded bytes; status JFSX_EFORMAT for a malformed stream.
-// Every output byte is also written to a 16 KiB LDS ring, so a match whose
-// source lies within it never waits for the wave's own global stores.
+// One wave per block.  ZDev.len = compressed bytes, ZDev.cap = dst capacity
+// (< 2^32, checked on the host); ZOut.out_len = decoded bytes; status
+// JFSX_EFORMAT for a malformed stream.  The control flow is wave-uniform
+// 32-bit scalar code: a sequence's token, offset and the first length byte
+// come from one 4-byte read of the register window.  Every output byte is
+// also written to a 16 KiB LDS ring, so a match whose source lies within it
+// never waits for the wave's own global stores.
 __global__ __launch_bounds__(64) void lz4_decompress_k(const ZDev *__restrict__ blks, ZOut *__restrict__ outs) {
     __shared__ uint8_t ring[kDRing];
     const uint32_t lane = threadIdx.x;
@@ -477,9 +486,9 @@ __global__ __launch_bounds__(64) void lz4_decompress_k(const ZDev *__restrict__ 
     const uint8_t *src = b.src;
     uint8_t *dst = b.dst;
     const uint32_t n = uni((uint32_t)b.len);
-    const int64_t cap = (int64_t)b.cap;
+    const uint32_t cap = uni((uint32_t)b.cap);
     constexpr uint32_t RM = kDRing - 1;
-    int64_t op = 0;
+    uint32_t op = 0;
     bool bad = false;
     if (cap == 0) {
         bad = !(n == 1 && ld8(src) == 0);
@@ -492,127 +501,143 @@ __global__ __launch_bounds__(64) void lz4_decompress_k(const ZDev *__restrict__ 
         W.al = (uintptr_t)src & ~(uintptr_t)3;
         W.sh = (uint32_t)((uintptr_t)src & 3);
         win_load(W, 0, lane);
-        int64_t ip = 0, fenced = 0;  // dst bytes [0, fenced) are visible to this wave's loads
-        const int64_t ni = n;
-        // literal run [ip, ip + len) -> output at op, and its last kDRing bytes -> ring
-        auto literals = [&](int64_t len) {
-            const uint32_t x = (uint32_t)ip + W.sh;
-            if (x >= W.w0 && x + (uint32_t)len <= W.w0 + 256u) {
-                const uint32_t r = x - W.w0;
-#pragma unroll
-                for (uint32_t k = 0; k < 4; k++) {
-                    const uint32_t j = lane + 64 * k, q = r + j;
-                    const uint32_t d = __shfl(W.w, (int)((q >> 2) & 63), 64);
-                    const uint32_t v = (d >> (8 * (q & 3))) & 255u;
-                    if (j < (uint32_t)len) {
-                        st8(dst + op + j, v);
-                        ring[(uint32_t)(op + j) & RM] = (uint8_t)v;
-                    }
-                }
-            } else {
-                wave_copy(dst + op, src + ip, (uint32_t)len, lane);
-                for (int64_t j = (len > (int64_t)kDRing ? len - kDRing : 0) + lane; j < len; j += 64)
-                    ring[(uint32_t)(op + j) & RM] = (uint8_t)ld8(src + ip + j);
-            }
-        };
+        uint32_t ip = 0, fenced = 0;  // dst bytes [0, fenced) are visible to this wave's loads
         for (;;) {
-            if (ip >= ni) { bad = true; break; }
-            const uint32_t token = win_byte(W, (uint32_t)ip++, lane);
-            int64_t len = token >> 4;
+            if (ip >= n) { bad = true; break; }
+            // token .. token + 3 in one read (the window then holds ip .. ip + 7)
+            uint32_t x = ip + W.sh;
+            if (x < W.w0 || x + 8u > W.w0 + 256u) {
+                win_load(W, ip, lane);
+                x = ip + W.sh;
+            }
+            const uint32_t r = x - W.w0;
+            const uint32_t D = __builtin_amdgcn_alignbyte(__builtin_amdgcn_readlane(W.w, (r >> 2) + 1),
+                                                          __builtin_amdgcn_readlane(W.w, r >> 2), r & 3);
+            const uint32_t token = D & 255u;
+            ip++;
+            uint32_t len = token >> 4;
             if (len == 15) {
                 uint32_t s;
                 do {
-                    if (ip >= ni - 15) { bad = true; break; }
-                    s = win_byte(W, (uint32_t)ip++, lane);
+                    if (ip + 15 >= n) { bad = true; break; }
+                    s = win_byte(W, ip++, lane);
                     len += s;
                 } while (s == 255);
                 if (bad) break;
             }
-            if (cap - op < len || ni - ip < len) { bad = true; break; }
-            if (op + len > cap - (int64_t)kMfLimit || ip + len > ni - (2 + 1 + (int64_t)kLastLit)) {
+            if (len > cap - op || len > n - ip) { bad = true; break; }
+            if ((uint64_t)op + len + kMfLimit > cap || (uint64_t)ip + len + (2 + 1 + kLastLit) > n) {
                 // the last sequence: it must end the input exactly
-                if (ip + len != ni || op + len > cap) { bad = true; break; }
-                if (!win_copy(dst + op, W, (uint32_t)ip, (uint32_t)len, lane))
-                    wave_copy(dst + op, src + ip, (uint32_t)len, lane);
+                if (ip + len != n) { bad = true; break; }
+                if (!win_copy(dst + op, W, ip, len, lane)) wave_copy(dst + op, src + ip, len, lane);
                 op += len;
                 break;
             }
-            literals(len);
-            ip += len;
-            op += len;
-            const uint32_t off = win_byte(W, (uint32_t)ip, lane) | (win_byte(W, (uint32_t)ip + 1, lane) << 8);
+            uint32_t off;
+            if (len == 0) {
+                off = (D >> 8) & 0xffffu;  // the offset follows the token
+            } else {
+                // literals -> output and ring (the ring needs only their last kDRing bytes)
+                const uint32_t xl = ip + W.sh;
+                if (xl >= W.w0 && xl + len <= W.w0 + 256u) {
+                    const uint32_t rl = xl - W.w0;
+#pragma unroll
+                    for (uint32_t k = 0; k < 4; k++) {
+                        const uint32_t j = lane + 64 * k, q = rl + j;
+                        const uint32_t d = __shfl(W.w, (int)((q >> 2) & 63), 64);
+                        const uint32_t v = (d >> (8 * (q & 3))) & 255u;
+                        if (j < len) {
+                            st8(dst + op + j, v);
+                            ring[(op + j) & RM] = (uint8_t)v;
+                        }
+                    }
+                } else {
+                    wave_copy(dst + op, src + ip, len, lane);
+                    for (uint32_t j = (len > kDRing ? len - kDRing : 0) + lane; j < len; j += 64)
+                        ring[(op + j) & RM] = (uint8_t)ld8(src + ip + j);
+                }
+                ip += len;
+                op += len;
+                off = win_byte(W, ip, lane) | (win_byte(W, ip + 1, lane) << 8);
+            }
             ip += 2;
-            if ((int64_t)off > op) { bad = true; break; }
-            int64_t ml = token & 15;
+            if (off > op) { bad = true; break; }
+            uint32_t ml = token & 15u;
             if (ml == 15) {
                 uint32_t s;
                 do {
-                    if (ip > ni - (int64_t)kLastLit) { bad = true; break; }
-                    s = win_byte(W, (uint32_t)ip++, lane);
+                    if (ip + kLastLit > n) { bad = true; break; }
+                    s = win_byte(W, ip++, lane);
                     ml += s;
                 } while (s == 255);
                 if (bad) break;
             }
             ml += kMinMatch;
-            if (cap - op < ml || op + ml > cap - (int64_t)kLastLit) { bad = true; break; }
+            if (ml > cap - op || (uint64_t)op + ml + kLastLit > cap) { bad = true; break; }
             uint8_t *o = dst + op;
-            const uint32_t uop = (uint32_t)op, uml = (uint32_t)ml;
-            if (off == 0) {
+            if (ml <= 64 && ml <= off && off + ml <= kDRing) {
+                // the common case: one step, disjoint source in the ring
+                if (lane < ml) {
+                    const uint32_t v = ring[(op - off + lane) & RM];
+                    st8(o + lane, v);
+                    ring[(op + lane) & RM] = (uint8_t)v;
+                }
+            } else if (off == 0) {
                 // an offset of 0 copies the bytes being written: LZ4 1.9 zero-fills them
-                for (uint32_t j = lane; j < uml; j += 64) {
+                for (uint32_t j = lane; j < ml; j += 64) {
                     st8(o + j, 0u);
-                    ring[(uop + j) & RM] = 0;
+                    ring[(op + j) & RM] = 0;
                 }
-            } else if (uml <= off && off + uml <= kDRing) {
+            } else if (ml <= off && off + ml <= kDRing) {
                 // disjoint source in the ring (no write of this match reaches a
-                // slot a later read of it needs): the common case, no modulo
-                for (uint32_t j = lane; j < uml; j += 64) {
-                    const uint32_t v = ring[(uop - off + j) & RM];
+                // slot a later read of it needs)
+                for (uint32_t j = lane; j < ml; j += 64) {
+                    const uint32_t v = ring[(op - off + j) & RM];
                     st8(o + j, v);
-                    ring[(uop + j) & RM] = (uint8_t)v;
+                    ring[(op + j) & RM] = (uint8_t)v;
                 }
-            } else if (off <= 64 && uml <= (1u << 24)) {
+            } else if (off <= 64 && ml <= (1u << 24)) {
                 // short period: the off source bytes, read once, repeat.  j % off
                 // by a float reciprocal (j < 2^24: the quotient is off by at most one)
                 const float rcp = 1.0f / (float)off;
                 auto mod = [&](uint32_t j) {
                     uint32_t q = (uint32_t)((float)j * rcp);
-                    int32_t r = (int32_t)(j - q * off);
-                    r += r < 0 ? (int32_t)off : 0;
-                    r -= r >= (int32_t)off ? (int32_t)off : 0;
-                    return (uint32_t)r;
+                    int32_t rr = (int32_t)(j - q * off);
+                    rr += rr < 0 ? (int32_t)off : 0;
+                    rr -= rr >= (int32_t)off ? (int32_t)off : 0;
+                    return (uint32_t)rr;
                 };
-                const uint32_t pat = ring[(uop - off + mod(lane)) & RM];
-                for (uint32_t j0 = 0; j0 < uml; j0 += 64) {
+                const uint32_t pat = ring[(op - off + mod(lane)) & RM];
+                for (uint32_t j0 = 0; j0 < ml; j0 += 64) {
                     // every lane joins the ds_bpermute (a disabled source lane reads 0)
                     const uint32_t j = j0 + lane;
                     const uint32_t v = __shfl(pat, (int)mod(j), 64);
-                    if (j < uml) {
+                    if (j < ml) {
                         st8(o + j, v);
-                        ring[(uop + j) & RM] = (uint8_t)v;
+                        ring[(op + j) & RM] = (uint8_t)v;
                     }
                 }
-            } else if (off + uml <= kDRing) {
+            } else if (off + ml <= kDRing) {
                 // overlapping, period > 64: the first off bytes repeat
-                for (uint32_t j = lane; j < uml; j += 64) {
-                    const uint32_t v = ring[(uop - off + (j < off ? j : j % off)) & RM];
+                for (uint32_t j = lane; j < ml; j += 64) {
+                    const uint32_t v = ring[(op - off + (j < off ? j : j % off)) & RM];
                     st8(o + j, v);
-                    ring[(uop + j) & RM] = (uint8_t)v;
+                    ring[(op + j) & RM] = (uint8_t)v;
                 }
             } else {
-                const int64_t need = op - off + (ml < (int64_t)off ? ml : (int64_t)off);  // source end
+                const uint32_t need = op - off + (ml < off ? ml : off);  // source end
                 if (need > fenced) {
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                     fenced = op;
                 }
                 const uint8_t *m = o - off;
-                if (ml <= (int64_t)off)
-                    wave_copy(o, m, uml, lane);  // disjoint
+                if (ml <= off)
+                    wave_copy(o, m, ml, lane);  // disjoint
                 else  // overlapping: the first off bytes repeat
-                    for (uint32_t j = lane; j < uml; j += 64) st8(o + j, ld8(m + j % off));
-                for (uint32_t j = (uml > kDRing ? uml - kDRing : 0) + lane; j < uml; j += 64)
-                    ring[(uop + j) & RM] = (uint8_t)ld8(m + (j < off ? j : j % off));
+                    for (uint32_t j = lane; j < ml; j += 64) st8(o + j, ld8(m + j % off));
+                for (uint32_t j = (ml > kDRing ? ml - kDRing : 0) + lane; j < ml; j += 64)
+                    ring[(op + j) & RM] = (uint8_t)ld8(m + (j < off ? j : j % off));
             }
             op += ml;
         }
