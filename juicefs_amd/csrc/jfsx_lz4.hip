@@ -27,9 +27,11 @@
 //     8192 x u16) lives in LDS: 10 waves per CU.
 // The decompressor parses tokens from a 256-byte window of the input held in
 // the wave's VGPRs (one dword per lane, read back with v_readlane) and copies
-// literals / matches 64 bytes per step; a match reads only output written
-// before it (overlapping matches are expanded as out[op+i] = out[op-off+i%off]),
-// after the wave's earlier stores have completed (s_waitcnt vmcnt(0)).
+// literals / matches 64 bytes per step into an LDS ring of the recent output,
+// which leaves for global memory in coalesced 1 KiB wave stores; a match reads
+// only output written before it (overlapping matches are expanded as
+// out[op+i] = out[op-off+i%off]), from the ring, or from global memory once
+// the wave's stores of it have completed (s_waitcnt vmcnt(0)).
 #include "jfsx_dev.h"
 
 namespace jfsx {
@@ -77,18 +79,46 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_re
 // lanes below / above this one
 __device__ __forceinline__ uint64_t lanes_below(uint32_t lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
-// dst[0, len) = src[0, len), 64 lanes x 4 bytes per step on dword-aligned
-// destination words (head and tail byte-wise); src and dst do not overlap
+// dst[0, len) = src[0, len); src and dst do not overlap.  16-byte stores on
+// 16-byte aligned destination units (head and tail byte-wise), each unit from
+// one dword-aligned 16-byte load plus, when src and dst disagree modulo 4,
+// the next dword (never a dword without a source byte: page-safe); four
+// 1 KiB wave steps in flight per round.
 __device__ void wave_copy(uint8_t *dst, const uint8_t *src, uint32_t len, uint32_t lane) {
-    uint32_t head = (uint32_t)(-(uintptr_t)dst & 3);
+    typedef __attribute__((address_space(1))) v4u gv4;
+    typedef __attribute__((address_space(1))) const v4u gcv4;
+    uint32_t head = (uint32_t)(-(uintptr_t)dst & 15);
     if (head > len) head = len;
     if (lane < head) st8(dst + lane, ld8(src + lane));
     uint32_t i = head;
-    for (; i + 256 <= len; i += 256) {
-        const uint32_t o = i + 4 * lane;
-        *(__attribute__((address_space(1))) uint32_t *)(dst + o) = ld32u(src + o);
+    const uintptr_t sx = (uintptr_t)(src + i);
+    const uint32_t sh = (uint32_t)(sx & 3);
+    const uint8_t *sa = (const uint8_t *)(sx & ~(uintptr_t)3);  // src + i - sh
+    uint8_t *d = dst + i;
+    auto unit = [&](uint32_t o) {  // 16 bytes at d + o from sa + o
+        const v4u v = *(gcv4 *)(sa + o);
+        v4u r;
+        if (sh) {
+            const uint32_t e = ld32a(sa + o + 16);
+            r.x = __builtin_amdgcn_alignbyte(v.y, v.x, sh);
+            r.y = __builtin_amdgcn_alignbyte(v.z, v.y, sh);
+            r.z = __builtin_amdgcn_alignbyte(v.w, v.z, sh);
+            r.w = __builtin_amdgcn_alignbyte(e, v.w, sh);
+        } else {
+            r = v;
+        }
+        *(gv4 *)(d + o) = r;
+    };
+    const uint32_t body = len - i;
+    uint32_t o = 0;
+    for (; o + 4096 <= body; o += 4096) {
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) unit(o + 1024 * k + 16 * lane);
     }
-    for (uint32_t j = i + lane; j < len; j += 64) st8(dst + j, ld8(src + j));
+    for (; o + 16 <= body; o += 1024)
+        if (o + 16 * lane + 16 <= body) unit(o + 16 * lane);
+    o = body & ~15u;
+    if (lane < body - o) st8(d + o + lane, ld8(src + i + o + lane));
 }
 
 __device__ void wave_fill255(uint8_t *dst, uint32_t cnt, uint32_t lane) {
@@ -431,7 +461,6 @@ namespace {
 
 // 256-byte window of the compressed input in the wave's VGPRs
 struct DWin {
-    const uint8_t *src;
     uint32_t n;
     uint32_t w0;   // window start (multiple of 4, relative to src's dword-aligned base)
     uint32_t w;    // this lane's dword
@@ -447,18 +476,16 @@ __device__ __forceinline__ void win_load(DWin &W, uint32_t pos, uint32_t lane) {
     W.w = in ? ld32a((const uint8_t *)(W.al + o)) : 0u;
 }
 
-// dst[0, len) = input [pos, pos + len) when the window holds it (else false)
-__device__ __forceinline__ bool win_copy(uint8_t *dst, const DWin &W, uint32_t pos, uint32_t len, uint32_t lane) {
+// input bytes [pos, pos + 4) as a little-endian word (uniform; reloads the
+// window at pos when it does not hold them).  Two v_readlane and one 64-bit
+// scalar shift: the parse stays in SGPRs.
+__device__ __forceinline__ uint32_t win_u32(DWin &W, uint32_t pos, uint32_t lane) {
     const uint32_t x = pos + W.sh;
-    if (x < W.w0 || x + len > W.w0 + 256u) return false;
+    if (x < W.w0 || x + 4u > W.w0 + 256u) win_load(W, pos, lane);
     const uint32_t r = x - W.w0;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
-        const uint32_t j = lane + 64 * k, q = r + j;
-        const uint32_t d = __shfl(W.w, (int)((q >> 2) & 63), 64);
-        if (j < len) st8(dst + j, (d >> (8 * (q & 3))) & 255u);
-    }
-    return true;
+    const uint64_t d = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(W.w, r >> 2) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(W.w, ((r >> 2) + 1) & 63) << 32);
+    return (uint32_t)(d >> (8 * (r & 3)));
 }
 
 __device__ __forceinline__ uint32_t win_byte(DWin &W, uint32_t pos, uint32_t lane) {
@@ -468,135 +495,320 @@ __device__ __forceinline__ uint32_t win_byte(DWin &W, uint32_t pos, uint32_t lan
     return (__builtin_amdgcn_readlane(W.w, r >> 2) >> (8 * (r & 3))) & 255u;
 }
 
+typedef __attribute__((address_space(1))) v4u gv4u;
+
 }  // namespace
 
-constexpr uint32_t kDRing = 16384;  // decoder's LDS copy of the most recent output bytes
+// The decoder writes its output into an LDS ring and from there to global
+// memory in coalesced 16-byte stores (one 1 KiB wave store per step).  Output
+// position p sits at ring[(p + s) & (R - 1)], s = dst & 15, so a ring slot and
+// the global address of its byte agree modulo 16.
+#ifndef JFSX_LZ4_RING
+#define JFSX_LZ4_RING 8192
+#endif
+constexpr uint32_t kDRing = JFSX_LZ4_RING;  // decoder ring: the most recent output bytes
+#ifndef JFSX_LZ4_FLUSH
+#define JFSX_LZ4_FLUSH 4096
+#endif
+constexpr uint32_t kDFlush = JFSX_LZ4_FLUSH;  // flush once this many unflushed bytes are in the ring
+
+namespace {
+
+// global image bytes [a, b) (image coordinate = position + s; dal = dst - s,
+// 16-byte aligned) from the ring: aligned 16-byte units as 1 KiB wave stores,
+// the partial units at either end byte-wise
+template <uint32_t R>
+__device__ void ring_flush(uint8_t *dal, const uint8_t *ring, uint32_t a, uint32_t b, uint32_t lane) {
+    constexpr uint32_t RM = R - 1;
+    if (a >= b) return;
+    const uint32_t u0 = (a + 15) & ~15u, u1 = b & ~15u;
+    if (u0 >= u1) {
+        if (lane < b - a) st8(dal + a + lane, ring[(a + lane) & RM]);
+        return;
+    }
+    if (lane < u0 - a) st8(dal + a + lane, ring[(a + lane) & RM]);
+    for (uint32_t u = u0; u < u1; u += 1024) {
+        const uint32_t x = u + 16 * lane;
+        if (x < u1) *(gv4u *)(dal + x) = *(const v4u *)(ring + (x & RM));
+    }
+    if (lane < b - u1) st8(dal + u1 + lane, ring[(u1 + lane) & RM]);
+}
+
+// ring bytes of positions [p, p + cnt) from global bytes g[0, cnt)
+template <uint32_t R>
+__device__ void ring_fill(uint8_t *ring, uint32_t s, uint32_t p, uint32_t cnt, const uint8_t *g, uint32_t lane) {
+    constexpr uint32_t RM = R - 1;
+#pragma unroll 1
+    for (uint32_t j = lane; j < cnt; j += 64) ring[(p + s + j) & RM] = (uint8_t)ld8(g + j);
+}
+
+}  // namespace
+
+// Lane L decodes the sequence that would start at input position base + L
+// (the window holds [base, base + 96)) for the fast path.  A sequence is
+// "short" when none of LZ4_decompress_safe's input-side checks can reject it:
+// literal run < 15, match nibble < 15, no overlap (off >= match length), and
+// it ends at least 8 bytes before the input end.
+//   c.f  bit 0: short and its successor token lies within the 64 lanes;
+//        bit 1: off > near (the source is farther back than the ring keeps);
+//        bit 2: short, but the successor lies past lane 63 (refresh first);
+//        bits 8-13: the successor's lane
+//   c.ll literal length, c.tot literal + match length, c.off offset
+struct SeqCand {
+    uint32_t f, ll, tot, off;
+};
+template <uint32_t NEAR>
+__device__ __forceinline__ SeqCand seq_candidates(const DWin &W, uint32_t base, uint32_t n, uint32_t lane) {
+    const uint32_t p = base + lane, r = p + W.sh - W.w0;
+    const uint32_t t = (__shfl(W.w, (int)(r >> 2), 64) >> (8 * (r & 3))) & 255u;
+    const uint32_t ll = t >> 4, mn = t & 15u, q = r + 1 + ll;
+    const uint32_t d0 = __shfl(W.w, (int)(q >> 2), 64), d1 = __shfl(W.w, (int)((q >> 2) + 1), 64);
+    const uint32_t off = __builtin_amdgcn_alignbyte(d1, d0, q & 3) & 0xffffu;
+    const uint32_t ml = mn + kMinMatch, next = lane + 3 + ll;
+    const bool shrt = ll < 15 && mn < 15 && off >= ml && p + 9 + ll <= n;
+    SeqCand c;
+    c.f = (uint32_t)(shrt && next < 64) | ((uint32_t)(off > NEAR) << 1) | ((uint32_t)(shrt && next >= 64) << 2) |
+          ((next & 63) << 8);
+    c.ll = ll;
+    c.tot = ll + ml;
+    c.off = off;
+    return c;
+}
 
 // One wave per block.  ZDev.len = compressed bytes, ZDev.cap = dst capacity
 // (< 2^32, checked on the host); ZOut.out_len = decoded bytes; status
 // JFSX_EFORMAT for a malformed stream.  The control flow is wave-uniform
-// 32-bit scalar code: a sequence's token, offset and the first length byte
-// come from one 4-byte read of the register window.  Every output byte is
-// also written to a 16 KiB LDS ring, so a match whose source lies within it
-// never waits for the wave's own global stores.
+// 32-bit scalar code: a sequence's token, offset and first length byte come
+// from one 4-byte read of the register window.  Output is assembled in the
+// LDS ring and leaves it in 4 KiB coalesced flushes, so a match whose source
+// lies in the ring reads LDS, and only a source farther back than the ring
+// (already flushed) is read from global memory.  Long literal runs and long
+// or far overlapping matches copy global to global after a flush.
+template <uint32_t R>
 __global__ __launch_bounds__(64) void lz4_decompress_k(const ZDev *__restrict__ blks, ZOut *__restrict__ outs) {
-    __shared__ uint8_t ring[kDRing];
+    // ring room: a flush leaves < kDFlush + 16 unflushed bytes; then a literal
+    // run of <= 256 bytes and a 64-byte copy; a far source (off > R - 64) is
+    // flushed when kDFlush + 142 <= R
+    static_assert(R >= kDFlush + 16 + 256 + 64 && (R & (R - 1)) == 0, "ring size");
+    __shared__ __attribute__((aligned(16))) uint8_t ring[R];
+    constexpr uint32_t RM = R - 1;
+    // a ring source must lie within the last R - 64 bytes: the fast path's
+    // 64-lane copies may overwrite the 64 slots after the write position
+    constexpr uint32_t NR = R - 64;
     const uint32_t lane = threadIdx.x;
     const ZDev b = blks[blockIdx.x];
     const uint8_t *src = b.src;
     uint8_t *dst = b.dst;
     const uint32_t n = uni((uint32_t)b.len);
     const uint32_t cap = uni((uint32_t)b.cap);
-    constexpr uint32_t RM = kDRing - 1;
-    uint32_t op = 0;
+    const uint32_t s = (uint32_t)((uintptr_t)dst & 15);
+    uint8_t *dal = dst - s;
+    uint32_t op = 0, fl = 0, fenced = 0;  // [0, fl) flushed to dst; [0, fenced) visible to this wave's loads
     bool bad = false;
+    // everything up to op to dst (the bulk paths write dst directly after it)
+    auto flush_all = [&]() {
+        ring_flush<R>(dal, ring, fl + s, op + s, lane);
+        fl = op;
+    };
+    // make dst bytes below need visible to this wave's loads
+    auto fence = [&](uint32_t need) {
+        if (need > fenced) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            fenced = fl;
+        }
+    };
     if (cap == 0) {
         bad = !(n == 1 && ld8(src) == 0);
     } else if (n == 0) {
         bad = true;
     } else {
         DWin W;
-        W.src = src;
         W.n = n;
         W.al = (uintptr_t)src & ~(uintptr_t)3;
         W.sh = (uint32_t)((uintptr_t)src & 3);
         win_load(W, 0, lane);
-        uint32_t ip = 0, fenced = 0;  // dst bytes [0, fenced) are visible to this wave's loads
-        for (;;) {
-            if (ip >= n) { bad = true; break; }
-            // token .. token + 3 in one read (the window then holds ip .. ip + 7)
-            uint32_t x = ip + W.sh;
-            if (x < W.w0 || x + 8u > W.w0 + 256u) {
-                win_load(W, ip, lane);
-                x = ip + W.sh;
+        uint32_t ip = 0, base = 0, litq = 0;
+        SeqCand cand{0, 0, 0, 0};
+        bool stale = true;
+        const uint32_t lane_s = lane + s;
+        // literals [ip, ip + len) to output position op.  A run the window
+        // holds goes to the ring; a longer one is copied global to global
+        // (and its last R bytes to the ring unless it ends the block).
+        auto literals = [&](uint32_t len, bool last) {
+            const uint32_t xl = ip + W.sh;
+            if (len <= 253u && (xl < W.w0 || xl + len > W.w0 + 256u)) win_load(W, ip, lane);
+            if (xl >= W.w0 && xl + len <= W.w0 + 256u) {
+                const uint32_t rl = xl - W.w0;
+#pragma unroll
+                for (uint32_t k = 0; k < 4; k++) {
+                    if (64 * k >= len) break;
+                    const uint32_t j = lane + 64 * k, q = rl + j;
+                    const uint32_t d = __shfl(W.w, (int)((q >> 2) & 63), 64);
+                    if (j < len) ring[(op + s + j) & RM] = (uint8_t)(d >> (8 * (q & 3)));
+                }
+            } else {
+                flush_all();
+                wave_copy(dst + op, src + ip, len, lane);
+                if (!last) {
+                    const uint32_t k = len > R ? len - R : 0u;
+                    ring_fill<R>(ring, s, op + k, len - k, src + ip + k, lane);
+                }
+                fl = op + len;
             }
-            const uint32_t r = x - W.w0;
-            const uint32_t D = __builtin_amdgcn_alignbyte(__builtin_amdgcn_readlane(W.w, (r >> 2) + 1),
-                                                          __builtin_amdgcn_readlane(W.w, r >> 2), r & 3);
+        };
+        for (;;) {
+            if (op - fl >= kDFlush) {
+                // flush whole 16-byte units only, so the next flush starts aligned
+                const uint32_t e = (op + s) & ~15u;
+                ring_flush<R>(dal, ring, fl + s, e, lane);
+                fl = e - s;
+            }
+            // ---- fast path: sequences decoded in advance by the lanes ----
+            if (stale || ip - base >= 64u) {
+                base = ip;
+                const uint32_t x = base + W.sh;
+                if (x < W.w0 || x + 96u > W.w0 + 256u) win_load(W, base, lane);
+                cand = seq_candidates<NR>(W, base, n, lane);
+                litq = base + 1 + W.sh - W.w0 + lane;  // window byte of literal lane for kk = 0
+                stale = false;
+            }
+            {
+                // Every check of a sequence comes before its first write, so an
+                // exit leaves (ip, op) at a sequence start for the general path.
+                // Copies run on all 64 lanes: the bytes past a literal run or
+                // match land on output positions written again before they are
+                // flushed, and on ring slots no near match (off <= R - 64) reads.
+                uint32_t kk = ip - base;
+                const uint32_t fstop = fl + kDFlush;
+                const uint32_t opstop = cap >= 44u ? min(fstop, cap - 43u) : 0u;
+                uint32_t info = __builtin_amdgcn_readlane(cand.f, kk);
+                auto run = [&](auto early) {
+                    while ((info & 1u) && op < opstop) {
+                        const uint32_t ll = __builtin_amdgcn_readlane(cand.ll, kk);
+                        const uint32_t off = __builtin_amdgcn_readlane(cand.off, kk);
+                        if (decltype(early)::value && op + ll < off) break;  // the general path rejects it
+                        // the literal run (64 window bytes) at op, then the match at op + ll
+                        const uint32_t q = kk + litq;
+                        const uint32_t d = __shfl(W.w, (int)((q >> 2) & 63), 64);
+                        ring[(op + lane_s) & RM] = (uint8_t)(d >> (8 * (q & 3)));
+                        const uint32_t dp = op + ll + lane_s;
+                        if (!(info & 2u)) {
+#ifdef JFSX_ABLATE_NEAR
+                            ring[dp & RM] = (uint8_t)off;
+#else
+                            ring[dp & RM] = ring[(dp - off) & RM];
+#endif
+                        } else {
+#ifdef JFSX_ABLATE_FAR
+                            ring[dp & RM] = (uint8_t)off;
+#else
+                            // farther back than the ring: flushed, read dst
+                            const uint32_t srcp = op + ll - off;
+                            fence(srcp + 64u);
+                            ring[dp & RM] = (uint8_t)ld8(dst + srcp + lane);
+#endif
+                        }
+                        op += __builtin_amdgcn_readlane(cand.tot, kk);
+                        kk = (info >> 8) & 63u;
+                        info = __builtin_amdgcn_readlane(cand.f, kk);
+                    }
+                };
+                if (op >= 65536u)
+                    run(std::false_type{});
+                else
+                    run(std::true_type{});
+                ip = base + kk;
+                if (op >= fstop) continue;  // flush, then on
+                if (!(info & 1u) && (info & 4u)) {
+                    stale = true;  // the next token is past the candidates
+                    continue;
+                }
+            }
+            // ---- general path: one sequence with every LZ4_decompress_safe check ----
+            stale = true;
+            if (ip >= n) { bad = true; break; }
+            const uint32_t D = win_u32(W, ip, lane);  // token and the next 3 bytes
             const uint32_t token = D & 255u;
             ip++;
             uint32_t len = token >> 4;
             if (len == 15) {
-                uint32_t s;
+                uint32_t sb;
                 do {
                     if (ip + 15 >= n) { bad = true; break; }
-                    s = win_byte(W, ip++, lane);
-                    len += s;
-                } while (s == 255);
+                    sb = win_byte(W, ip++, lane);
+                    len += sb;
+                } while (sb == 255);
                 if (bad) break;
             }
             if (len > cap - op || len > n - ip) { bad = true; break; }
             if ((uint64_t)op + len + kMfLimit > cap || (uint64_t)ip + len + (2 + 1 + kLastLit) > n) {
                 // the last sequence: it must end the input exactly
                 if (ip + len != n) { bad = true; break; }
-                if (!win_copy(dst + op, W, ip, len, lane)) wave_copy(dst + op, src + ip, len, lane);
+                literals(len, true);
                 op += len;
                 break;
             }
-            uint32_t off;
+            uint32_t off, ml = token & 15u, e1;  // e1: the byte after the offset
             if (len == 0) {
-                off = (D >> 8) & 0xffffu;  // the offset follows the token
+                off = (D >> 8) & 0xffffu;
+                e1 = D >> 24;
             } else {
-                // literals -> output and ring (the ring needs only their last kDRing bytes)
-                const uint32_t xl = ip + W.sh;
-                if (xl >= W.w0 && xl + len <= W.w0 + 256u) {
-                    const uint32_t rl = xl - W.w0;
-#pragma unroll
-                    for (uint32_t k = 0; k < 4; k++) {
-                        const uint32_t j = lane + 64 * k, q = rl + j;
-                        const uint32_t d = __shfl(W.w, (int)((q >> 2) & 63), 64);
-                        const uint32_t v = (d >> (8 * (q & 3))) & 255u;
-                        if (j < len) {
-                            st8(dst + op + j, v);
-                            ring[(op + j) & RM] = (uint8_t)v;
-                        }
-                    }
-                } else {
-                    wave_copy(dst + op, src + ip, len, lane);
-                    for (uint32_t j = (len > kDRing ? len - kDRing : 0) + lane; j < len; j += 64)
-                        ring[(op + j) & RM] = (uint8_t)ld8(src + ip + j);
-                }
+                literals(len, false);
                 ip += len;
                 op += len;
-                off = win_byte(W, ip, lane) | (win_byte(W, ip + 1, lane) << 8);
+                const uint32_t w = win_u32(W, ip, lane);
+                off = w & 0xffffu;
+                e1 = (w >> 16) & 255u;
             }
             ip += 2;
             if (off > op) { bad = true; break; }
-            uint32_t ml = token & 15u;
             if (ml == 15) {
-                uint32_t s;
-                do {
+                if (ip + kLastLit > n) { bad = true; break; }
+                uint32_t sb = e1;
+                ip++;
+                ml += sb;
+                while (sb == 255) {
                     if (ip + kLastLit > n) { bad = true; break; }
-                    s = win_byte(W, ip++, lane);
-                    ml += s;
-                } while (s == 255);
+                    sb = win_byte(W, ip++, lane);
+                    ml += sb;
+                }
                 if (bad) break;
             }
             ml += kMinMatch;
             if (ml > cap - op || (uint64_t)op + ml + kLastLit > cap) { bad = true; break; }
-            uint8_t *o = dst + op;
-            if (ml <= 64 && ml <= off && off + ml <= kDRing) {
-                // the common case: one step, disjoint source in the ring
-                if (lane < ml) {
-                    const uint32_t v = ring[(op - off + lane) & RM];
-                    st8(o + lane, v);
-                    ring[(op + lane) & RM] = (uint8_t)v;
-                }
-            } else if (off == 0) {
+            if (ml <= 64 && ml <= off && off <= NR) {
+                // one step, the source in the ring (all of this step's reads
+                // happen before its writes)
+#ifdef JFSX_ABLATE_NEAR
+                if (lane < ml) ring[(op + s + lane) & RM] = (uint8_t)off;
+#else
+                if (lane < ml) ring[(op + s + lane) & RM] = ring[(op - off + s + lane) & RM];
+#endif
+                op += ml;
+                continue;
+            }
+            if (op + ml > fl + R) flush_all();  // ring room for the match
+            if (ml <= R && off == 0) {
                 // an offset of 0 copies the bytes being written: LZ4 1.9 zero-fills them
-                for (uint32_t j = lane; j < ml; j += 64) {
-                    st8(o + j, 0u);
-                    ring[(op + j) & RM] = 0;
+                for (uint32_t j = lane; j < ml; j += 64) ring[(op + s + j) & RM] = 0;
+            } else if (ml <= R && ml <= off && off <= NR) {
+                // disjoint, in the ring: step k's source lies above every slot
+                // steps < k overwrote
+                for (uint32_t j0 = 0; j0 < ml; j0 += 64) {
+                    const uint32_t j = j0 + lane;
+                    if (j < ml) ring[(op + s + j) & RM] = ring[(op - off + s + j) & RM];
                 }
-            } else if (ml <= off && off + ml <= kDRing) {
-                // disjoint source in the ring (no write of this match reaches a
-                // slot a later read of it needs)
-                for (uint32_t j = lane; j < ml; j += 64) {
-                    const uint32_t v = ring[(op - off + j) & RM];
-                    st8(o + j, v);
-                    ring[(op + j) & RM] = (uint8_t)v;
-                }
-            } else if (off <= 64 && ml <= (1u << 24)) {
+            } else if (ml <= 64 && ml <= off) {
+                // disjoint and farther back than the ring: flushed, read dst
+#ifdef JFSX_ABLATE_FAR
+                if (lane < ml) ring[(op + s + lane) & RM] = (uint8_t)off;
+#else
+                if (op - off + ml > fl) flush_all();
+                fence(op - off + ml);
+                if (lane < ml) ring[(op + s + lane) & RM] = (uint8_t)ld8(dst + op - off + lane);
+#endif
+            } else if (off != 0 && off <= 64 && ml <= R && ml <= (1u << 24)) {
                 // short period: the off source bytes, read once, repeat.  j % off
                 // by a float reciprocal (j < 2^24: the quotient is off by at most one)
                 const float rcp = 1.0f / (float)off;
@@ -607,41 +819,38 @@ __global__ __launch_bounds__(64) void lz4_decompress_k(const ZDev *__restrict__ 
                     rr -= rr >= (int32_t)off ? (int32_t)off : 0;
                     return (uint32_t)rr;
                 };
-                const uint32_t pat = ring[(op - off + mod(lane)) & RM];
+                const uint32_t pat = ring[(op - off + s + mod(lane)) & RM];
                 for (uint32_t j0 = 0; j0 < ml; j0 += 64) {
                     // every lane joins the ds_bpermute (a disabled source lane reads 0)
                     const uint32_t j = j0 + lane;
                     const uint32_t v = __shfl(pat, (int)mod(j), 64);
-                    if (j < ml) {
-                        st8(o + j, v);
-                        ring[(op + j) & RM] = (uint8_t)v;
-                    }
+                    if (j < ml) ring[(op + s + j) & RM] = (uint8_t)v;
                 }
-            } else if (off + ml <= kDRing) {
+            } else if (off != 0 && off <= NR && off + ml <= R) {
                 // overlapping, period > 64: the first off bytes repeat
-                for (uint32_t j = lane; j < ml; j += 64) {
-                    const uint32_t v = ring[(op - off + (j < off ? j : j % off)) & RM];
-                    st8(o + j, v);
-                    ring[(op + j) & RM] = (uint8_t)v;
-                }
+                for (uint32_t j = lane; j < ml; j += 64)
+                    ring[(op + s + j) & RM] = ring[(op - off + s + (j < off ? j : j % off)) & RM];
             } else {
-                const uint32_t need = op - off + (ml < off ? ml : off);  // source end
-                if (need > fenced) {
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                    fenced = op;
-                }
+                // long: global to global after a flush, then the last R bytes to the ring
+                flush_all();
+                fence(op);
+                uint8_t *o = dst + op;
                 const uint8_t *m = o - off;
-                if (ml <= off)
+                if (off == 0)
+                    for (uint32_t j = lane; j < ml; j += 64) st8(o + j, 0u);
+                else if (ml <= off)
                     wave_copy(o, m, ml, lane);  // disjoint
                 else  // overlapping: the first off bytes repeat
                     for (uint32_t j = lane; j < ml; j += 64) st8(o + j, ld8(m + j % off));
-                for (uint32_t j = (ml > kDRing ? ml - kDRing : 0) + lane; j < ml; j += 64)
-                    ring[(op + j) & RM] = (uint8_t)ld8(m + (j < off ? j : j % off));
+#pragma unroll 1
+                for (uint32_t j = (ml > R ? ml - R : 0) + lane; j < ml; j += 64)
+                    ring[(op + s + j) & RM] = off == 0 ? 0 : (uint8_t)ld8(m + (j < off ? j : j % off));
+                fl = op + ml;
             }
             op += ml;
         }
     }
+    if (!bad) ring_flush<R>(dal, ring, fl + s, op + s, lane);
     if (lane == 0) {
         outs[blockIdx.x].out_len = bad ? 0 : (uint64_t)op;
         outs[blockIdx.x].status = bad ? JFSX_EFORMAT : JFSX_OK;
@@ -653,7 +862,7 @@ void launch_lz4_compress(hipStream_t s, int n, const ZDev *blks, ZOut *outs) {
 }
 
 void launch_lz4_decompress(hipStream_t s, int n, const ZDev *blks, ZOut *outs) {
-    if (n > 0) hipLaunchKernelGGL(lz4_decompress_k, dim3(n), dim3(64), 0, s, blks, outs);
+    if (n > 0) hipLaunchKernelGGL(lz4_decompress_k<kDRing>, dim3(n), dim3(64), 0, s, blks, outs);
 }
 
 }  // namespace jfsx
