@@ -198,14 +198,22 @@ __device__ __forceinline__ void iwin_copy(uint8_t *dst, const IWin &W, const Img
 // Match length beyond MINMATCH at (ip, match): LZ4_count(ip + 4, match + 4,
 // matchlimit).  Loads the window C at ip + 4 (input side) and, in the same
 // round of loads, the catch-up bytes before ip / match (limc <= 64 of them;
-// back = equal bytes found, 64 when all were equal).  Returns mc.
+// back = equal bytes found, 64 when all were equal).  Returns mc.  With
+// skip = 0 the count starts at ip itself: the result is the number of equal
+// bytes from (ip, match), so the 4-byte test read32(match) == read32(ip) and
+// the count share one round of loads (result >= 4 <=> the test holds).
 __device__ uint32_t count_and_back(IWin &C, const Img &I, const uint8_t *src, uint32_t ip, uint32_t match,
-                                   uint32_t matchlimit, uint32_t limc, uint32_t &back, uint32_t lane) {
-    const uint32_t aa = ip + kMinMatch, off = ip - match;
+                                   uint32_t matchlimit, uint32_t limc, uint32_t &back, uint32_t lane,
+                                   uint32_t skip = kMinMatch) {
+    const uint32_t aa = ip + skip, off = ip - match;
     iwin_load(C, I, aa, lane);
     const uint32_t lp = C.w0 + 4 * lane - I.sh;  // input position of this lane's first window byte (may wrap below 0 on lane 0)
     const uint32_t mp = lp - off;
-    const uint32_t mw = ld32u(src + (mp + 4 <= I.n ? mp : I.n - 4));
+    // with skip = 0 and a match in the block's first 3 bytes, lane 0's match
+    // dword starts before byte 0: read the block's first dword shifted up
+    // (the bytes below 0 face input bytes before aa and are not compared)
+    const int32_t mps = (int32_t)mp;
+    const uint32_t mw = mps < 0 ? ld32u(src) << (8 * (uint32_t)(-mps)) : ld32u(src + (mp + 4 <= I.n ? mp : I.n - 4));
     bool ceq = false;
     if (lane < limc) ceq = ld8(src + ip - 1 - lane) == ld8(src + match - 1 - lane);
     const uint64_t cst = ballot(!ceq);
@@ -225,7 +233,7 @@ __device__ uint32_t count_and_back(IWin &C, const Img &I, const uint8_t *src, ui
     // a long match: continue 256 bytes per step from the window's end
     const uint32_t avail = matchlimit > aa ? matchlimit - aa : 0u;
     uint32_t mc = C.w0 + 256 - I.sh - aa;
-    const uint8_t *a2 = src + aa, *m2 = src + match + kMinMatch;
+    const uint8_t *a2 = src + aa, *m2 = src + match + skip;
     for (;;) {
         if (mc >= avail) return avail;
         const uint32_t t = mc + 4 * lane;
@@ -421,13 +429,17 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
                 const uint32_t h = uni(hash_of(w0, b0, small));
                 const uint32_t mi = uni(TGET(h));
                 if (lane == 0) TPUT(h, ip);
-                if ((small || mi + 65535u >= ip) && uni(ld32u(src + mi)) == w0) {
-                    tokpos = op++;
-                    tok = 0;
-                    match = mi;
+                if (small || mi + 65535u >= ip) {
+                    // the 4-byte test and the match length in one round of loads
                     uint32_t nb;
-                    mc = count_and_back(C, I, src, ip, match, matchlimit, 0u, nb, lane);
-                    continue;
+                    const uint32_t t = count_and_back(C, I, src, ip, mi, matchlimit, 0u, nb, lane, 0u);
+                    if (t >= kMinMatch) {
+                        tokpos = op++;
+                        tok = 0;
+                        match = mi;
+                        mc = t - kMinMatch;
+                        continue;
+                    }
                 }
                 break;
             }
