@@ -726,9 +726,10 @@ int run_lz4(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, bool comp) {
     if (n == 0) return 0;
     int rc;
     Workspace &w = c->ws[0];
-    const size_t o_out = align256(sizeof(ZDev) * n), dbytes = o_out + align256(sizeof(ZOut) * n);
+    const size_t o_out = align256(sizeof(ZDev) * n), o_tab = o_out + align256(sizeof(ZOut) * n);
+    const size_t dbytes = o_tab + (comp ? kLz4TabBytes * (size_t)n : 0);
     if ((rc = ensure_dev(c, &w.d, &w.dcap, dbytes))) return rc;
-    if ((rc = ensure_host(&w.h, &w.hcap, dbytes))) return rc;
+    if ((rc = ensure_host(&w.h, &w.hcap, o_tab))) return rc;  // descriptors and results only
     hipStream_t s = c->stream;
     ZDev *hz = (ZDev *)w.h;
     std::vector<char *> sdst(n, nullptr);
@@ -752,7 +753,7 @@ int run_lz4(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, bool comp) {
     HIP_OK(hipMemcpyAsync(w.d, w.h, sizeof(ZDev) * n, hipMemcpyHostToDevice, s));
     if (c->timing) HIP_OK(hipEventRecord(c->ev_k0[0], s));
     if (comp)
-        launch_lz4_compress(s, n, (const ZDev *)w.d, (ZOut *)(w.d + o_out));
+        launch_lz4_compress(s, n, (const ZDev *)w.d, (ZOut *)(w.d + o_out), (uint32_t *)(w.d + o_tab));
     else
         launch_lz4_decompress(s, n, (const ZDev *)w.d, (ZOut *)(w.d + o_out));
     if (c->timing) HIP_OK(hipEventRecord(c->ev_k1[0], s));

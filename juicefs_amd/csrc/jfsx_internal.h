@@ -288,7 +288,9 @@ void launch_crc_finalize(hipStream_t s, int n, int crc_mode, const BlkDev *blks,
 void launch_gen_synthetic(hipStream_t s, uint8_t *dst, uint64_t len, uint64_t seed, uint64_t block);
 void launch_gen_synthetic_batch(hipStream_t s, uint8_t *dst, uint64_t stride, int n, const uint64_t *lens,
                                 uint64_t seed, uint64_t block0);
-void launch_lz4_compress(hipStream_t s, int n, const ZDev *blks, ZOut *outs);
+// tabs: n x 16 KiB of device memory, the blocks' LZ4 hash tables
+constexpr size_t kLz4TabBytes = 16384;
+void launch_lz4_compress(hipStream_t s, int n, const ZDev *blks, ZOut *outs, uint32_t *tabs);
 void launch_lz4_decompress(hipStream_t s, int n, const ZDev *blks, ZOut *outs);
 // batched RSA-OAEP unwrap (jfsx_rsa.hip): key = device jfsx_rsa::Key
 void async_detach(jfsx_ctx *c);  // jfsx_agg.cpp

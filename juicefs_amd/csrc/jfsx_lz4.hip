@@ -218,13 +218,13 @@ __device__ uint32_t count_and_back(IWin &C, const Img &I, const uint8_t *src, ui
     if (lane < limc) ceq = ld8(src + ip - 1 - lane) == ld8(src + match - 1 - lane);
     const uint64_t cst = ballot(!ceq);
     back = cst ? (uint32_t)__builtin_ctzll(cst) : 64u;
-    const uint32_t x = C.w ^ mw;
-    uint32_t si = 4;
-#pragma unroll
-    for (int i = 3; i >= 0; i--) {
-        const int32_t ad = (int32_t)(lp + i);  // input position (signed: lane 0 may start before byte 0)
-        if (ad >= (int32_t)aa && ((uint32_t)ad >= matchlimit || ((x >> (8 * i)) & 255u))) si = (uint32_t)i;
-    }
+    // first byte i of this lane's 4 that stops the count: at or after aa, and
+    // differing or at or past matchlimit (k: bytes before aa, lane 0 only, <= 3)
+    const int32_t k = (int32_t)(aa - lp), m = (int32_t)(matchlimit - lp);
+    const uint32_t pre = k > 0 ? (0xffffffffu << (8 * (uint32_t)k)) : 0xffffffffu;
+    const uint32_t lim = m >= 4 ? 0u : (m <= 0 ? 0xffffffffu : (0xffffffffu << (8 * (uint32_t)m)));
+    const uint32_t y = ((C.w ^ mw) | lim) & pre;
+    const uint32_t si = y ? (uint32_t)__builtin_ctz(y) >> 3 : 4u;
     const uint64_t sm = ballot(si < 4);
     if (sm) {
         const int L = __builtin_ctzll(sm);
@@ -253,11 +253,45 @@ __device__ uint32_t count_and_back(IWin &C, const Img &I, const uint8_t *src, ui
 
 }  // namespace
 
+#ifdef JFSX_LZ4_STAMP
+// diagnostic build only: cycles per compressor section, summed over waves
+__device__ unsigned long long g_lz4_stamps[8];
+#define LZ_STAMP(t)                                                                   \
+    do {                                                                              \
+        __builtin_amdgcn_sched_barrier(0);                                            \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");   \
+        __builtin_amdgcn_sched_barrier(0);                                            \
+    } while (0)
+#define LZ_SEC(k)                      \
+    do {                               \
+        unsigned long long t_;         \
+        LZ_STAMP(t_);                  \
+        st_acc[k] += t_ - st_last;     \
+        st_last = t_;                  \
+    } while (0)
+#else
+#define LZ_SEC(k) \
+    do {          \
+    } while (0)
+#endif
+
 // One wave per block.  ZDev.len = input bytes, ZDev.cap >= LZ4_compressBound
 // (checked on the host); ZOut.out_len = compressed bytes.
-__global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ blks, ZOut *__restrict__ outs) {
+__global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ blks, ZOut *__restrict__ outs,
+                                                     uint32_t *__restrict__ tabs) {
+#ifdef JFSX_LZ4_LDS_TABLE
     __shared__ uint32_t T[4096];
     uint16_t *T16 = reinterpret_cast<uint16_t *>(T);
+#else
+    // The hash table in global memory (16 KiB per block, L2/MALL resident):
+    // occupancy is then set by VGPRs (8 waves per SIMD) instead of 16 KiB of
+    // LDS per wave (10 waves per CU).  A wave's own table reads and writes
+    // reach memory in program order, as LDS ones do.
+    typedef __attribute__((address_space(1))) uint32_t gtu32;
+    typedef __attribute__((address_space(1))) uint16_t gtu16;
+    gtu32 *T = (gtu32 *)(tabs + (size_t)blockIdx.x * 4096);
+    gtu16 *T16 = (gtu16 *)T;
+#endif
     const uint32_t lane = threadIdx.x;
     const ZDev b = blks[blockIdx.x];
     const uint8_t *src = b.src;
@@ -265,8 +299,12 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
     const uint32_t n = uni((uint32_t)b.len);
     const Img I{(const uint8_t *)((uintptr_t)src & ~(uintptr_t)3), (uint32_t)((uintptr_t)src & 3), n};
     const bool small = n < kLimit64K;
+#ifdef JFSX_LZ4_LDS_TABLE
     for (uint32_t i = lane; i < 4096; i += 64) T[i] = 0;
     __syncthreads();
+#else
+    for (uint32_t i = 4 * lane; i < 4096; i += 256) *(__attribute__((address_space(1))) v4u *)(T + i) = v4u{0, 0, 0, 0};
+#endif
 #define TGET(h) (small ? (uint32_t)T16[(h)] : T[(h)])
 #define TPUT(h, v)                            \
     do {                                      \
@@ -279,6 +317,10 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
         const uint32_t mflimit1 = n - kMfLimit + 1, matchlimit = n - kLastLit;
         if (lane == 0) TPUT(lz_hash(src, small), 0u);
         uint32_t ip = 1;
+#ifdef JFSX_LZ4_STAMP
+        unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last;
+        LZ_STAMP(st_last);
+#endif
         IWin W;  // input window; a search starts with it holding [anchor, anchor + 253)
         W.w0 = 0xfffff000u;  // empty
         W.w = 0;
@@ -351,6 +393,7 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
                     if (vmask != ~0ull) break;
                 }
             }
+            LZ_SEC(0);  // search
             if (!found) break;
             // ---- catch-up and match length in one round of loads ----
             // (bytes [ip', ip + 4) are equal after the catch-up, so the length
@@ -378,6 +421,7 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
             ip -= back;
             match -= back;
             mc += back;
+            LZ_SEC(1);  // catch-up + count
             // ---- literals ----
             uint32_t tokpos = op, tok;
             {
@@ -395,6 +439,7 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
                     wave_copy(dst + op, src + anchor, ll, lane);
                 op += ll;
             }
+            LZ_SEC(2);  // literals
             // ---- match, then as long as the next position matches at once ----
             for (;;) {
                 const uint32_t off = ip - match;
@@ -413,6 +458,7 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
                 if (lane == 0) st8(dst + tokpos, tok);
                 anchor = ip;
                 if (ip >= mflimit1) break;
+                LZ_SEC(3);  // emit match
                 // fill the table at ip - 2, then test ip itself (bytes from the
                 // count window when it holds them)
                 uint32_t wm2, bm2, w0, b0;
@@ -425,14 +471,17 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
                     w0 = uni(ld32u(src + ip));
                     b0 = uni(ld8(src + ip + 4));
                 }
-                if (lane == 0) TPUT(hash_of(wm2, bm2, small), ip - 2);
+                const uint32_t hm2 = uni(hash_of(wm2, bm2, small));
                 const uint32_t h = uni(hash_of(w0, b0, small));
+                if (lane == 0) TPUT(hm2, ip - 2);
                 const uint32_t mi = uni(TGET(h));
                 if (lane == 0) TPUT(h, ip);
                 if (small || mi + 65535u >= ip) {
                     // the 4-byte test and the match length in one round of loads
                     uint32_t nb;
+                    LZ_SEC(4);  // table + hash
                     const uint32_t t = count_and_back(C, I, src, ip, mi, matchlimit, 0u, nb, lane, 0u);
+                    LZ_SEC(5);  // next-position count
                     if (t >= kMinMatch) {
                         tokpos = op++;
                         tok = 0;
@@ -446,7 +495,12 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
             if (anchor >= mflimit1) break;
             ip++;
             W = C;  // the next search starts inside the count window
+            LZ_SEC(6);  // next-test tail
         }
+#ifdef JFSX_LZ4_STAMP
+        if (lane == 0)
+            for (int k = 0; k < 7; k++) atomicAdd(&g_lz4_stamps[k], st_acc[k]);
+#endif
     }
     // ---- last literals ----
     {
@@ -869,8 +923,22 @@ __global__ __launch_bounds__(64) void lz4_decompress_k(const ZDev *__restrict__ 
     }
 }
 
-void launch_lz4_compress(hipStream_t s, int n, const ZDev *blks, ZOut *outs) {
-    if (n > 0) hipLaunchKernelGGL(lz4_compress_k, dim3(n), dim3(64), 0, s, blks, outs);
+#ifdef JFSX_LZ4_STAMP
+}  // namespace jfsx
+extern "C" int jfsx_debug_lz4_stamps(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(jfsx::g_lz4_stamps), sizeof(unsigned long long) * 8) != hipSuccess)
+        return -1;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(jfsx::g_lz4_stamps), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+namespace jfsx {
+#endif
+
+void launch_lz4_compress(hipStream_t s, int n, const ZDev *blks, ZOut *outs, uint32_t *tabs) {
+    if (n > 0) hipLaunchKernelGGL(lz4_compress_k, dim3(n), dim3(64), 0, s, blks, outs, tabs);
 }
 
 void launch_lz4_decompress(hipStream_t s, int n, const ZDev *blks, ZOut *outs) {
