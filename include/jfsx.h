@@ -318,6 +318,17 @@ int jfsx_agg_lz4_decompress(jfsx_agg *agg, jfsx_zblk *blk, int mem);
 int jfsx_mctx_lz4_compress_batch(jfsx_mctx *m, int n, jfsx_zblk *blks, int mem);
 int jfsx_mctx_lz4_decompress_batch(jfsx_mctx *m, int n, jfsx_zblk *blks, int mem);
 
+/* Zstandard decompression (load side of "zstd" volumes):
+ * ZStandard.Decompress of pkg/compress (compress.go:93-100,
+ * github.com/DataDog/zstd v1.5.0 -> ZSTD_decompress), as cachedStore.load
+ * calls it (cached_store.go:680-745).  Each zblk's src holds zstd frames
+ * (concatenated frames and skippable frames allowed, as ZSTD_decompress);
+ * out_len = decoded bytes; status JFSX_EFORMAT where ZSTD_decompress returns
+ * an error (malformed frame, dictionary id, checksum mismatch, or output
+ * larger than dst_cap).  Compression ("zstd" Compress, level 1) stays on the
+ * host's libzstd. */
+int jfsx_zstd_decompress_batch(jfsx_ctx *ctx, int n, jfsx_zblk *blks, int mem);
+
 /* header helper: returns wrapped-key length and offset/size of the nonce so a
  * caller can unwrap the key first (encrypt.go:197-205) */
 int jfsx_parse_header(const void *obj, uint64_t olen, int *klen, int *nlen);

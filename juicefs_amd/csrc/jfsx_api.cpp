@@ -715,7 +715,7 @@ uint64_t lz4_bound(uint64_t n) { return n > kLz4MaxInput ? 0 : n + n / 255 + 16;
 // LZ4 stage (jfsx_lz4.hip): one wave per block.  Host-memory batches are
 // staged through the context's slot-0 staging buffer (inputs up, the
 // out_len bytes of each output down).
-int run_lz4(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, bool comp) {
+int run_lz4(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, bool comp, bool zstd = false) {
     if (n < 0 || (mem != JFSX_MEM_DEVICE && mem != JFSX_MEM_HOST)) return JFSX_EINVAL;
     for (int i = 0; i < n; i++) {
         if ((z[i].src_len && !z[i].src) || (z[i].dst_cap && !z[i].dst) || z[i].src_len > kLz4MaxInput ||
@@ -727,7 +727,7 @@ int run_lz4(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, bool comp) {
     int rc;
     Workspace &w = c->ws[0];
     const size_t o_out = align256(sizeof(ZDev) * n), o_tab = o_out + align256(sizeof(ZOut) * n);
-    const size_t dbytes = o_tab + (comp ? kLz4TabBytes * (size_t)n : 0);
+    const size_t dbytes = o_tab + (comp ? kLz4TabBytes * (size_t)n : zstd ? kZstdScratch * (size_t)n : 0);
     if ((rc = ensure_dev(c, &w.d, &w.dcap, dbytes))) return rc;
     if ((rc = ensure_host(&w.h, &w.hcap, o_tab))) return rc;  // descriptors and results only
     hipStream_t s = c->stream;
@@ -754,6 +754,8 @@ int run_lz4(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, bool comp) {
     if (c->timing) HIP_OK(hipEventRecord(c->ev_k0[0], s));
     if (comp)
         launch_lz4_compress(s, n, (const ZDev *)w.d, (ZOut *)(w.d + o_out), (uint32_t *)(w.d + o_tab));
+    else if (zstd)
+        launch_zstd_decompress(s, n, (const ZDev *)w.d, (ZOut *)(w.d + o_out), (uint8_t *)(w.d + o_tab));
     else
         launch_lz4_decompress(s, n, (const ZDev *)w.d, (ZOut *)(w.d + o_out));
     if (c->timing) HIP_OK(hipEventRecord(c->ev_k1[0], s));
@@ -980,6 +982,13 @@ int jfsx_lz4_decompress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
     std::lock_guard<std::mutex> g(c->mu);
     HIP_OK(hipSetDevice(c->device));
     return run_lz4(c, n, blks, mem, false);
+}
+
+int jfsx_zstd_decompress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
+    if (!c || (n > 0 && !blks)) return JFSX_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_OK(hipSetDevice(c->device));
+    return run_lz4(c, n, blks, mem, false, true);
 }
 
 int jfsx_checksum(jfsx_ctx *c, const void *data, uint64_t len, uint8_t *out) {

@@ -1,0 +1,121 @@
+// jfsx_zstd.hip -- Zstandard frame decompression on gfx950 (the load side of
+// --compress zstd volumes): one wave per object, the decoder
+// of jfsx_zstd.h run wave-uniformly.
+//
+// Replaces ZStandard.Decompress = zstd.Decompress(dst, src)
+// (pkg/compress/compress.go:93-100; DataDog/zstd v1.5.0) as called by
+// cachedStore.load (pkg/chunk/cached_store.go:680-745).
+//   * The compressed input is read with scalar loads (uniform addresses:
+//     the bit readers' 8-byte windows come from the scalar cache).
+//   * Decoding tables live in LDS (jzd::Tables, 20 KiB); table writes come
+//     from lane 0 and every lane reads them (same wave: LDS order holds).
+//   * Huffman literals go to a per-object 128 KiB scratch buffer; literal,
+//     raw and RLE runs and matches are copied by the 64 lanes; a match reads
+//     output written before it once the wave's stores have completed
+//     (s_waitcnt vmcnt(0)), overlapping matches as out[o+j] = out[o-off+j%off].
+#include "jfsx_dev.h"
+#include "jfsx_zstd.h"
+
+namespace jfsx {
+
+namespace {
+
+typedef __attribute__((address_space(4))) const uint32_t ccu32;
+typedef __attribute__((address_space(1))) const uint8_t gcu8z;
+typedef __attribute__((address_space(1))) uint8_t gu8z;
+
+struct DevEnv {
+    const uint8_t *src;  // compressed object
+    int64_t n;
+    uint8_t *dst;        // output (frame positions are offsets from dst)
+    uint8_t *lit;        // literal scratch (jzd::kBlockMax + 64 bytes)
+    uint32_t lane;
+
+    // input dword d (bytes [4d - sh, 4d - sh + 4) of src, src = al + sh), zero
+    // when it holds no input byte; scalar load (uniform address)
+    __device__ uint32_t dw(int64_t d) const {
+        const uintptr_t al = (uintptr_t)src & ~(uintptr_t)3;
+        const int64_t sh = (int64_t)((uintptr_t)src & 3);
+        const int64_t b0 = 4 * d - sh;  // first src byte of the dword
+        if (b0 + 3 < 0 || b0 >= n) return 0u;
+        uint32_t v = *(ccu32 *)(al + 4 * d);
+        // bytes outside [0, n) read as zero
+        if (b0 < 0) v &= 0xffffffffu << (8 * (uint32_t)(-b0));
+        if (b0 + 4 > n) v &= 0xffffffffu >> (8 * (uint32_t)(b0 + 4 - n));
+        return v;
+    }
+    __device__ uint32_t in8(int64_t i) const {
+        if (i < 0 || i >= n) return 0;
+        const int64_t x = i + (int64_t)((uintptr_t)src & 3);
+        return (dw(x >> 2) >> (8 * (uint32_t)(x & 3))) & 255u;
+    }
+    __device__ uint64_t in64(int64_t i) const {
+        const int64_t x = i + (int64_t)((uintptr_t)src & 3);
+        const int64_t d = x >> 2;  // floor (x may be negative)
+        const uint32_t s = (uint32_t)(x & 3);
+        const uint64_t lo = (uint64_t)dw(d) | ((uint64_t)dw(d + 1) << 32);
+        if (!s) return lo;
+        const uint64_t hi = dw(d + 2);
+        return (lo >> (8 * s)) | (hi << (64 - 8 * s));
+    }
+    __device__ void lit_put(uint64_t i, uint32_t b) const {
+        if (lane == 0) *(gu8z *)(lit + i) = (uint8_t)b;
+    }
+    __device__ void lit_fill(uint64_t i, uint32_t b, uint64_t cnt) const {
+        for (uint64_t j = lane; j < cnt; j += 64) *(gu8z *)(lit + i + j) = (uint8_t)b;
+    }
+    __device__ void fence() const {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+    __device__ void lit_sync() const { fence(); }
+    __device__ void out_sync() const { fence(); }
+    __device__ void out_from_in(uint64_t o, int64_t i, uint64_t cnt) const {
+        for (uint64_t j = lane; j < cnt; j += 64) *(gu8z *)(dst + o + j) = (uint8_t)in8_v(i + (int64_t)j);
+    }
+    // per-lane input byte (vector load)
+    __device__ uint32_t in8_v(int64_t i) const { return *(gcu8z *)(src + i); }
+    __device__ void out_from_lit(uint64_t o, uint64_t i, uint64_t cnt) const {
+        for (uint64_t j = lane; j < cnt; j += 64) *(gu8z *)(dst + o + j) = *(gcu8z *)(lit + i + j);
+    }
+    __device__ void out_fill(uint64_t o, uint32_t b, uint64_t cnt) const {
+        for (uint64_t j = lane; j < cnt; j += 64) *(gu8z *)(dst + o + j) = (uint8_t)b;
+    }
+    __device__ void out_match(uint64_t o, uint64_t off, uint64_t cnt) const {
+        fence();
+        const uint8_t *m = dst + o - off;
+        if (off >= cnt) {
+            for (uint64_t j = lane; j < cnt; j += 64) *(gu8z *)(dst + o + j) = *(gcu8z *)(m + j);
+        } else {
+            for (uint64_t j = lane; j < cnt; j += 64) *(gu8z *)(dst + o + j) = *(gcu8z *)(m + j % off);
+        }
+    }
+    __device__ uint64_t out64(uint64_t o) const {
+        uint64_t v = 0;
+        for (uint32_t k = 0; k < 8; k++) v |= (uint64_t)(*(gcu8z *)(dst + o + k)) << (8 * k);
+        return v;
+    }
+};
+
+}  // namespace
+
+// One wave per object.  ZDev.len = compressed bytes, ZDev.cap = dst capacity;
+// ZOut.out_len = decoded bytes, status JFSX_EFORMAT for a frame
+// ZSTD_decompress rejects (or one that does not fit in cap).
+__global__ __launch_bounds__(64) void zstd_decompress_k(const ZDev *__restrict__ blks, ZOut *__restrict__ outs,
+                                                        uint8_t *__restrict__ scratch) {
+    __shared__ jzd::Tables T;
+    const ZDev b = blks[blockIdx.x];
+    DevEnv e{b.src, (int64_t)b.len, b.dst, scratch + (size_t)blockIdx.x * (jzd::kBlockMax + 64), threadIdx.x};
+    const int64_t r = jzd::decompress(e, T, b.len, b.cap);
+    if (threadIdx.x == 0) {
+        outs[blockIdx.x].out_len = r < 0 ? 0 : (uint64_t)r;
+        outs[blockIdx.x].status = r < 0 ? JFSX_EFORMAT : JFSX_OK;
+    }
+}
+
+void launch_zstd_decompress(hipStream_t s, int n, const ZDev *blks, ZOut *outs, uint8_t *scratch) {
+    if (n > 0) hipLaunchKernelGGL(zstd_decompress_k, dim3(n), dim3(64), 0, s, blks, outs, scratch);
+}
+
+}  // namespace jfsx

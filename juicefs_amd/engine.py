@@ -40,6 +40,7 @@ EXPORTS = [
     "jfsx_mctx_seal_batch", "jfsx_mctx_open_batch", "jfsx_mctx_crc32c_segments", "jfsx_agg_new_mctx",
     "jfsx_agg_dev_batches", "jfsx_lz4_bound", "jfsx_lz4_compress_batch", "jfsx_lz4_decompress_batch",
     "jfsx_agg_lz4_compress", "jfsx_agg_lz4_decompress", "jfsx_mctx_lz4_compress_batch", "jfsx_mctx_lz4_decompress_batch",
+    "jfsx_zstd_decompress_batch",
 ]
 
 
@@ -150,6 +151,7 @@ def load_library(path=LIB_PATH):
             "jfsx_agg_lz4_decompress": (I, [P, ctypes.POINTER(jfsx_zblk), I]),
             "jfsx_mctx_lz4_compress_batch": (I, [P, I, ctypes.POINTER(jfsx_zblk), I]),
             "jfsx_mctx_lz4_decompress_batch": (I, [P, I, ctypes.POINTER(jfsx_zblk), I]),
+            "jfsx_zstd_decompress_batch": (I, [P, I, ctypes.POINTER(jfsx_zblk), I]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -367,6 +369,19 @@ class Engine:
         arr, n = self.make_zblocks((s.ctypes.data, s.size, d.ctypes.data, int(c))
                                    for s, d, c in zip(srcs, dsts, caps))
         self.lz4_decompress_batch(arr, n, MEM_HOST)
+        return [(arr[i].status, d[:arr[i].out_len].tobytes()) for i, d in enumerate(dsts)]
+
+    # -- Zstandard decompression (jfsx_zstd_decompress_batch) -------------
+    def zstd_decompress_batch(self, zblks, n, mem=MEM_DEVICE):
+        self._check(self.L.jfsx_zstd_decompress_batch(self.ctx, n, zblks, mem), "jfsx_zstd_decompress_batch")
+
+    def zstd_decompress(self, datas, caps):
+        """Host buffers of zstd frames in; list of (status, bytes) out (dst of caps[i] bytes)."""
+        srcs = [_u8(d) for d in datas]
+        dsts = [np.empty(max(int(c), 1), np.uint8) for c in caps]
+        arr, n = self.make_zblocks((s.ctypes.data, s.size, d.ctypes.data, int(c))
+                                   for s, d, c in zip(srcs, dsts, caps))
+        self.zstd_decompress_batch(arr, n, MEM_HOST)
         return [(arr[i].status, d[:arr[i].out_len].tobytes()) for i, d in enumerate(dsts)]
 
     # -- asynchronous batches (jfsx_*_async + jfsx_wait) ------------------

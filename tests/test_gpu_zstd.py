@@ -1,0 +1,103 @@
+"""GPU Zstandard decompression (jfsx_zstd_decompress_batch, jfsx_zstd.hip)
+against the system zstd library: decoded bytes of frames at several levels,
+with checksums, concatenated / skippable frames, device-resident unaligned
+buffers, and accept/reject of malformed frames as ZSTD_decompress."""
+import numpy as np
+import pytest
+
+from juicefs_amd import engine as E
+from tests import lz4_data, zstd_lib
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = E.Engine(0)
+    yield e
+    e.close()
+
+
+def test_levels_and_checksums(eng):
+    srcs, frames = [], []
+    for kind in lz4_data.KINDS:
+        for n in (0, 1, 100, 4096, 100003, 1 << 20):
+            for level, ck in ((1, False), (3, True), (-3, False), (9, True)):
+                src = lz4_data.sample(kind, n, seed=n + level + 10)
+                srcs.append(src)
+                frames.append(zstd_lib.compress(src, level, ck))
+    got = eng.zstd_decompress(frames, [len(s) for s in srcs])
+    for i, (src, (st, d)) in enumerate(zip(srcs, got)):
+        assert st == E.OK and d == src, i
+
+
+@pytest.mark.parametrize("kind", ["text", "random", "runs"])
+def test_4mib_blocks(eng, kind):
+    srcs = [lz4_data.sample(kind, 4 << 20, seed=s) for s in range(3)]
+    got = eng.zstd_decompress([zstd_lib.compress(s, 1) for s in srcs], [4 << 20] * 3)
+    assert all(st == E.OK and d == s for s, (st, d) in zip(srcs, got))
+
+
+def test_concatenated_skippable_and_edges(eng):
+    a = lz4_data.sample("text", 70000, seed=1)
+    b = lz4_data.sample("runs", 5000, seed=2)
+    fr = zstd_lib.skippable(b"juicefs") + zstd_lib.compress(a) + zstd_lib.skippable(b"", 15) + \
+        zstd_lib.compress(b, 3, True)
+    got = eng.zstd_decompress([fr, b"", fr + b"\x28\xb5", zstd_lib.compress(a)], [len(a) + len(b), 10, 10**6,
+                                                                                  len(a) - 1])
+    assert got[0] == (E.OK, a + b)
+    assert got[1] == (E.OK, b"")
+    assert got[2][0] == E.EFORMAT and got[3][0] == E.EFORMAT
+
+
+def test_device_batch_unaligned(eng):
+    rng = np.random.default_rng(5)
+    n = 24
+    lens = [int(x) for x in rng.integers(0, 300000, n)]
+    srcs = [lz4_data.sample(lz4_data.KINDS[i % 6], lens[i], seed=50 + i) for i in range(n)]
+    frames = [zstd_lib.compress(s, 1 + (i % 3)) for i, s in enumerate(srcs)]
+    inb = eng.alloc(sum(len(f) + 8 for f in frames))
+    outb = eng.alloc(sum(L + 8 for L in lens))
+    specs, io, oo = [], 0, 0
+    for i, f in enumerate(frames):
+        a, c = io + (i % 4), oo + (i % 3)
+        inb.upload(np.frombuffer(f, np.uint8), a)
+        specs.append((inb.ptr + a, len(f), outb.ptr + c, lens[i]))
+        io += len(f) + 8
+        oo += lens[i] + 8
+    arr, m = eng.make_zblocks(specs)
+    eng.zstd_decompress_batch(arr, m, E.MEM_DEVICE)
+    for i in range(n):
+        assert arr[i].status == E.OK and arr[i].out_len == lens[i]
+        assert outb.download(lens[i], specs[i][2] - outb.ptr).tobytes() == srcs[i]
+
+
+def test_malformed_agrees_with_library(eng):
+    rng = np.random.default_rng(3)
+    frames, caps, ref = [], [], []
+    for trial in range(600):
+        kind = lz4_data.KINDS[trial % 6]
+        n = int(rng.choice([50, 700, 5000, 70000]))
+        fr = bytearray(zstd_lib.compress(lz4_data.sample(kind, n, seed=trial), int(rng.choice([1, 3, -1])),
+                                         trial % 3 == 0))
+        m = trial % 3
+        if m == 0 and len(fr) > 1:
+            fr = fr[:int(rng.integers(0, len(fr)))]
+        elif m == 1:
+            i = int(rng.integers(0, len(fr)))
+            fr[i] ^= 1 << int(rng.integers(0, 8))
+        else:
+            fr[int(rng.integers(0, len(fr)))] = int(rng.integers(0, 256))
+        cap = n if rng.random() < 0.8 else int(rng.integers(0, n + 10))
+        frames.append(bytes(fr))
+        caps.append(cap)
+        ref.append(zstd_lib.decompress(bytes(fr), cap))
+    got = eng.zstd_decompress(frames, caps)
+    rejects = 0
+    for (st, d), (rc, r) in zip(got, ref):
+        if rc < 0:
+            rejects += 1
+            assert st == E.EFORMAT
+        else:
+            assert st == E.OK and d == r
+    assert rejects > 200

@@ -1,0 +1,64 @@
+"""The system zstd C library (libzstd.so.1, 1.4.8 here) through ctypes: the
+checker for the engine's Zstandard decoder (test data and reference results
+only; the reference binds github.com/DataDog/zstd v1.5.0, go.mod:10, whose
+vendored C sources are not in /root/reference).  Decoding is defined by the
+format (RFC 8878), so frames from this library decode to the same bytes under
+any conforming decoder; accept/reject of malformed frames is compared with
+this library's ZSTD_decompress."""
+import ctypes
+import ctypes.util
+
+_z = None
+
+
+def lib():
+    global _z
+    if _z is None:
+        z = ctypes.CDLL(ctypes.util.find_library("zstd") or "libzstd.so.1")
+        z.ZSTD_compressBound.restype = ctypes.c_size_t
+        z.ZSTD_decompress.restype = ctypes.c_size_t
+        z.ZSTD_isError.restype = ctypes.c_uint
+        z.ZSTD_createCCtx.restype = ctypes.c_void_p
+        z.ZSTD_compress2.restype = ctypes.c_size_t
+        z.ZSTD_CCtx_setParameter.restype = ctypes.c_size_t
+        z.ZSTD_freeCCtx.argtypes = [ctypes.c_void_p]
+        _z = z
+    return _z
+
+
+def version():
+    return lib().ZSTD_versionNumber()
+
+
+def compress(src, level=1, checksum=False):
+    """ZSTD_compress2 at level (ZSTD_c_compressionLevel = 100) with
+    ZSTD_c_checksumFlag (201); level 1 without checksum is what
+    zstd.CompressLevel(dst, src, 1) of the "zstd" Compressor writes."""
+    z = lib()
+    cap = z.ZSTD_compressBound(len(src))
+    out = ctypes.create_string_buffer(max(cap, 1))
+    cc = ctypes.c_void_p(z.ZSTD_createCCtx())
+    try:
+        z.ZSTD_CCtx_setParameter(cc, 100, int(level))
+        z.ZSTD_CCtx_setParameter(cc, 201, 1 if checksum else 0)
+        r = z.ZSTD_compress2(cc, out, cap, bytes(src), len(src))
+        if z.ZSTD_isError(r):
+            raise RuntimeError("ZSTD_compress2 failed")
+    finally:
+        z.ZSTD_freeCCtx(cc)
+    return out.raw[:r]
+
+
+def decompress(frame, cap):
+    """ZSTD_decompress into cap bytes: (rc, bytes) with rc < 0 on error."""
+    z = lib()
+    out = ctypes.create_string_buffer(max(cap, 1))
+    r = z.ZSTD_decompress(out, cap, bytes(frame), len(frame))
+    if z.ZSTD_isError(r):
+        return -1, b""
+    return r, out.raw[:r]
+
+
+def skippable(payload, nibble=0):
+    """A skippable frame (magic 0x184D2A50 + nibble) carrying payload."""
+    return (0x184D2A50 + nibble).to_bytes(4, "little") + len(payload).to_bytes(4, "little") + bytes(payload)
