@@ -37,7 +37,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--blocks", type=int, default=16384, help="4 MiB blocks per GPU (16384 = 64 GiB)")
     ap.add_argument("--block-bytes", type=int, default=BLOCK)
-    ap.add_argument("--mode", choices=["seal", "open", "crc", "decrypt", "agg", "lz4", "unlz4"], default="seal",
+    ap.add_argument("--mode", choices=["seal", "open", "crc", "decrypt", "agg", "lz4", "unlz4", "unzstd"], default="seal",
                     help="decrypt = dataEncryptor.Decrypt end to end: batched RSA-OAEP key unwrap + Open + CRC verify; "
                          "agg = one-block Seal calls from --threads threads on pinned host blocks, through the "
                          "aggregator (jfsx_agg) and, for comparison, as direct one-block batches")
@@ -197,6 +197,8 @@ def main():
         return agg_bench(args, world, rank, local, dist, eng)
     if args.mode in ("lz4", "unlz4"):
         return lz4_bench(args, world, rank, local, dist, eng)
+    if args.mode == "unzstd":
+        return zstd_bench(args, world, rank, local, dist, eng)
     if args.mem == "host":
         return host_ingest(args, world, rank, local, dist, eng)
     nb, L = args.blocks, args.block_bytes
@@ -719,6 +721,112 @@ def lz4_bench(args, world, rank, local, dist, eng):
                          "frac": round(algo_bytes / (k_avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if k_n else None,
                          "traffic": None, "kernel": "lz4_compress_k" if args.mode == "lz4" else "lz4_decompress_k",
                          "kernel_avg_ms": round(k_avg, 3), "algorithmic_bytes_per_launch": algo_bytes},
+            "cpu_baseline": cpu, "verified_blocks": verified}), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def zstd_cpu_baseline(frames, L):
+    """ZSTD_decompress of the system zstd library (the C library DataDog/zstd
+    binds) over the distinct frames, one thread per core."""
+    import ctypes
+    from concurrent.futures import ThreadPoolExecutor
+    from tests import zstd_lib
+    z = zstd_lib.lib()
+    threads, note = host_cores()
+    outs = [ctypes.create_string_buffer(L) for _ in range(threads)]
+
+    def work(i):
+        f = frames[i % len(frames)]
+        return z.ZSTD_decompress(outs[i % threads], L, f, len(f))
+    reps = max(len(frames), 4 * threads)
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(work, range(threads)))
+        t0 = time.perf_counter()
+        list(ex.map(work, range(reps)))
+        el = time.perf_counter() - t0
+    return {"value": round(reps * L / el / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": "%d x 4 MiB frames (%d distinct), ZSTD_decompress of the system libzstd %d (the C library "
+                      "github.com/DataDog/zstd binds), %d threads (%s)" % (reps, len(frames), zstd_lib.version(),
+                                                                          threads, note)}
+
+
+def zstd_bench(args, world, rank, local, dist, eng):
+    """SURVEY 8f-4 / cachedStore.load's Decompress (cached_store.go:738) for
+    "zstd" volumes: a device-resident batch of level-1 zstd frames of 4 MiB
+    blocks (compressed on the host by the system libzstd: 256 distinct blocks,
+    repeated over the batch) through jfsx_zstd_decompress_batch.  value =
+    decompressed GB/s."""
+    import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
+    from juicefs_amd import engine as E
+    from tests import zstd_lib
+    nb = args.blocks
+    L = args.block_bytes
+    base = rank * nb
+    nd = min(nb, 256)
+    if args.lz4_data == "text":
+        pool = _text_pool(16 << 20, SEED + rank)
+        blocks = [pool[(((base + b) * 2654435761) % (pool.size - L)):][:L].tobytes() for b in range(nd)]
+    else:
+        rng = np.random.default_rng(SEED + rank)
+        blocks = [rng.integers(0, 256, L, dtype=np.uint8).tobytes() for _ in range(nd)]
+    with ThreadPoolExecutor(16) as ex:
+        frames = list(ex.map(lambda b: zstd_lib.compress(b, 1), blocks))
+    fcap = max(len(f) for f in frames)
+    cmp_ = eng.alloc(nb * fcap)
+    for b in range(nb):
+        cmp_.upload(np.frombuffer(frames[b % nd], np.uint8), b * fcap)
+    out = eng.alloc(nb * L)
+    darr, n = eng.make_zblocks((cmp_.ptr + b * fcap, len(frames[b % nd]), out.ptr + b * L, L) for b in range(nb))
+    csum = sum(len(frames[b % nd]) for b in range(nb))
+
+    def step():
+        eng.zstd_decompress_batch(darr, n, E.MEM_DEVICE)
+    for _ in range(args.warmup):
+        step()
+    eng.sync()
+    eng.kernel_time(reset=True)
+    eng.set_timing(True)
+    barrier(dist)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    eng.sync()
+    barrier(dist)
+    el = max_over_ranks(dist, time.perf_counter() - t0, local)
+    eng.set_timing(False)
+    k_ms, k_n = eng.kernel_time(reset=True)
+    k_avg = k_ms / max(k_n, 1)
+    verified = 0
+    if args.verify:
+        for b in range(0, nb, max(1, nb // args.verify))[:args.verify]:
+            if darr[b].status != E.OK or out.download(L, b * L).tobytes() != blocks[b % nd]:
+                raise SystemExit("bench: zstd block %d does not decode" % b)
+            verified += 1
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = zstd_cpu_baseline(frames, L)
+    algo_bytes = nb * L + csum
+    if rank == 0:
+        print(json.dumps({
+            "metric": "zstd decompressed GB/s (uncompressed bytes), 4 MiB blocks",
+            "value": round(world * nb * L * args.steps / el / 1e9, 2), "unit": "GB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (%s), level-1 frames from the system libzstd %d, device-resident" % (
+                "zipf word text, 4 MiB windows of a 16 MiB pool" if args.lz4_data == "text" else "random bytes",
+                zstd_lib.version()),
+            "config": {"workload": "%s GiB device-resident batch of 4 MiB blocks per GPU, zstd decompress" % (
+                round(nb * L / 2**30, 3)), "blocks_per_gpu": nb, "block_bytes": L, "mode": args.mode,
+                "data": args.lz4_data, "ratio": round(csum / (nb * L), 4),
+                "parallelism": "block-sharded x%d, no collective" % world},
+            "roofline": {"bound": "hbm", "achieved": round(algo_bytes / (k_avg / 1e3) / 1e9, 1) if k_n else None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(algo_bytes / (k_avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if k_n else None,
+                         "traffic": None, "kernel": "zstd_decompress_k", "kernel_avg_ms": round(k_avg, 3),
+                         "algorithmic_bytes_per_launch": algo_bytes},
             "cpu_baseline": cpu, "verified_blocks": verified}), flush=True)
     eng.close()
     if dist is not None:

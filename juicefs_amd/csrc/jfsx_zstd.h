@@ -19,7 +19,7 @@
 #include <stddef.h>
 
 #if defined(__HIPCC__)
-#define ZD_HD __host__ __device__
+#define ZD_HD __host__ __device__ __attribute__((always_inline))
 #else
 #define ZD_HD
 #endif
@@ -35,7 +35,20 @@
     } while (0)
 #endif
 
+// Values the whole wave agrees on (table entries read back from LDS, input
+// words): on the device, taken from lane 0 so the decoder's control state
+// stays in SGPRs and its input reads stay scalar.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define ZD_U32(x) ((uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x)))
+#else
+#define ZD_U32(x) ((uint32_t)(x))
+#endif
+
 namespace jzd {
+
+ZD_HD inline uint64_t zd_u64(uint64_t v) {
+    return (uint64_t)ZD_U32(v) | ((uint64_t)ZD_U32(v >> 32) << 32);
+}
 
 enum : int { ZD_OK = 0, ZD_EFORMAT = -1, ZD_EDSTSIZE = -2 };
 
@@ -59,6 +72,7 @@ struct Tables {
     int16_t norm[256];
     uint16_t snext[256];
     uint8_t sym[1u << kLLLog];       // spread symbols
+    uint32_t rank[kHufLogMax + 2];   // Huffman weight counts, then rank starts
 };
 
 // Frame-to-frame state (registers): which tables the repeat modes reuse.
@@ -76,13 +90,15 @@ ZD_HD inline uint32_t highbit(uint32_t v) {  // v > 0
 // ---------------------------------------------------------------------------
 // Bit readers over input bytes (Env::in8 / in64: zeros outside [0, insize))
 // ---------------------------------------------------------------------------
+// (readers keep a copy of the Env, a few pointers: no address of the Env is
+// taken, so on the device it stays in registers)
 template <class Env>
 struct Fwd {  // forward, LSB-first (FSE_readNCount)
-    const Env *e;
-    int64_t base;
-    uint64_t pos;
+    Env e;
+    int32_t base;
+    uint32_t pos;
     ZD_HD uint32_t peek(uint32_t k) const {  // k <= 32; bits past the region read as zeros by the caller's bound
-        const uint64_t v = e->in64(base + (int64_t)(pos >> 3));
+        const uint64_t v = e.in64(base + (int32_t)(pos >> 3));
         return (uint32_t)(v >> (pos & 7)) & (uint32_t)((1ull << k) - 1);
     }
 };
@@ -92,29 +108,29 @@ struct Fwd {  // forward, LSB-first (FSE_readNCount)
 // as zeros, as libzstd's shifted container gives them)
 template <class Env>
 struct Bwd {
-    const Env *e;
-    int64_t base;
-    int64_t rem;
+    Env e;
+    int32_t base;
+    int32_t rem;
     uint64_t cont;  // stream bytes [cb, cb + 8)
-    int64_t cb;
+    int32_t cb;
     ZD_HD void fill() {
-        int64_t top = (rem - 1) >> 3;  // byte of the next bit
+        int32_t top = (rem - 1) >> 3;  // byte of the next bit
         if (top < 7) top = 7;
         cb = top - 7;
-        cont = e->in64(base + cb);
+        cont = zd_u64(e.in64(base + cb));
     }
-    ZD_HD uint64_t peek(uint32_t k) {  // k <= 56
-        const int64_t lo = rem - (int64_t)k;
+    ZD_HD uint32_t peek(uint32_t k) {  // k <= 32
+        const int32_t lo = rem - (int32_t)k;
         if (rem > cb * 8 + 64 || (lo < cb * 8 && cb > 0)) fill();
-        const int64_t sh = lo - cb * 8;
-        if (sh >= 0) return (cont >> sh) & ((1ull << k) - 1);
+        const int32_t sh = lo - cb * 8;
+        if (sh >= 0) return (uint32_t)((cont >> sh) & ((1ull << k) - 1));
         // over-read below byte 0 (cb == 0): the missing low bits are zero
         if (rem <= 0) return 0;
-        return (cont << (uint32_t)(-sh)) & ((1ull << k) - 1);
+        return (uint32_t)((cont << (uint32_t)(-sh)) & ((1ull << k) - 1));
     }
-    ZD_HD uint64_t read(uint32_t k) {
+    ZD_HD uint32_t read(uint32_t k) {
         if (k == 0) return 0;
-        const uint64_t v = peek(k);
+        const uint32_t v = peek(k);
         rem -= k;
         return v;
     }
@@ -123,14 +139,14 @@ struct Bwd {
 // BIT_initDStream: error if n == 0 or the last byte (end marker) is 0.  Bytes
 // of the stream region only: the region must lie inside the input.
 template <class Env>
-ZD_HD bool bwd_init(Bwd<Env> &b, const Env &e, int64_t base, int64_t n) {
+ZD_HD bool bwd_init(Bwd<Env> &b, const Env &e, int32_t base, int32_t n) {
     if (n <= 0) return false;
-    const uint32_t last = e.in8(base + n - 1);
+    const uint32_t last = ZD_U32(e.in8(base + n - 1));
     if (last == 0) return false;
-    b.e = &e;
+    b.e = e;
     b.base = base;
-    b.rem = 8 * (n - 1) + (int64_t)highbit(last);
-    b.cb = 1ll << 40;
+    b.rem = 8 * (n - 1) + (int32_t)highbit(last);
+    b.cb = 1 << 30;
     b.cont = 0;
     b.fill();
     return true;
@@ -141,23 +157,23 @@ ZD_HD bool bwd_init(Bwd<Env> &b, const Env &e, int64_t base, int64_t n) {
 // the bytes used, or -1.  maxsv in: largest allowed symbol; out: last symbol.
 // ---------------------------------------------------------------------------
 template <class Env>
-ZD_HD int64_t read_ncount(const Env &e, int64_t base, int64_t n, int16_t *norm, uint32_t &maxsv, uint32_t &tlog) {
+ZD_HD int32_t read_ncount(const Env &e, int32_t base, int32_t n, int16_t *norm, uint32_t &maxsv, uint32_t &tlog) {
     // headers shorter than 4 bytes are read zero-padded to 4 (libzstd copies
     // them into a 4-byte buffer); bits past the region read as zeros
-    const int64_t nb4 = n < 4 ? 4 : n;
+    const int32_t nb4 = n < 4 ? 4 : n;
     struct Lim {
-        const Env *e;
-        int64_t base, n;
-        ZD_HD uint64_t in64(int64_t i) const {
+        Env e;
+        int32_t base, n;
+        ZD_HD uint64_t in64(int32_t i) const {
             uint64_t v = 0;
             for (int k = 0; k < 8; k++) {
-                const int64_t j = i + k;
-                if (j >= base && j < base + n) v |= (uint64_t)e->in8(j) << (8 * k);
+                const int32_t j = i + k;
+                if (j >= base && j < base + n) v |= (uint64_t)e.in8(j) << (8 * k);
             }
             return v;
         }
-    } lim{&e, base, n};
-    Fwd<Lim> r{&lim, base, 0};
+    };
+    Fwd<Lim> r{Lim{e, base, n}, base, 0};
     for (uint32_t i = 0; i <= maxsv; i++) ZD_ONE(norm[i] = 0);
     uint32_t nbits = r.peek(4) + 5;
     r.pos += 4;
@@ -198,11 +214,11 @@ ZD_HD int64_t read_ncount(const Env &e, int64_t base, int64_t n, int16_t *norm, 
             nbits--;
             threshold >>= 1;
         }
-        if (r.pos > 8ull * (uint64_t)nb4 + 64) return -1;  // libzstd's clamped read fails at the end
+        if (r.pos > 8ull * (uint32_t)nb4 + 64) return -1;  // libzstd's clamped read fails at the end
     }
     if (remaining != 1) return -1;
-    if (r.pos > 8ull * (uint64_t)nb4) return -1;
-    const int64_t used = (int64_t)((r.pos + 7) >> 3);
+    if (r.pos > 8ull * (uint32_t)nb4) return -1;
+    const int32_t used = (int32_t)((r.pos + 7) >> 3);
     if (used > n) return -1;
     maxsv = ch - 1;
     return used;
@@ -215,18 +231,19 @@ ZD_HD inline bool fse_spread(Tables &t, uint32_t maxsv, uint32_t tlog) {
     const uint32_t size = 1u << tlog;
     uint32_t high = size - 1;
     for (uint32_t s = 0; s <= maxsv; s++) {
-        if (t.norm[s] == -1) {
+        const int32_t ns = (int16_t)ZD_U32((uint16_t)t.norm[s]);
+        if (ns == -1) {
             ZD_ONE(t.sym[high] = (uint8_t)s);
             high--;
             ZD_ONE(t.snext[s] = 1);
         } else {
-            ZD_ONE(t.snext[s] = (uint16_t)t.norm[s]);
+            ZD_ONE(t.snext[s] = (uint16_t)ns);
         }
     }
     const uint32_t mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
     uint32_t pos = 0;
     for (uint32_t s = 0; s <= maxsv; s++)
-        for (int32_t i = 0; i < t.norm[s]; i++) {
+        for (int32_t i = 0, ns = (int16_t)ZD_U32((uint16_t)t.norm[s]); i < ns; i++) {
             ZD_ONE(t.sym[pos] = (uint8_t)s);
             pos = (pos + step) & mask;
             while (pos > high) pos = (pos + step) & mask;
@@ -234,21 +251,34 @@ ZD_HD inline bool fse_spread(Tables &t, uint32_t maxsv, uint32_t tlog) {
     return pos == 0;
 }
 
+// a table entry as wave-uniform values
+ZD_HD inline SeqEnt ld_seq(const SeqEnt *p) {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(p);
+    const uint32_t a = ZD_U32(w[0]), b = ZD_U32(w[1]);
+    SeqEnt d;
+    d.base = a;
+    d.next = (uint16_t)(b & 0xffff);
+    d.nbBits = (uint8_t)((b >> 16) & 255);
+    d.addBits = (uint8_t)(b >> 24);
+    return d;
+}
+
 // sequence table from counts (ZSTD_buildFSETable) into dt[1 << tlog]
-ZD_HD inline void build_seq(Tables &t, SeqEnt *dt, uint32_t maxsv, uint32_t tlog, const uint32_t *baseV,
-                            const uint8_t *bitsV) {
+ZD_HD inline uint32_t code_base(uint32_t kind, uint32_t s);
+ZD_HD inline uint32_t code_bits(uint32_t kind, uint32_t s);
+ZD_HD inline void build_seq(Tables &t, SeqEnt *dt, uint32_t maxsv, uint32_t tlog, uint32_t kind) {
     fse_spread(t, maxsv, tlog);
     const uint32_t size = 1u << tlog;
     for (uint32_t u = 0; u < size; u++) {
-        const uint32_t s = t.sym[u];
-        const uint32_t nx = t.snext[s];
+        const uint32_t s = ZD_U32(t.sym[u]);
+        const uint32_t nx = ZD_U32(t.snext[s]);
         ZD_ONE(t.snext[s] = (uint16_t)(nx + 1));
         const uint32_t nb = tlog - highbit(nx);
         SeqEnt d;
         d.nbBits = (uint8_t)nb;
         d.next = (uint16_t)((nx << nb) - size);
-        d.addBits = bitsV[s];
-        d.base = baseV[s];
+        d.addBits = (uint8_t)code_bits(kind, s);
+        d.base = code_base(kind, s);
         ZD_ONE(dt[u] = d);
     }
 }
@@ -256,40 +286,26 @@ ZD_HD inline void build_seq(Tables &t, SeqEnt *dt, uint32_t maxsv, uint32_t tlog
 // ---------------------------------------------------------------------------
 // Sequence code tables (RFC 8878 3.1.1.3.2.1.1) and predefined distributions
 // ---------------------------------------------------------------------------
-ZD_HD inline uint32_t ll_base(uint32_t c) {
-    const uint32_t b[36] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10,  11,  12,  13,   14,   15,   16,    18,
-                            20, 22, 24, 28, 32, 40, 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
-    return b[c];
-}
-ZD_HD inline uint8_t ll_bits(uint32_t c) {
-    const uint8_t b[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
-    return b[c];
-}
-ZD_HD inline uint32_t ml_base(uint32_t c) {
-    const uint32_t b[53] = {3,  4,  5,  6,  7,  8,  9,  10, 11, 12,  13,  14,  15,  16,   17,   18,   19,   20,
-                            21, 22, 23, 24, 25, 26, 27, 28, 29, 30,  31,  32,  33,  34,   35,   37,   39,   41,
-                            43, 47, 51, 59, 67, 83, 99, 131, 259, 515, 1027, 2051, 4099, 8195, 16387, 32771, 65539};
-    return b[c];
-}
-ZD_HD inline uint8_t ml_bits(uint32_t c) {
-    const uint8_t b[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
-                           0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
-    return b[c];
-}
-// offset codes: base = 1 << c, bits = c (offset value, before the repeat rules)
-ZD_HD inline int16_t ll_def(uint32_t s) {
-    const int16_t d[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
-    return d[s];
-}
-ZD_HD inline int16_t ml_def(uint32_t s) {
-    const int16_t d[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
-                           1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
-    return d[s];
-}
-ZD_HD inline int16_t of_def(uint32_t s) {
-    const int16_t d[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
-    return d[s];
-}
+constexpr uint32_t kLLBase[36] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,   10,  11,  12,   13,   14,   15,    16,    18,
+                                   20, 22, 24, 28, 32, 40, 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
+constexpr uint8_t kLLBits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1,
+                                 1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+constexpr uint32_t kMLBase[53] = {3,  4,  5,  6,  7,  8,  9,  10, 11, 12,  13,  14,  15,   16,   17,   18,   19,    20,
+                                  21, 22, 23, 24, 25, 26, 27, 28, 29, 30,  31,  32,  33,   34,   35,   37,   39,    41,
+                                  43, 47, 51, 59, 67, 83, 99, 131, 259, 515, 1027, 2051, 4099, 8195, 16387, 32771, 65539};
+constexpr uint8_t kMLBits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+// predefined distributions (RFC 8878 3.1.1.3.2.2)
+constexpr int16_t kLLDef[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
+                                2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
+constexpr int16_t kMLDef[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+constexpr int16_t kOFDef[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+
+// code -> (base, extra bits); offset codes: base 1 << c, c bits (the offset
+// value before the repeat rules)
+ZD_HD inline uint32_t code_base(uint32_t kind, uint32_t s);
+ZD_HD inline uint32_t code_bits(uint32_t kind, uint32_t s);
 
 enum Kind : uint32_t { KLL = 0, KML = 1, KOF = 2 };
 
@@ -298,30 +314,26 @@ ZD_HD inline void kind_params(uint32_t kind, uint32_t &maxsv, uint32_t &maxlog) 
     maxlog = kind == KLL ? kLLLog : kind == KML ? kMLLog : kOffLog;
 }
 
-ZD_HD inline void fill_codes(uint32_t kind, uint32_t *baseV, uint8_t *bitsV) {
-    const uint32_t n = kind == KLL ? 36 : kind == KML ? 53 : 32;
-    for (uint32_t s = 0; s < n; s++) {
-        baseV[s] = kind == KLL ? ll_base(s) : kind == KML ? ml_base(s) : (1u << s);
-        bitsV[s] = kind == KLL ? ll_bits(s) : kind == KML ? ml_bits(s) : (uint8_t)s;
-    }
+ZD_HD inline uint32_t code_base(uint32_t kind, uint32_t s) {
+    return kind == KLL ? kLLBase[s] : kind == KML ? kMLBase[s] : (1u << s);
+}
+ZD_HD inline uint32_t code_bits(uint32_t kind, uint32_t s) {
+    return kind == KLL ? kLLBits[s] : kind == KML ? kMLBits[s] : s;
 }
 
 // ZSTD_buildSeqTable for one of LL / ML / OF; returns bytes used or -1
 template <class Env>
-ZD_HD int64_t seq_table(const Env &e, Tables &t, Mode &m, uint32_t kind, uint32_t type, int64_t p, int64_t end) {
+ZD_HD int32_t seq_table(const Env &e, Tables &t, Mode &m, uint32_t kind, uint32_t type, int32_t p, int32_t end) {
     uint32_t maxsv, maxlog;
     kind_params(kind, maxsv, maxlog);
     SeqEnt *dt = kind == KLL ? t.ll : kind == KML ? t.ml : t.of;
     uint32_t &logr = kind == KLL ? m.llLog : kind == KML ? m.mlLog : m.ofLog;
-    uint32_t baseV[53];
-    uint8_t bitsV[53];
-    fill_codes(kind, baseV, bitsV);
     if (type == 0) {  // predefined
         const uint32_t n = kind == KLL ? 36 : kind == KML ? 53 : 29;
         for (uint32_t s = 0; s < n; s++)
-            ZD_ONE(t.norm[s] = kind == KLL ? ll_def(s) : kind == KML ? ml_def(s) : of_def(s));
+            ZD_ONE(t.norm[s] = kind == KLL ? kLLDef[s] : kind == KML ? kMLDef[s] : kOFDef[s]);
         const uint32_t lg = kind == KOF ? 5 : 6;
-        build_seq(t, dt, n - 1, lg, baseV, bitsV);
+        build_seq(t, dt, n - 1, lg, kind);
         logr = lg;
         return 0;
     }
@@ -330,8 +342,8 @@ ZD_HD int64_t seq_table(const Env &e, Tables &t, Mode &m, uint32_t kind, uint32_
         const uint32_t s = e.in8(p);
         if (s > maxsv) return -1;
         SeqEnt d;
-        d.base = baseV[s];
-        d.addBits = bitsV[s];
+        d.base = code_base(kind, s);
+        d.addBits = (uint8_t)code_bits(kind, s);
         d.nbBits = 0;
         d.next = 0;
         ZD_ONE(dt[0] = d);
@@ -343,9 +355,9 @@ ZD_HD int64_t seq_table(const Env &e, Tables &t, Mode &m, uint32_t kind, uint32_
         return 0;
     }
     uint32_t mx = maxsv, tlog;
-    const int64_t hs = read_ncount(e, p, end - p, t.norm, mx, tlog);
+    const int32_t hs = read_ncount(e, p, end - p, t.norm, mx, tlog);
     if (hs < 0 || tlog > maxlog) return -1;
-    build_seq(t, dt, mx, tlog, baseV, bitsV);
+    build_seq(t, dt, mx, tlog, kind);
     logr = tlog;
     return hs;
 }
@@ -354,10 +366,10 @@ ZD_HD int64_t seq_table(const Env &e, Tables &t, Mode &m, uint32_t kind, uint32_
 // Huffman weights and table (HUF_readStats + HUF_readDTableX1)
 // ---------------------------------------------------------------------------
 template <class Env>
-ZD_HD int64_t huf_table(const Env &e, Tables &t, int64_t p, int64_t n, uint32_t &hlog) {
+ZD_HD int32_t huf_table(const Env &e, Tables &t, int32_t p, int32_t n, uint32_t &hlog) {
     if (n <= 0) return -1;
     uint32_t hb = e.in8(p), nw;
-    int64_t isize;
+    int32_t isize;
     if (hb >= 128) {  // direct 4-bit weights
         nw = hb - 127;
         isize = (nw + 1) / 2;
@@ -370,15 +382,15 @@ ZD_HD int64_t huf_table(const Env &e, Tables &t, int64_t p, int64_t n, uint32_t 
     } else {  // FSE-compressed weights (accuracy <= 6), two interleaved states
         isize = hb;
         if (isize + 1 > n) return -1;
-        const int64_t q = p + 1;
+        const int32_t q = p + 1;
         uint32_t mx = 255, tlog;
-        const int64_t hs = read_ncount(e, q, isize, t.norm, mx, tlog);
+        const int32_t hs = read_ncount(e, q, isize, t.norm, mx, tlog);
         if (hs < 0 || tlog > 6) return -1;
         if (!fse_spread(t, mx, tlog)) return -1;
         const uint32_t size = 1u << tlog;
         for (uint32_t u = 0; u < size; u++) {
-            const uint32_t s = t.sym[u];
-            const uint32_t nx = t.snext[s];
+            const uint32_t s = ZD_U32(t.sym[u]);
+            const uint32_t nx = ZD_U32(t.snext[s]);
             ZD_ONE(t.snext[s] = (uint16_t)(nx + 1));
             const uint32_t nb = tlog - highbit(nx);
             ZD_ONE(t.fw[u] = s | (nb << 8) | (((nx << nb) - size) << 16));
@@ -390,22 +402,22 @@ ZD_HD int64_t huf_table(const Env &e, Tables &t, int64_t p, int64_t n, uint32_t 
         const uint32_t omax = 255;  // FSE_decompress_wksp(.., hwSize - 1 = 255, ..)
         for (;;) {
             if (o > omax - 2) return -1;
-            uint32_t f = t.fw[s1];
+            uint32_t f = ZD_U32(t.fw[s1]);
             ZD_ONE(t.w[o] = (uint8_t)(f & 255));
             o++;
             s1 = (f >> 16) + (uint32_t)b.read((f >> 8) & 255);
             if (b.rem < 0) {
-                ZD_ONE(t.w[o] = (uint8_t)(t.fw[s2] & 255));
+                ZD_ONE(t.w[o] = (uint8_t)(ZD_U32(t.fw[s2]) & 255));
                 o++;
                 break;
             }
             if (o > omax - 2) return -1;
-            f = t.fw[s2];
+            f = ZD_U32(t.fw[s2]);
             ZD_ONE(t.w[o] = (uint8_t)(f & 255));
             o++;
             s2 = (f >> 16) + (uint32_t)b.read((f >> 8) & 255);
             if (b.rem < 0) {
-                ZD_ONE(t.w[o] = (uint8_t)(t.fw[s1] & 255));
+                ZD_ONE(t.w[o] = (uint8_t)(ZD_U32(t.fw[s1]) & 255));
                 o++;
                 break;
             }
@@ -413,13 +425,14 @@ ZD_HD int64_t huf_table(const Env &e, Tables &t, int64_t p, int64_t n, uint32_t 
         nw = o;
     }
     // weight statistics, implied last weight
-    uint32_t rank[kHufLogMax + 1];
-    for (uint32_t k = 0; k <= kHufLogMax; k++) rank[k] = 0;
+    uint32_t *rank = t.rank;
+    for (uint32_t k = 0; k <= kHufLogMax + 1; k++) ZD_ONE(rank[k] = 0);
     uint32_t total = 0;
     for (uint32_t k = 0; k < nw; k++) {
-        const uint32_t wk = t.w[k];
+        const uint32_t wk = ZD_U32(t.w[k]);
         if (wk >= kHufLogMax) return -1;
-        rank[wk]++;
+        const uint32_t rk = ZD_U32(rank[wk]);
+        ZD_ONE(rank[wk] = rk + 1);
         total += (1u << wk) >> 1;
     }
     if (total == 0) return -1;
@@ -429,23 +442,29 @@ ZD_HD int64_t huf_table(const Env &e, Tables &t, int64_t p, int64_t n, uint32_t 
     if ((1u << highbit(rest)) != rest) return -1;
     const uint32_t lastw = highbit(rest) + 1;
     ZD_ONE(t.w[nw] = (uint8_t)lastw);
-    rank[lastw]++;
-    if (rank[1] < 2 || (rank[1] & 1)) return -1;
+    {
+        const uint32_t rk = ZD_U32(rank[lastw]);
+        ZD_ONE(rank[lastw] = rk + 1);
+    }
+    const uint32_t r1 = ZD_U32(rank[1]);
+    if (r1 < 2 || (r1 & 1)) return -1;
     const uint32_t nsym = nw + 1;
     // X1 table: symbols in order, each weight's range starting at rankStart[w]
-    uint32_t start[kHufLogMax + 2];
+    // (rank[] turned into the starts in place)
     uint32_t next = 0;
     for (uint32_t wv = 1; wv <= tl; wv++) {
-        start[wv] = next;
-        next += rank[wv] << (wv - 1);
+        const uint32_t cur = next;
+        next += ZD_U32(rank[wv]) << (wv - 1);
+        ZD_ONE(rank[wv] = cur);
     }
     for (uint32_t s = 0; s < nsym; s++) {
-        const uint32_t wv = t.w[s];
+        const uint32_t wv = ZD_U32(t.w[s]);
         if (!wv) continue;
         const uint32_t len = (1u << wv) >> 1;
         const uint16_t ent = (uint16_t)(s | ((tl + 1 - wv) << 8));
-        for (uint32_t k = 0; k < len; k++) ZD_ONE(t.huf[start[wv] + k] = ent);
-        start[wv] += len;
+        const uint32_t st = ZD_U32(rank[wv]);
+        e.huf_fill(t.huf + st, ent, len);
+        ZD_ONE(rank[wv] = st + len);
     }
     hlog = tl;
     return isize + 1;
@@ -453,11 +472,11 @@ ZD_HD int64_t huf_table(const Env &e, Tables &t, int64_t p, int64_t n, uint32_t 
 
 // one Huffman stream [p, p + n) into the literal buffer [o, o + cnt)
 template <class Env>
-ZD_HD bool huf_stream(const Env &e, Tables &t, uint32_t hlog, int64_t p, int64_t n, uint32_t o, uint32_t cnt) {
+ZD_HD bool huf_stream(const Env &e, Tables &t, uint32_t hlog, int32_t p, int32_t n, uint32_t o, uint32_t cnt) {
     Bwd<Env> b;
     if (!bwd_init(b, e, p, n)) return false;
     for (uint32_t k = 0; k < cnt; k++) {
-        const uint32_t ent = t.huf[b.peek(hlog)];
+        const uint32_t ent = ZD_U32(t.huf[b.peek(hlog)]);
         b.rem -= ent >> 8;
         e.lit_put(o + k, ent & 255);
     }
@@ -470,17 +489,18 @@ ZD_HD bool huf_stream(const Env &e, Tables &t, uint32_t hlog, int64_t p, int64_t
 // written or an error (< 0).
 // ---------------------------------------------------------------------------
 template <class Env>
-ZD_HD int64_t block(Env &e, Tables &t, Mode &m, int64_t p, int64_t n, uint64_t fo, uint64_t op, uint64_t cap) {
-    if (n >= (int64_t)kBlockMax) return ZD_EFORMAT;
+ZD_HD int32_t block(Env &e, Tables &t, Mode &m, int32_t p, int32_t n, uint32_t fo, uint32_t op, uint32_t cap) {
+    if (n >= (int32_t)kBlockMax) return ZD_EFORMAT;
     if (n < 3) return ZD_EFORMAT;  // MIN_CBLOCK_SIZE
-    const int64_t end = p + n;
+    const int32_t end = p + n;
     // ---- literals section ----
+    e.stamp(4);
     const uint32_t h0 = e.in8(p);
     const uint32_t ltype = h0 & 3, sf = (h0 >> 2) & 3;
     uint32_t litSize;
-    int64_t lused;
+    int32_t lused;
     bool litInInput = false;  // raw literals read straight from the input
-    int64_t litSrc = 0;
+    int32_t litSrc = 0;
     if (ltype == 0 || ltype == 1) {
         uint32_t lh;
         if (sf == 0 || sf == 2) {
@@ -494,7 +514,7 @@ ZD_HD int64_t block(Env &e, Tables &t, Mode &m, int64_t p, int64_t n, uint64_t f
             litSize = (h0 | (e.in8(p + 1) << 8) | (e.in8(p + 2) << 16)) >> 4;
         }
         if (ltype == 0) {
-            if ((int64_t)lh + litSize > n) return ZD_EFORMAT;
+            if (lh + litSize > (uint32_t)n) return ZD_EFORMAT;
             litInInput = true;
             litSrc = p + lh;
             lused = lh + litSize;
@@ -526,11 +546,11 @@ ZD_HD int64_t block(Env &e, Tables &t, Mode &m, int64_t p, int64_t n, uint64_t f
             litC = (lhc >> 22) + ((uint32_t)e.in8(p + 4) << 10);
         }
         if (litSize > kBlockMax) return ZD_EFORMAT;
-        if ((int64_t)litC + lh > n) return ZD_EFORMAT;
-        int64_t q = p + lh, qn = litC;
+        if (litC + lh > (uint32_t)n) return ZD_EFORMAT;
+        int32_t q = p + lh, qn = litC;
         if (ltype == 2) {
             uint32_t hl;
-            const int64_t hs = huf_table(e, t, q, qn, hl);
+            const int32_t hs = huf_table(e, t, q, qn, hl);
             if (hs < 0) return ZD_EFORMAT;
             if (hs >= qn) return ZD_EFORMAT;
             m.hufLog = hl;
@@ -542,9 +562,9 @@ ZD_HD int64_t block(Env &e, Tables &t, Mode &m, int64_t p, int64_t n, uint64_t f
         } else {
             if (litSize == 0) return ZD_EFORMAT;
             if (qn < 10) return ZD_EFORMAT;
-            const int64_t l1 = e.in8(q) | (e.in8(q + 1) << 8), l2 = e.in8(q + 2) | (e.in8(q + 3) << 8),
+            const int32_t l1 = e.in8(q) | (e.in8(q + 1) << 8), l2 = e.in8(q + 2) | (e.in8(q + 3) << 8),
                           l3 = e.in8(q + 4) | (e.in8(q + 5) << 8);
-            const int64_t l4 = qn - (l1 + l2 + l3 + 6);
+            const int32_t l4 = qn - (l1 + l2 + l3 + 6);
             if (l4 < 0) return ZD_EFORMAT;
             const uint32_t seg = (litSize + 3) / 4;
             if (3 * seg > litSize) {
@@ -552,7 +572,7 @@ ZD_HD int64_t block(Env &e, Tables &t, Mode &m, int64_t p, int64_t n, uint64_t f
                 // the first streams into its spare buffer room
                 return ZD_EFORMAT;
             }
-            const int64_t s1 = q + 6, s2 = s1 + l1, s3 = s2 + l2, s4 = s3 + l3;
+            const int32_t s1 = q + 6, s2 = s1 + l1, s3 = s2 + l2, s4 = s3 + l3;
             if (!huf_stream(e, t, m.hufLog, s1, l1, 0, seg)) return ZD_EFORMAT;
             if (!huf_stream(e, t, m.hufLog, s2, l2, seg, seg)) return ZD_EFORMAT;
             if (!huf_stream(e, t, m.hufLog, s3, l3, 2 * seg, seg)) return ZD_EFORMAT;
@@ -561,8 +581,9 @@ ZD_HD int64_t block(Env &e, Tables &t, Mode &m, int64_t p, int64_t n, uint64_t f
         lused = lh + litC;
     }
     e.lit_sync();
+    e.stamp(0);  // literals
     // ---- sequences section ----
-    int64_t s = p + lused;
+    int32_t s = p + lused;
     if (s >= end) return ZD_EFORMAT;  // MIN_SEQUENCES_SIZE
     uint32_t nbSeq = e.in8(s++);
     if (nbSeq == 0) {
@@ -581,7 +602,7 @@ ZD_HD int64_t block(Env &e, Tables &t, Mode &m, int64_t p, int64_t n, uint64_t f
         }
         if (s + 1 > end) return ZD_EFORMAT;
         const uint32_t modes = e.in8(s++);
-        int64_t u;
+        int32_t u;
         if ((u = seq_table(e, t, m, KLL, modes >> 6, s, end)) < 0) return ZD_EFORMAT;
         s += u;
         if ((u = seq_table(e, t, m, KOF, (modes >> 4) & 3, s, end)) < 0) return ZD_EFORMAT;
@@ -590,7 +611,8 @@ ZD_HD int64_t block(Env &e, Tables &t, Mode &m, int64_t p, int64_t n, uint64_t f
         s += u;
     }
     // ---- execute ----
-    uint64_t o = op, lp = 0;  // output, literal read position
+    e.stamp(1);  // sequence headers and tables
+    uint32_t o = op, lp = 0;  // output, literal read position
     if (nbSeq) {
         m.seqEntropy = true;
         Bwd<Env> b;
@@ -598,12 +620,12 @@ ZD_HD int64_t block(Env &e, Tables &t, Mode &m, int64_t p, int64_t n, uint64_t f
         uint32_t sl = (uint32_t)b.read(m.llLog), so = (uint32_t)b.read(m.ofLog), sm = (uint32_t)b.read(m.mlLog);
         for (uint32_t k = 0; k < nbSeq; k++) {
             if (b.rem < 0) return ZD_EFORMAT;  // BIT_reloadDStream overflow before a sequence
-            const SeqEnt dl = t.ll[sl], dm = t.ml[sm], dof = t.of[so];
+            const SeqEnt dl = ld_seq(t.ll + sl), dm = ld_seq(t.ml + sm), dof = ld_seq(t.of + so);
             // offset
-            uint64_t off;
+            uint32_t off;
             const uint32_t ofc = dof.addBits;
             const uint32_t ll0 = dl.base == 0 && dl.addBits == 0 ? 1u : 0u;
-            uint64_t ml, ll;
+            uint32_t ml, ll;
             {
                 if (ofc > 1) {
                     off = dof.base + b.read(ofc) - 3;
@@ -620,7 +642,7 @@ ZD_HD int64_t block(Env &e, Tables &t, Mode &m, int64_t p, int64_t n, uint64_t f
                     }
                 } else {
                     const uint32_t idx = 1 + ll0 + (uint32_t)b.read(1);
-                    uint64_t tmp = idx == 3 ? (uint64_t)m.rep[0] - 1 : (uint64_t)m.rep[idx];
+                    uint32_t tmp = idx == 3 ? m.rep[0] - 1 : idx == 2 ? m.rep[2] : m.rep[1];
                     tmp += !tmp;
                     if (idx != 1) m.rep[2] = m.rep[1];
                     m.rep[1] = m.rep[0];
@@ -634,12 +656,13 @@ ZD_HD int64_t block(Env &e, Tables &t, Mode &m, int64_t p, int64_t n, uint64_t f
             sl = dl.next + (uint32_t)b.read(dl.nbBits);
             sm = dm.next + (uint32_t)b.read(dm.nbBits);
             so = dof.next + (uint32_t)b.read(dof.nbBits);
+            e.stamp(2);  // sequence decode
             // ZSTD_execSequence
             if (ll + ml > cap - o) return ZD_EDSTSIZE;
-            const uint64_t litAvail = litSize - lp;
+            const uint32_t litAvail = litSize - lp;
             if (ll > litAvail) return ZD_EFORMAT;
             if (litInInput)
-                e.out_from_in(fo + o, litSrc + (int64_t)lp, ll);
+                e.out_from_in(fo + o, litSrc + (int32_t)lp, ll);
             else
                 e.out_from_lit(fo + o, lp, ll);
             o += ll;
@@ -647,18 +670,19 @@ ZD_HD int64_t block(Env &e, Tables &t, Mode &m, int64_t p, int64_t n, uint64_t f
             if (off > o) return ZD_EFORMAT;
             e.out_match(fo + o, off, ml);
             o += ml;
+            e.stamp(3);  // sequence execution
         }
         if (b.rem > 0) return ZD_EFORMAT;  // not all bits consumed
     }
     // last literals
-    const uint64_t last = litSize - lp;
+    const uint32_t last = litSize - lp;
     if (last > cap - o) return ZD_EDSTSIZE;
     if (litInInput)
-        e.out_from_in(fo + o, litSrc + (int64_t)lp, last);
+        e.out_from_in(fo + o, litSrc + (int32_t)lp, last);
     else
         e.out_from_lit(fo + o, lp, last);
     o += last;
-    return (int64_t)(o - op);
+    return (int32_t)(o - op);
 }
 
 // ---------------------------------------------------------------------------
@@ -678,8 +702,9 @@ ZD_HD inline uint64_t xmerge(uint64_t acc, uint64_t v) {
     return acc * P1 + P4;
 }
 template <class Env>
-ZD_HD uint64_t xxh64(const Env &e, uint64_t fo, uint64_t len) {
-    uint64_t h, i = 0;
+ZD_HD uint64_t xxh64(const Env &e, uint32_t fo, uint32_t len) {
+    uint64_t h;
+    uint32_t i = 0;
     if (len >= 32) {
         uint64_t v1 = P1 + P2, v2 = P2, v3 = 0, v4 = 0 - P1;
         for (; i + 32 <= len; i += 32) {
@@ -723,34 +748,34 @@ ZD_HD uint64_t xxh64(const Env &e, uint64_t fo, uint64_t len) {
 // Returns the decoded size, or ZD_EFORMAT / ZD_EDSTSIZE.
 // ---------------------------------------------------------------------------
 template <class Env>
-ZD_HD int64_t decompress(Env &e, Tables &t, uint64_t insize, uint64_t cap) {
-    int64_t p = 0;
-    const int64_t n = (int64_t)insize;
-    uint64_t out = 0;
+ZD_HD int32_t decompress(Env &e, Tables &t, uint32_t insize, uint32_t cap) {
+    int32_t p = 0;
+    const int32_t n = (int32_t)insize;
+    uint32_t out = 0;
     while (n - p >= 5) {
         const uint32_t magic = e.in8(p) | (e.in8(p + 1) << 8) | (e.in8(p + 2) << 16) | ((uint32_t)e.in8(p + 3) << 24);
         if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {  // skippable frame
             if (n - p < 8) return ZD_EFORMAT;
             const uint64_t sz = e.in8(p + 4) | (e.in8(p + 5) << 8) | (e.in8(p + 6) << 16) | ((uint64_t)e.in8(p + 7) << 24);
             if (sz + 8 > (uint64_t)(n - p)) return ZD_EFORMAT;
-            p += 8 + (int64_t)sz;
+            p += 8 + (int32_t)sz;
             continue;
         }
         if (magic != 0xFD2FB528u) return ZD_EFORMAT;
         if (n - p < 9) return ZD_EFORMAT;  // ZSTD_FRAMEHEADERSIZE_MIN + block header
         const uint32_t fhd = e.in8(p + 4);
         const uint32_t dictCode = fhd & 3, checksum = (fhd >> 2) & 1, single = (fhd >> 5) & 1, fcsId = fhd >> 6;
-        const int64_t hsize = 5 + (single ? 0 : 1) + (dictCode == 3 ? 4 : dictCode) +
+        const int32_t hsize = 5 + (single ? 0 : 1) + (dictCode == 3 ? 4 : dictCode) +
                               (fcsId == 0 ? (single ? 1 : 0) : fcsId == 1 ? 2 : fcsId == 2 ? 4 : 8);
         if (n - p < hsize + 3) return ZD_EFORMAT;
         if (fhd & 0x08) return ZD_EFORMAT;
-        int64_t q = p + 5;
+        int32_t q = p + 5;
         if (!single) {
             const uint32_t wl = e.in8(q++);
             if ((wl >> 3) + 10 > 31) return ZD_EFORMAT;
         }
-        uint64_t dict = 0;
-        for (uint32_t k = 0, dn = dictCode == 3 ? 4 : dictCode; k < dn; k++) dict |= (uint64_t)e.in8(q++) << (8 * k);
+        uint32_t dict = 0;
+        for (uint32_t k = 0, dn = dictCode == 3 ? 4 : dictCode; k < dn; k++) dict |= e.in8(q++) << (8 * k);
         if (dict) return ZD_EFORMAT;  // no dictionary loaded
         bool hasFcs = true;
         uint64_t fcs = 0;
@@ -770,17 +795,17 @@ ZD_HD int64_t decompress(Env &e, Tables &t, uint64_t insize, uint64_t cap) {
         m.rep[0] = 1;
         m.rep[1] = 4;
         m.rep[2] = 8;
-        const uint64_t fo = out;
-        uint64_t op = 0;
+        const uint32_t fo = out;
+        uint32_t op = 0;
         for (;;) {
             if (n - q < 3) return ZD_EFORMAT;
             const uint32_t bh = e.in8(q) | (e.in8(q + 1) << 8) | (e.in8(q + 2) << 16);
             q += 3;
             const uint32_t lastb = bh & 1, btype = (bh >> 1) & 3, bsize = bh >> 3;
-            const int64_t csize = btype == 1 ? 1 : (int64_t)bsize;
+            const int32_t csize = btype == 1 ? 1 : (int32_t)bsize;
             if (btype == 3) return ZD_EFORMAT;
             if (csize > n - q) return ZD_EFORMAT;
-            int64_t got;
+            int32_t got;
             if (btype == 0) {
                 if (bsize > cap - out - op) return ZD_EDSTSIZE;
                 e.out_from_in(fo + op, q, bsize);
@@ -794,11 +819,11 @@ ZD_HD int64_t decompress(Env &e, Tables &t, uint64_t insize, uint64_t cap) {
                 if (got < 0) return got;
             }
             e.out_sync();
-            op += (uint64_t)got;
+            op += (uint32_t)got;
             q += csize;
             if (lastb) break;
         }
-        if (hasFcs && op != fcs) return ZD_EFORMAT;
+        if (hasFcs && (uint64_t)op != fcs) return ZD_EFORMAT;
         if (checksum) {
             if (n - q < 4) return ZD_EFORMAT;
             const uint32_t want = e.in8(q) | (e.in8(q + 1) << 8) | (e.in8(q + 2) << 16) | ((uint32_t)e.in8(q + 3) << 24);
@@ -809,7 +834,7 @@ ZD_HD int64_t decompress(Env &e, Tables &t, uint64_t insize, uint64_t cap) {
         p = q;
     }
     if (p != n) return ZD_EFORMAT;
-    return (int64_t)out;
+    return (int32_t)out;
 }
 
 }  // namespace jzd

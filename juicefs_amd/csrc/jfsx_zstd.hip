@@ -30,26 +30,40 @@ struct DevEnv {
     uint8_t *dst;        // output (frame positions are offsets from dst)
     uint8_t *lit;        // literal scratch (jzd::kBlockMax + 64 bytes)
     uint32_t lane;
+    uint64_t fenced;     // output below this is visible to the wave's loads
+#ifdef JFSX_ZSTD_STAMP
+    unsigned long long st[5], last;
+    __device__ __forceinline__ void stamp(int k) {
+        unsigned long long t;
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+        st[k] += t - last;
+        last = t;
+    }
+#else
+    __device__ __forceinline__ void stamp(int) {}
+#endif
 
     // input dword d (bytes [4d - sh, 4d - sh + 4) of src, src = al + sh), zero
     // when it holds no input byte; scalar load (uniform address)
-    __device__ uint32_t dw(int64_t d) const {
+    __device__ __forceinline__ uint32_t dw(int64_t d) const {
         const uintptr_t al = (uintptr_t)src & ~(uintptr_t)3;
         const int64_t sh = (int64_t)((uintptr_t)src & 3);
         const int64_t b0 = 4 * d - sh;  // first src byte of the dword
         if (b0 + 3 < 0 || b0 >= n) return 0u;
-        uint32_t v = *(ccu32 *)(al + 4 * d);
+        uint32_t v = ZD_U32(*(ccu32 *)(al + 4 * d));
         // bytes outside [0, n) read as zero
         if (b0 < 0) v &= 0xffffffffu << (8 * (uint32_t)(-b0));
         if (b0 + 4 > n) v &= 0xffffffffu >> (8 * (uint32_t)(b0 + 4 - n));
         return v;
     }
-    __device__ uint32_t in8(int64_t i) const {
+    __device__ __forceinline__ uint32_t in8(int64_t i) const {
         if (i < 0 || i >= n) return 0;
         const int64_t x = i + (int64_t)((uintptr_t)src & 3);
         return (dw(x >> 2) >> (8 * (uint32_t)(x & 3))) & 255u;
     }
-    __device__ uint64_t in64(int64_t i) const {
+    __device__ __forceinline__ uint64_t in64(int64_t i) const {
         const int64_t x = i + (int64_t)((uintptr_t)src & 3);
         const int64_t d = x >> 2;  // floor (x may be negative)
         const uint32_t s = (uint32_t)(x & 3);
@@ -58,31 +72,39 @@ struct DevEnv {
         const uint64_t hi = dw(d + 2);
         return (lo >> (8 * s)) | (hi << (64 - 8 * s));
     }
-    __device__ void lit_put(uint64_t i, uint32_t b) const {
+    __device__ __forceinline__ void lit_put(uint64_t i, uint32_t b) const {
         if (lane == 0) *(gu8z *)(lit + i) = (uint8_t)b;
     }
-    __device__ void lit_fill(uint64_t i, uint32_t b, uint64_t cnt) const {
+    __device__ __forceinline__ void lit_fill(uint64_t i, uint32_t b, uint64_t cnt) const {
         for (uint64_t j = lane; j < cnt; j += 64) *(gu8z *)(lit + i + j) = (uint8_t)b;
     }
-    __device__ void fence() const {
+    __device__ __forceinline__ void fence() const {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
-    __device__ void lit_sync() const { fence(); }
-    __device__ void out_sync() const { fence(); }
-    __device__ void out_from_in(uint64_t o, int64_t i, uint64_t cnt) const {
+    __device__ __forceinline__ void lit_sync() const { fence(); }
+    __device__ __forceinline__ void huf_fill(uint16_t *p, uint16_t v, uint32_t cnt) const {
+        for (uint32_t j = lane; j < cnt; j += 64) p[j] = v;
+    }
+    __device__ __forceinline__ void out_sync() const { fence(); }
+    __device__ __forceinline__ void out_from_in(uint64_t o, int64_t i, uint64_t cnt) const {
         for (uint64_t j = lane; j < cnt; j += 64) *(gu8z *)(dst + o + j) = (uint8_t)in8_v(i + (int64_t)j);
     }
     // per-lane input byte (vector load)
-    __device__ uint32_t in8_v(int64_t i) const { return *(gcu8z *)(src + i); }
-    __device__ void out_from_lit(uint64_t o, uint64_t i, uint64_t cnt) const {
+    __device__ __forceinline__ uint32_t in8_v(int64_t i) const { return *(gcu8z *)(src + i); }
+    __device__ __forceinline__ void out_from_lit(uint64_t o, uint64_t i, uint64_t cnt) const {
         for (uint64_t j = lane; j < cnt; j += 64) *(gu8z *)(dst + o + j) = *(gcu8z *)(lit + i + j);
     }
-    __device__ void out_fill(uint64_t o, uint32_t b, uint64_t cnt) const {
+    __device__ __forceinline__ void out_fill(uint64_t o, uint32_t b, uint64_t cnt) const {
         for (uint64_t j = lane; j < cnt; j += 64) *(gu8z *)(dst + o + j) = (uint8_t)b;
     }
-    __device__ void out_match(uint64_t o, uint64_t off, uint64_t cnt) const {
-        fence();
+    __device__ __forceinline__ void out_match(uint64_t o, uint64_t off, uint64_t cnt) {
+        // wait for the wave's stores only when the source reaches past the
+        // last fence (the output before o is all written by then)
+        if (o - off + (off < cnt ? off : cnt) > fenced) {
+            fence();
+            fenced = o;
+        }
         const uint8_t *m = dst + o - off;
         if (off >= cnt) {
             for (uint64_t j = lane; j < cnt; j += 64) *(gu8z *)(dst + o + j) = *(gcu8z *)(m + j);
@@ -90,7 +112,7 @@ struct DevEnv {
             for (uint64_t j = lane; j < cnt; j += 64) *(gu8z *)(dst + o + j) = *(gcu8z *)(m + j % off);
         }
     }
-    __device__ uint64_t out64(uint64_t o) const {
+    __device__ __forceinline__ uint64_t out64(uint64_t o) const {
         uint64_t v = 0;
         for (uint32_t k = 0; k < 8; k++) v |= (uint64_t)(*(gcu8z *)(dst + o + k)) << (8 * k);
         return v;
@@ -99,6 +121,20 @@ struct DevEnv {
 
 }  // namespace
 
+#ifdef JFSX_ZSTD_STAMP
+__device__ unsigned long long g_zstd_stamps[8];  // diagnostic build: cycles per decoder section
+}  // namespace jfsx
+extern "C" int jfsx_debug_zstd_stamps(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(jfsx::g_zstd_stamps), 64) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(jfsx::g_zstd_stamps), z, 64) != hipSuccess) return -1;
+    }
+    return 0;
+}
+namespace jfsx {
+#endif
+
 // One wave per object.  ZDev.len = compressed bytes, ZDev.cap = dst capacity;
 // ZOut.out_len = decoded bytes, status JFSX_EFORMAT for a frame
 // ZSTD_decompress rejects (or one that does not fit in cap).
@@ -106,8 +142,16 @@ __global__ __launch_bounds__(64) void zstd_decompress_k(const ZDev *__restrict__
                                                         uint8_t *__restrict__ scratch) {
     __shared__ jzd::Tables T;
     const ZDev b = blks[blockIdx.x];
-    DevEnv e{b.src, (int64_t)b.len, b.dst, scratch + (size_t)blockIdx.x * (jzd::kBlockMax + 64), threadIdx.x};
+    DevEnv e{b.src, (int64_t)b.len, b.dst, scratch + (size_t)blockIdx.x * (jzd::kBlockMax + 64), threadIdx.x, 0};
+#ifdef JFSX_ZSTD_STAMP
+    for (int k = 0; k < 5; k++) e.st[k] = 0;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(e.last)::"memory");
+#endif
     const int64_t r = jzd::decompress(e, T, b.len, b.cap);
+#ifdef JFSX_ZSTD_STAMP
+    if (threadIdx.x == 0)
+        for (int k = 0; k < 5; k++) atomicAdd(&g_zstd_stamps[k], e.st[k]);
+#endif
     if (threadIdx.x == 0) {
         outs[blockIdx.x].out_len = r < 0 ? 0 : (uint64_t)r;
         outs[blockIdx.x].status = r < 0 ? JFSX_EFORMAT : JFSX_OK;

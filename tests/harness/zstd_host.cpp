@@ -10,19 +10,23 @@ struct HostEnv {
     const uint8_t *src;
     int64_t n;
     uint8_t *dst;
-    std::vector<uint8_t> lit;
+    uint8_t *lit;
     uint8_t in8(int64_t i) const { return (i >= 0 && i < n) ? src[i] : 0; }
     uint64_t in64(int64_t i) const {
         uint64_t v = 0;
         for (int k = 0; k < 8; k++) v |= (uint64_t)in8(i + k) << (8 * k);
         return v;
     }
-    void lit_put(uint64_t i, uint32_t b) const { const_cast<HostEnv *>(this)->lit[i] = (uint8_t)b; }
-    void lit_fill(uint64_t i, uint32_t b, uint64_t cnt) { memset(&lit[i], (int)b, cnt); }
+    void lit_put(uint64_t i, uint32_t b) const { lit[i] = (uint8_t)b; }
+    void lit_fill(uint64_t i, uint32_t b, uint64_t cnt) { memset(lit + i, (int)b, cnt); }
     void lit_sync() {}
+    void stamp(int) {}
+    void huf_fill(uint16_t *p, uint16_t v, uint32_t cnt) const {
+        for (uint32_t j = 0; j < cnt; j++) p[j] = v;
+    }
     void out_sync() {}
     void out_from_in(uint64_t o, int64_t i, uint64_t cnt) { memcpy(dst + o, src + i, cnt); }
-    void out_from_lit(uint64_t o, uint64_t i, uint64_t cnt) { memcpy(dst + o, &lit[i], cnt); }
+    void out_from_lit(uint64_t o, uint64_t i, uint64_t cnt) { memcpy(dst + o, lit + i, cnt); }
     void out_fill(uint64_t o, uint32_t b, uint64_t cnt) { memset(dst + o, (int)b, cnt); }
     void out_match(uint64_t o, uint64_t off, uint64_t cnt) {
         for (uint64_t j = 0; j < cnt; j++) dst[o + j] = dst[o - off + j];
@@ -37,7 +41,8 @@ struct HostEnv {
 
 extern "C" int64_t zstd_host_decompress(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap) {
     static thread_local jzd::Tables t;
-    HostEnv e{src, n, dst, std::vector<uint8_t>(jzd::kBlockMax + 64)};
+    std::vector<uint8_t> litbuf(jzd::kBlockMax + 64);
+    HostEnv e{src, n, dst, litbuf.data()};
     // out64 may read up to 7 bytes past the output: decode into a padded copy
     std::vector<uint8_t> pad((size_t)cap + 8);
     e.dst = pad.data();
