@@ -6,15 +6,17 @@ decompress steps of the chunk store's block upload and load.
   noOp (copy; "buffer too short: %d < %d")                         compress.go:52-70
   LZ4 (lz4.CompressDefault / lz4.DecompressSafe;
        "decompress an empty input")                                compress.go:104-125
+  ZStandard.Decompress (zstd.Decompress; "buffer too short")       compress.go:93-102
   upload_block: CompressBound buffer, Compress, then Put           cached_store.go:371-392
   load_block: Get, Decompress into the block, "read %s fully"      cached_store.go:673-745
 
 The LZ4 block codec runs on the HIP engine (jfsx_lz4_compress_batch /
 jfsx_lz4_decompress_batch, jfsx_lz4.hip), bit-exact to the LZ4 C library the
 reference binds; CompressBatch / DecompressBatch are the batched entry points
-(one engine call per batch).  Zstandard (DataDog/zstd, level 1) is not part of
-this engine: NewCompressor("zstd") returns a compressor whose codec calls
-raise NotImplementedError rather than run anywhere else.
+(one engine call per batch).  Zstandard decompression runs on the engine
+too (jfsx_zstd_decompress_batch, jfsx_zstd.hip); Zstandard compression
+(zstd.CompressLevel at level 1) stays with the Go host's libzstd, so
+ZStandard.Compress raises NotImplementedError rather than run anywhere else.
 """
 from . import engine as E
 from .encrypt import default_engine
@@ -98,10 +100,16 @@ class LZ4:
 
 
 class ZStandard:
-    """zstd level 1 (DataDog/zstd) -- not built in this engine."""
+    """The "zstd" compressor (DataDog/zstd v1.5.0, level 1).  Decompress runs on
+    the engine; Compress is the Go host's libzstd call."""
 
-    def __init__(self, level=1):
+    def __init__(self, level=1, eng=None):
         self.level = level
+        self._eng = eng
+
+    @property
+    def eng(self):
+        return self._eng or default_engine()
 
     def Name(self):
         return "Zstd"
@@ -110,17 +118,41 @@ class ZStandard:
         # ZSTD_COMPRESSBOUND(n)
         return n + (n >> 8) + (((128 << 10) - n) >> 11 if n < (128 << 10) else 0)
 
-    def _absent(self, *a):
-        raise NotImplementedError("zstd compression is not part of the jfsx engine")
+    def Compress(self, dst, src):
+        raise NotImplementedError("zstd compression runs in the Go host's libzstd, not in the jfsx engine")
 
-    Compress = Decompress = _absent
+    def Decompress(self, dst, src):
+        d = self.DecompressBatch([src], [len(dst)])[0]
+        if isinstance(d, Exception):
+            raise d
+        dst[:len(d)] = d
+        return len(d)
+
+    def DecompressBatch(self, blobs, sizes):
+        """(frames, destination size) per block -> decoded bytes, or a
+        CompressError: "buffer too short: %d < %d" where the frames decode but
+        not into the destination (zstd.Decompress then returns a larger
+        buffer, compress.go:98-100), else the decoder's error."""
+        res = self.eng.zstd_decompress(blobs, sizes)
+        out, retry = [], []
+        for i, (st, d) in enumerate(res):
+            out.append(d if st == E.OK else None)
+            if st != E.OK:
+                retry.append(i)
+        if retry:
+            big = self.eng.zstd_decompress([blobs[i] for i in retry],
+                                           [max(4 * sizes[i], 1 << 20) for i in retry])
+            for i, (st, d) in zip(retry, big):
+                out[i] = CompressError("buffer too short: %d < %d" % (sizes[i], len(d)) if st == E.OK
+                                       else "zstd: corrupted frame")
+        return out
 
 
 def NewCompressor(algr, eng=None):
     """compress.go:38-50: None for an unknown name."""
     algr = algr.lower()
     if algr == "zstd":
-        return ZStandard(1)
+        return ZStandard(1, eng)
     if algr == "lz4":
         return LZ4(eng)
     if algr in ("none", ""):
@@ -152,7 +184,7 @@ def load_blocks(store, keys, lengths, compressor):
     the block's length; a short result is "read %s fully: %s (%d < %d)"."""
     objs = [store.Get(k, 0, -1) for k in keys]
     compressed = [compressor.CompressBound(n) > n for n in lengths]
-    if isinstance(compressor, LZ4):
+    if isinstance(compressor, (LZ4, ZStandard)):
         dec = compressor.DecompressBatch(objs, lengths)
     else:
         dec = []

@@ -621,6 +621,7 @@ ZD_HD int32_t block(Env &e, Tables &t, Mode &m, int32_t p, int32_t n, uint32_t f
         for (uint32_t k = 0; k < nbSeq; k++) {
             if (b.rem < 0) return ZD_EFORMAT;  // BIT_reloadDStream overflow before a sequence
             const SeqEnt dl = ld_seq(t.ll + sl), dm = ld_seq(t.ml + sm), dof = ld_seq(t.of + so);
+            e.stamp(5);  // table reads
             // offset
             uint32_t off;
             const uint32_t ofc = dof.addBits;
@@ -650,6 +651,7 @@ ZD_HD int32_t block(Env &e, Tables &t, Mode &m, int32_t p, int32_t n, uint32_t f
                     off = tmp;
                 }
             }
+            e.stamp(6);  // offset
             ml = dm.base + b.read(dm.addBits);
             ll = dl.base + b.read(dl.addBits);
             // state updates (libzstd 1.4 updates after the last sequence too)

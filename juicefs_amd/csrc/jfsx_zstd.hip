@@ -32,7 +32,7 @@ struct DevEnv {
     uint32_t lane;
     uint64_t fenced;     // output below this is visible to the wave's loads
 #ifdef JFSX_ZSTD_STAMP
-    unsigned long long st[5], last;
+    unsigned long long st[8], last;
     __device__ __forceinline__ void stamp(int k) {
         unsigned long long t;
         __builtin_amdgcn_sched_barrier(0);
@@ -144,13 +144,13 @@ __global__ __launch_bounds__(64) void zstd_decompress_k(const ZDev *__restrict__
     const ZDev b = blks[blockIdx.x];
     DevEnv e{b.src, (int64_t)b.len, b.dst, scratch + (size_t)blockIdx.x * (jzd::kBlockMax + 64), threadIdx.x, 0};
 #ifdef JFSX_ZSTD_STAMP
-    for (int k = 0; k < 5; k++) e.st[k] = 0;
+    for (int k = 0; k < 8; k++) e.st[k] = 0;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(e.last)::"memory");
 #endif
     const int64_t r = jzd::decompress(e, T, b.len, b.cap);
 #ifdef JFSX_ZSTD_STAMP
     if (threadIdx.x == 0)
-        for (int k = 0; k < 5; k++) atomicAdd(&g_zstd_stamps[k], e.st[k]);
+        for (int k = 0; k < 8; k++) atomicAdd(&g_zstd_stamps[k], e.st[k]);
 #endif
     if (threadIdx.x == 0) {
         outs[blockIdx.x].out_len = r < 0 ? 0 : (uint64_t)r;

@@ -10,7 +10,7 @@ import bench  # noqa: E402
 from juicefs_amd import engine as E  # noqa: E402
 from tests import zstd_lib  # noqa: E402
 
-names = ["literals", "seq headers", "seq decode", "seq execute", "block start/raw"]
+names = ["literals", "seq headers", "ml/ll/states", "seq execute", "block start/raw", "table reads", "offset", "-"]
 nb, L = int(sys.argv[1]) if len(sys.argv) > 1 else 256, 4 << 20
 eng = E.Engine(0)
 lib = E._lib
@@ -24,8 +24,8 @@ out = (ctypes.c_ulonglong * 8)()
 lib.jfsx_debug_zstd_stamps(out, 1)
 eng.zstd_decompress([frames[i % 16] for i in range(nb)], [L] * nb)
 lib.jfsx_debug_zstd_stamps(out, 1)
-tot = sum(out[k] for k in range(5))
+tot = sum(out[k] for k in range(8))
 print("cycles per frame (per wave) %.3e" % (tot / nb))
-for k in range(5):
+for k in range(7):
     print("%-16s %5.1f %%" % (names[k], 100.0 * out[k] / tot))
 eng.close()

@@ -101,3 +101,34 @@ def test_malformed_agrees_with_library(eng):
         else:
             assert st == E.OK and d == r
     assert rejects > 200
+
+
+def test_mirror_decompress_and_load_blocks(eng):
+    """compress.go:93-102 (ZStandard.Decompress) and cachedStore.load's
+    decompress step (cached_store.go:680-745) through the engine."""
+    from juicefs_amd import compress as C
+    z = C.NewCompressor("zstd", eng)
+    src = lz4_data.sample("text", 300000, seed=9)
+    fr = zstd_lib.compress(src)
+    dst = bytearray(len(src))
+    assert z.Decompress(dst, fr) == len(src) and bytes(dst) == src
+    with pytest.raises(C.CompressError, match="buffer too short: %d < %d" % (len(src) - 1, len(src))):
+        z.Decompress(bytearray(len(src) - 1), fr)
+    with pytest.raises(C.CompressError, match="zstd: corrupted frame"):
+        z.Decompress(bytearray(len(src)), fr[:len(fr) // 2])
+
+    class Store:
+        def __init__(self):
+            self.d = {}
+
+        def Put(self, k, v):
+            self.d[k] = bytes(v)
+
+        def Get(self, k, off, lim):
+            return self.d[k]
+    st = Store()
+    blocks = [lz4_data.sample(k, 4 << 20, seed=i) for i, k in enumerate(("text", "runs", "random"))]
+    keys = ["chunks/0/0/%d_0_%d" % (i, len(b)) for i, b in enumerate(blocks)]
+    for k, b in zip(keys, blocks):
+        st.Put(k, zstd_lib.compress(b))
+    assert C.load_blocks(st, keys, [len(b) for b in blocks], z) == blocks
