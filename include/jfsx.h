@@ -328,6 +328,9 @@ int jfsx_mctx_lz4_decompress_batch(jfsx_mctx *m, int n, jfsx_zblk *blks, int mem
  * larger than dst_cap).  Compression ("zstd" Compress, level 1) stays on the
  * host's libzstd. */
 int jfsx_zstd_decompress_batch(jfsx_ctx *ctx, int n, jfsx_zblk *blks, int mem);
+/* per block through the aggregator, and over a multi-device context */
+int jfsx_agg_zstd_decompress(jfsx_agg *agg, jfsx_zblk *blk, int mem);
+int jfsx_mctx_zstd_decompress_batch(jfsx_mctx *m, int n, jfsx_zblk *blks, int mem);
 
 /* header helper: returns wrapped-key length and offset/size of the nonce so a
  * caller can unwrap the key first (encrypt.go:197-205) */

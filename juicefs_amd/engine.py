@@ -40,7 +40,7 @@ EXPORTS = [
     "jfsx_mctx_seal_batch", "jfsx_mctx_open_batch", "jfsx_mctx_crc32c_segments", "jfsx_agg_new_mctx",
     "jfsx_agg_dev_batches", "jfsx_lz4_bound", "jfsx_lz4_compress_batch", "jfsx_lz4_decompress_batch",
     "jfsx_agg_lz4_compress", "jfsx_agg_lz4_decompress", "jfsx_mctx_lz4_compress_batch", "jfsx_mctx_lz4_decompress_batch",
-    "jfsx_zstd_decompress_batch",
+    "jfsx_zstd_decompress_batch", "jfsx_agg_zstd_decompress", "jfsx_mctx_zstd_decompress_batch",
 ]
 
 
@@ -152,6 +152,8 @@ def load_library(path=LIB_PATH):
             "jfsx_mctx_lz4_compress_batch": (I, [P, I, ctypes.POINTER(jfsx_zblk), I]),
             "jfsx_mctx_lz4_decompress_batch": (I, [P, I, ctypes.POINTER(jfsx_zblk), I]),
             "jfsx_zstd_decompress_batch": (I, [P, I, ctypes.POINTER(jfsx_zblk), I]),
+            "jfsx_agg_zstd_decompress": (I, [P, ctypes.POINTER(jfsx_zblk), I]),
+            "jfsx_mctx_zstd_decompress_batch": (I, [P, I, ctypes.POINTER(jfsx_zblk), I]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -615,6 +617,9 @@ class MultiEngine:
     def lz4_decompress_batch(self, zblks, n, mem=MEM_HOST):
         self._check(self.L.jfsx_mctx_lz4_decompress_batch(self.m, n, zblks, mem), "jfsx_mctx_lz4_decompress_batch")
 
+    def zstd_decompress_batch(self, zblks, n, mem=MEM_HOST):
+        self._check(self.L.jfsx_mctx_zstd_decompress_batch(self.m, n, zblks, mem), "jfsx_mctx_zstd_decompress_batch")
+
 
 class Aggregator:
     """jfsx_agg: per-block calls from many threads coalesced into batches
@@ -674,6 +679,9 @@ class Aggregator:
 
     def lz4_decompress(self, z, mem=MEM_HOST):
         self.eng._check(self.L.jfsx_agg_lz4_decompress(self.h, ctypes.byref(z), mem), "jfsx_agg_lz4_decompress")
+
+    def zstd_decompress(self, z, mem=MEM_HOST):
+        self.eng._check(self.L.jfsx_agg_zstd_decompress(self.h, ctypes.byref(z), mem), "jfsx_agg_zstd_decompress")
 
     def stats(self):
         """(calls, batches, blocks carried by those batches)"""

@@ -132,3 +132,42 @@ def test_mirror_decompress_and_load_blocks(eng):
     for k, b in zip(keys, blocks):
         st.Put(k, zstd_lib.compress(b))
     assert C.load_blocks(st, keys, [len(b) for b in blocks], z) == blocks
+
+
+def test_per_block_calls_through_the_aggregator_and_mctx():
+    """cachedStore.load calls Decompress once per block from many goroutines:
+    through jfsx_agg they become batches; a multi-device context splits a
+    host batch over its devices (one here)."""
+    import threading
+    eng = E.Engine(0)
+    try:
+        T = 24
+        srcs = [lz4_data.sample(lz4_data.KINDS[i % 6], 50000 + 997 * i, seed=i) for i in range(T)]
+        frames = [np.frombuffer(zstd_lib.compress(s, 1 + i % 3), np.uint8) for i, s in enumerate(srcs)]
+        backs = [np.zeros(len(s), np.uint8) for s in srcs]
+        zd = [E.jfsx_zblk() for _ in range(T)]
+        with E.Aggregator(eng, window_us=3000) as agg:
+            def worker(i):
+                d = zd[i]
+                d.src, d.src_len, d.dst, d.dst_cap = frames[i].ctypes.data, frames[i].size, backs[i].ctypes.data, \
+                    backs[i].size
+                agg.zstd_decompress(d)
+            th = [threading.Thread(target=worker, args=(i,)) for i in range(T)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            calls, batches, blocks = agg.stats()
+        for i in range(T):
+            assert zd[i].status == E.OK and zd[i].out_len == len(srcs[i]) and backs[i].tobytes() == srcs[i]
+        assert calls == T and batches < calls
+    finally:
+        eng.close()
+    m = E.MultiEngine(0)
+    try:
+        outs = [np.zeros(len(s), np.uint8) for s in srcs]
+        arr, n = E.Engine.make_zblocks((f.ctypes.data, f.size, o.ctypes.data, o.size) for f, o in zip(frames, outs))
+        m.zstd_decompress_batch(arr, n)
+        assert all(arr[i].status == E.OK and outs[i].tobytes() == srcs[i] for i in range(T))
+    finally:
+        m.close()
