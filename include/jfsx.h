@@ -325,8 +325,9 @@ int jfsx_mctx_lz4_decompress_batch(jfsx_mctx *m, int n, jfsx_zblk *blks, int mem
  * (concatenated frames and skippable frames allowed, as ZSTD_decompress);
  * out_len = decoded bytes; status JFSX_EFORMAT where ZSTD_decompress returns
  * an error (malformed frame, dictionary id, checksum mismatch, or output
- * larger than dst_cap).  Compression ("zstd" Compress, level 1) stays on the
- * host's libzstd. */
+ * larger than dst_cap); dst_cap < 2^31, src_len <= 0x7E000000 (JFSX_EINVAL
+ * otherwise).  Compression ("zstd" Compress, level 1) stays on the host's
+ * libzstd. */
 int jfsx_zstd_decompress_batch(jfsx_ctx *ctx, int n, jfsx_zblk *blks, int mem);
 /* per block through the aggregator, and over a multi-device context */
 int jfsx_agg_zstd_decompress(jfsx_agg *agg, jfsx_zblk *blk, int mem);

@@ -722,6 +722,7 @@ int run_lz4(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, bool comp, bool zstd = fa
             z[i].dst_cap >= ((uint64_t)1 << 32))
             return JFSX_EINVAL;
         if (comp && z[i].dst_cap < lz4_bound(z[i].src_len)) return JFSX_EINVAL;
+        if (zstd && z[i].dst_cap >= ((uint64_t)1 << 31)) return JFSX_EINVAL;  // 32-bit frame positions
     }
     if (n == 0) return 0;
     int rc;

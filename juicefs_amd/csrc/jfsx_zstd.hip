@@ -26,11 +26,12 @@ typedef __attribute__((address_space(1))) uint8_t gu8z;
 
 struct DevEnv {
     const uint8_t *src;  // compressed object
-    int64_t n;
+    int32_t n;
     uint8_t *dst;        // output (frame positions are offsets from dst)
-    uint8_t *lit;        // literal scratch (jzd::kBlockMax + 64 bytes)
+    uint8_t *lit;        // literal scratch (kZstdScratch bytes)
     uint32_t lane;
-    uint64_t fenced;     // output below this is visible to the wave's loads
+    uint32_t fenced;     // output below this is visible to the wave's loads
+    uint32_t lw0, lwv;   // literal window: scratch bytes [lw0, lw0 + 256), lane L holds dword L
 #ifdef JFSX_ZSTD_STAMP
     unsigned long long st[8], last;
     __device__ __forceinline__ void stamp(int k) {
@@ -47,58 +48,79 @@ struct DevEnv {
 
     // input dword d (bytes [4d - sh, 4d - sh + 4) of src, src = al + sh), zero
     // when it holds no input byte; scalar load (uniform address)
-    __device__ __forceinline__ uint32_t dw(int64_t d) const {
+    __device__ __forceinline__ uint32_t dw(int32_t d) const {
         const uintptr_t al = (uintptr_t)src & ~(uintptr_t)3;
-        const int64_t sh = (int64_t)((uintptr_t)src & 3);
-        const int64_t b0 = 4 * d - sh;  // first src byte of the dword
+        const int32_t sh = (int32_t)((uintptr_t)src & 3);
+        const int32_t b0 = 4 * d - sh;  // first src byte of the dword
         if (b0 + 3 < 0 || b0 >= n) return 0u;
-        uint32_t v = ZD_U32(*(ccu32 *)(al + 4 * d));
+        uint32_t v = ZD_U32(*(ccu32 *)(al + 4 * (int64_t)d));
         // bytes outside [0, n) read as zero
         if (b0 < 0) v &= 0xffffffffu << (8 * (uint32_t)(-b0));
         if (b0 + 4 > n) v &= 0xffffffffu >> (8 * (uint32_t)(b0 + 4 - n));
         return v;
     }
-    __device__ __forceinline__ uint32_t in8(int64_t i) const {
+    __device__ __forceinline__ uint32_t in8(int32_t i) const {
         if (i < 0 || i >= n) return 0;
-        const int64_t x = i + (int64_t)((uintptr_t)src & 3);
+        const int32_t x = i + (int32_t)((uintptr_t)src & 3);
         return (dw(x >> 2) >> (8 * (uint32_t)(x & 3))) & 255u;
     }
-    __device__ __forceinline__ uint64_t in64(int64_t i) const {
-        const int64_t x = i + (int64_t)((uintptr_t)src & 3);
-        const int64_t d = x >> 2;  // floor (x may be negative)
+    __device__ __forceinline__ uint64_t in64(int32_t i) const {
+        const int32_t x = i + (int32_t)((uintptr_t)src & 3);
+        const int32_t d = x >> 2;  // floor (x may be negative)
         const uint32_t s = (uint32_t)(x & 3);
         const uint64_t lo = (uint64_t)dw(d) | ((uint64_t)dw(d + 1) << 32);
         if (!s) return lo;
         const uint64_t hi = dw(d + 2);
         return (lo >> (8 * s)) | (hi << (64 - 8 * s));
     }
-    __device__ __forceinline__ void lit_put(uint64_t i, uint32_t b) const {
+    __device__ __forceinline__ void lit_put(uint32_t i, uint32_t b) const {
         if (lane == 0) *(gu8z *)(lit + i) = (uint8_t)b;
     }
-    __device__ __forceinline__ void lit_fill(uint64_t i, uint32_t b, uint64_t cnt) const {
-        for (uint64_t j = lane; j < cnt; j += 64) *(gu8z *)(lit + i + j) = (uint8_t)b;
+    __device__ __forceinline__ void lit_fill(uint32_t i, uint32_t b, uint32_t cnt) const {
+        for (uint32_t j = lane; j < cnt; j += 64) *(gu8z *)(lit + i + j) = (uint8_t)b;
     }
     __device__ __forceinline__ void fence() const {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
-    __device__ __forceinline__ void lit_sync() const { fence(); }
+    __device__ __forceinline__ void lit_sync() {
+        fence();
+        lw0 = 0xffffffffu;  // the block's literals are new
+    }
     __device__ __forceinline__ void huf_fill(uint16_t *p, uint16_t v, uint32_t cnt) const {
         for (uint32_t j = lane; j < cnt; j += 64) p[j] = v;
     }
     __device__ __forceinline__ void out_sync() const { fence(); }
-    __device__ __forceinline__ void out_from_in(uint64_t o, int64_t i, uint64_t cnt) const {
-        for (uint64_t j = lane; j < cnt; j += 64) *(gu8z *)(dst + o + j) = (uint8_t)in8_v(i + (int64_t)j);
+    __device__ __forceinline__ void out_from_in(uint32_t o, int32_t i, uint32_t cnt) const {
+        for (uint32_t j = lane; j < cnt; j += 64) *(gu8z *)(dst + o + j) = (uint8_t)in8_v(i + (int32_t)j);
     }
     // per-lane input byte (vector load)
-    __device__ __forceinline__ uint32_t in8_v(int64_t i) const { return *(gcu8z *)(src + i); }
-    __device__ __forceinline__ void out_from_lit(uint64_t o, uint64_t i, uint64_t cnt) const {
-        for (uint64_t j = lane; j < cnt; j += 64) *(gu8z *)(dst + o + j) = *(gcu8z *)(lit + i + j);
+    __device__ __forceinline__ uint32_t in8_v(int32_t i) const { return *(gcu8z *)(src + i); }
+    // literal runs of up to 252 bytes come from a 256-byte register window of
+    // the literal buffer (one load per window, not one per sequence)
+    __device__ __forceinline__ void out_from_lit(uint32_t o, uint32_t i, uint32_t cnt) {
+        if (cnt == 0) return;
+        if (cnt <= 252) {
+            if (i < lw0 || i + cnt > lw0 + 256u) {
+                lw0 = i & ~3u;
+                lwv = *(const __attribute__((address_space(1))) uint32_t *)(lit + lw0 + 4 * lane);
+            }
+            const uint32_t r = i - lw0;
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) {
+                if (64 * k >= cnt) break;
+                const uint32_t j = lane + 64 * k, q = r + j;
+                const uint32_t d = __shfl(lwv, (int)((q >> 2) & 63), 64);
+                if (j < cnt) *(gu8z *)(dst + o + j) = (uint8_t)(d >> (8 * (q & 3)));
+            }
+            return;
+        }
+        for (uint32_t j = lane; j < cnt; j += 64) *(gu8z *)(dst + o + j) = *(gcu8z *)(lit + i + j);
     }
-    __device__ __forceinline__ void out_fill(uint64_t o, uint32_t b, uint64_t cnt) const {
-        for (uint64_t j = lane; j < cnt; j += 64) *(gu8z *)(dst + o + j) = (uint8_t)b;
+    __device__ __forceinline__ void out_fill(uint32_t o, uint32_t b, uint32_t cnt) const {
+        for (uint32_t j = lane; j < cnt; j += 64) *(gu8z *)(dst + o + j) = (uint8_t)b;
     }
-    __device__ __forceinline__ void out_match(uint64_t o, uint64_t off, uint64_t cnt) {
+    __device__ __forceinline__ void out_match(uint32_t o, uint32_t off, uint32_t cnt) {
         // wait for the wave's stores only when the source reaches past the
         // last fence (the output before o is all written by then)
         if (o - off + (off < cnt ? off : cnt) > fenced) {
@@ -107,12 +129,12 @@ struct DevEnv {
         }
         const uint8_t *m = dst + o - off;
         if (off >= cnt) {
-            for (uint64_t j = lane; j < cnt; j += 64) *(gu8z *)(dst + o + j) = *(gcu8z *)(m + j);
+            for (uint32_t j = lane; j < cnt; j += 64) *(gu8z *)(dst + o + j) = *(gcu8z *)(m + j);
         } else {
-            for (uint64_t j = lane; j < cnt; j += 64) *(gu8z *)(dst + o + j) = *(gcu8z *)(m + j % off);
+            for (uint32_t j = lane; j < cnt; j += 64) *(gu8z *)(dst + o + j) = *(gcu8z *)(m + j % off);
         }
     }
-    __device__ __forceinline__ uint64_t out64(uint64_t o) const {
+    __device__ __forceinline__ uint64_t out64(uint32_t o) const {
         uint64_t v = 0;
         for (uint32_t k = 0; k < 8; k++) v |= (uint64_t)(*(gcu8z *)(dst + o + k)) << (8 * k);
         return v;
@@ -142,7 +164,7 @@ __global__ __launch_bounds__(64) void zstd_decompress_k(const ZDev *__restrict__
                                                         uint8_t *__restrict__ scratch) {
     __shared__ jzd::Tables T;
     const ZDev b = blks[blockIdx.x];
-    DevEnv e{b.src, (int64_t)b.len, b.dst, scratch + (size_t)blockIdx.x * (jzd::kBlockMax + 64), threadIdx.x, 0};
+    DevEnv e{b.src, (int32_t)b.len, b.dst, scratch + (size_t)blockIdx.x * kZstdScratch, threadIdx.x, 0, 0xffffffffu, 0};
 #ifdef JFSX_ZSTD_STAMP
     for (int k = 0; k < 8; k++) e.st[k] = 0;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(e.last)::"memory");
