@@ -17,6 +17,7 @@
 #pragma once
 #include <stdint.h>
 #include <stddef.h>
+#include <type_traits>
 
 #if defined(__HIPCC__)
 #define ZD_HD __host__ __device__ __attribute__((always_inline))
@@ -114,10 +115,14 @@ struct Bwd {
     uint64_t cont;  // stream bytes [cb, cb + 8)
     int32_t cb;
     ZD_HD void fill() {
-        int32_t top = (rem - 1) >> 3;  // byte of the next bit
-        if (top < 7) top = 7;
-        cb = top - 7;
-        cont = zd_u64(e.in64(base + cb));
+        const int32_t top = (rem - 1) >> 3;  // byte of the next bit
+        if (top >= 7) {
+            cb = top - 7;
+            cont = e.in64u(base + cb);  // inside the stream region
+        } else {
+            cb = 0;
+            cont = zd_u64(e.in64(base));
+        }
     }
     ZD_HD uint32_t peek(uint32_t k) {  // k <= 32
         const int32_t lo = rem - (int32_t)k;
@@ -133,6 +138,18 @@ struct Bwd {
         const uint32_t v = peek(k);
         rem -= k;
         return v;
+    }
+    // true when bits [rem - t, rem) all lie in the window (after at most one
+    // refill): the caller may then take t bits with take(), no further checks
+    ZD_HD bool ensure(uint32_t t) {
+        if (rem - (int32_t)t >= cb * 8) return true;
+        if (cb == 0) return false;
+        fill();
+        return rem - (int32_t)t >= cb * 8;
+    }
+    ZD_HD uint32_t take(uint32_t k) {  // k <= 31, inside an ensure()d budget
+        rem -= (int32_t)k;
+        return (uint32_t)(cont >> ((uint32_t)(rem - cb * 8) & 63u)) & ((1u << k) - 1u);
     }
 };
 
@@ -470,17 +487,74 @@ ZD_HD int32_t huf_table(const Env &e, Tables &t, int32_t p, int32_t n, uint32_t 
     return isize + 1;
 }
 
+// Huffman symbols [k, cnt) of one stream into the literal buffer at o + k,
+// bit by bit (the tail of a stream, and over-reads past its start)
+template <class Env>
+ZD_HD void huf_tail(const Env &e, Tables &t, Bwd<Env> &b, uint32_t hlog, uint32_t o, uint32_t k, uint32_t cnt) {
+    for (; k < cnt; k++) {
+        const uint32_t ent = ZD_U32(t.huf[b.peek(hlog)]);
+        b.rem -= ent >> 8;
+        e.lit_put(o + k, ent & 255);
+    }
+}
+
+// one symbol from an ensure()d window: returns it, consumes its bits
+template <class Env>
+ZD_HD uint32_t huf_sym(const Tables &t, Bwd<Env> &b, uint32_t hlog) {
+    const uint32_t ent = ZD_U32(t.huf[(uint32_t)(b.cont >> ((uint32_t)(b.rem - (int32_t)hlog - b.cb * 8) & 63u)) &
+                                       ((1u << hlog) - 1u)]);
+    b.rem -= ent >> 8;
+    return ent & 255;
+}
+
+// four symbols of one stream, packed little-endian (window ensure()d for 4 * hlog bits)
+template <class Env>
+ZD_HD uint32_t huf_sym4(const Tables &t, Bwd<Env> &b, uint32_t hlog) {
+    uint32_t w = huf_sym(t, b, hlog);
+    w |= huf_sym(t, b, hlog) << 8;
+    w |= huf_sym(t, b, hlog) << 16;
+    return w | huf_sym(t, b, hlog) << 24;
+}
+
 // one Huffman stream [p, p + n) into the literal buffer [o, o + cnt)
 template <class Env>
 ZD_HD bool huf_stream(const Env &e, Tables &t, uint32_t hlog, int32_t p, int32_t n, uint32_t o, uint32_t cnt) {
     Bwd<Env> b;
     if (!bwd_init(b, e, p, n)) return false;
-    for (uint32_t k = 0; k < cnt; k++) {
-        const uint32_t ent = ZD_U32(t.huf[b.peek(hlog)]);
-        b.rem -= ent >> 8;
-        e.lit_put(o + k, ent & 255);
+    uint32_t k = 0;
+    for (; k + 4 <= cnt && b.ensure(4 * hlog); k += 4) {
+        const uint32_t w = huf_sym4(t, b, hlog);
+        e.lit_put4(o + k, w, o + k, w, o + k, w, o + k, w);
     }
+    huf_tail(e, t, b, hlog, o, k, cnt);
     return b.rem == 0;
+}
+
+// the four streams of a 4-stream literal section, decoded interleaved (four
+// independent table-lookup chains) into [0, seg), [seg, 2 seg), ...
+template <class Env>
+ZD_HD bool huf_streams4(const Env &e, Tables &t, uint32_t hlog, int32_t s1, int32_t l1, int32_t s2, int32_t l2,
+                        int32_t s3, int32_t l3, int32_t s4, int32_t l4, uint32_t seg, uint32_t c4) {
+    Bwd<Env> b0, b1, b2, b3;
+    if (!bwd_init(b0, e, s1, l1) || !bwd_init(b1, e, s2, l2) || !bwd_init(b2, e, s3, l3) || !bwd_init(b3, e, s4, l4))
+        return false;
+    const uint32_t need = 4 * hlog;
+    uint32_t k = 0;  // c4 <= seg
+    for (; k + 4 <= c4 && b0.ensure(need) && b1.ensure(need) && b2.ensure(need) && b3.ensure(need); k += 4) {
+        uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+        for (uint32_t i = 0; i < 4; i++) {
+            w0 |= huf_sym(t, b0, hlog) << (8 * i);
+            w1 |= huf_sym(t, b1, hlog) << (8 * i);
+            w2 |= huf_sym(t, b2, hlog) << (8 * i);
+            w3 |= huf_sym(t, b3, hlog) << (8 * i);
+        }
+        e.lit_put4(k, w0, seg + k, w1, 2 * seg + k, w2, 3 * seg + k, w3);
+    }
+    huf_tail(e, t, b0, hlog, 0, k, seg);
+    huf_tail(e, t, b1, hlog, seg, k, seg);
+    huf_tail(e, t, b2, hlog, 2 * seg, k, seg);
+    huf_tail(e, t, b3, hlog, 3 * seg, k, c4);
+    return b0.rem == 0 && b1.rem == 0 && b2.rem == 0 && b3.rem == 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -573,10 +647,8 @@ ZD_HD int32_t block(Env &e, Tables &t, Mode &m, int32_t p, int32_t n, uint32_t f
                 return ZD_EFORMAT;
             }
             const int32_t s1 = q + 6, s2 = s1 + l1, s3 = s2 + l2, s4 = s3 + l3;
-            if (!huf_stream(e, t, m.hufLog, s1, l1, 0, seg)) return ZD_EFORMAT;
-            if (!huf_stream(e, t, m.hufLog, s2, l2, seg, seg)) return ZD_EFORMAT;
-            if (!huf_stream(e, t, m.hufLog, s3, l3, 2 * seg, seg)) return ZD_EFORMAT;
-            if (!huf_stream(e, t, m.hufLog, s4, l4, 3 * seg, litSize - 3 * seg)) return ZD_EFORMAT;
+            if (!huf_streams4(e, t, m.hufLog, s1, l1, s2, l2, s3, l3, s4, l4, seg, litSize - 3 * seg))
+                return ZD_EFORMAT;
         }
         lused = lh + litC;
     }
@@ -622,14 +694,22 @@ ZD_HD int32_t block(Env &e, Tables &t, Mode &m, int32_t p, int32_t n, uint32_t f
             if (b.rem < 0) return ZD_EFORMAT;  // BIT_reloadDStream overflow before a sequence
             const SeqEnt dl = ld_seq(t.ll + sl), dm = ld_seq(t.ml + sm), dof = ld_seq(t.of + so);
             e.stamp(5);  // table reads
-            // offset
-            uint32_t off;
-            const uint32_t ofc = dof.addBits;
+            const uint32_t ofc = dof.addBits;  // the offset takes ofc bits (1 for ofc == 1)
             const uint32_t ll0 = dl.base == 0 && dl.addBits == 0 ? 1u : 0u;
-            uint32_t ml, ll;
-            {
+            uint32_t off, ml, ll;
+            // one window check per sequence when its bits are all in the
+            // window (the common case); otherwise bit-by-bit reads
+            auto decode = [&](auto fastc) {
+                auto rd = [&](uint32_t nb) -> uint32_t {
+                    uint32_t v;
+                    if constexpr (decltype(fastc)::value)
+                        v = b.take(nb);
+                    else
+                        v = b.read(nb);
+                    return v;
+                };
                 if (ofc > 1) {
-                    off = dof.base + b.read(ofc) - 3;
+                    off = dof.base + rd(ofc) - 3;
                     m.rep[2] = m.rep[1];
                     m.rep[1] = m.rep[0];
                     m.rep[0] = (uint32_t)off;
@@ -642,7 +722,7 @@ ZD_HD int32_t block(Env &e, Tables &t, Mode &m, int32_t p, int32_t n, uint32_t f
                         m.rep[0] = (uint32_t)off;
                     }
                 } else {
-                    const uint32_t idx = 1 + ll0 + (uint32_t)b.read(1);
+                    const uint32_t idx = 1 + ll0 + rd(1);
                     uint32_t tmp = idx == 3 ? m.rep[0] - 1 : idx == 2 ? m.rep[2] : m.rep[1];
                     tmp += !tmp;
                     if (idx != 1) m.rep[2] = m.rep[1];
@@ -650,14 +730,17 @@ ZD_HD int32_t block(Env &e, Tables &t, Mode &m, int32_t p, int32_t n, uint32_t f
                     m.rep[0] = (uint32_t)tmp;
                     off = tmp;
                 }
-            }
-            e.stamp(6);  // offset
-            ml = dm.base + b.read(dm.addBits);
-            ll = dl.base + b.read(dl.addBits);
-            // state updates (libzstd 1.4 updates after the last sequence too)
-            sl = dl.next + (uint32_t)b.read(dl.nbBits);
-            sm = dm.next + (uint32_t)b.read(dm.nbBits);
-            so = dof.next + (uint32_t)b.read(dof.nbBits);
+                ml = dm.base + rd(dm.addBits);
+                ll = dl.base + rd(dl.addBits);
+                // state updates (libzstd 1.4 updates after the last sequence too)
+                sl = dl.next + rd(dl.nbBits);
+                sm = dm.next + rd(dm.nbBits);
+                so = dof.next + rd(dof.nbBits);
+            };
+            if (b.ensure(ofc + dm.addBits + dl.addBits + dl.nbBits + dm.nbBits + dof.nbBits))
+                decode(std::true_type{});
+            else
+                decode(std::false_type{});
             e.stamp(2);  // sequence decode
             // ZSTD_execSequence
             if (ll + ml > cap - o) return ZD_EDSTSIZE;

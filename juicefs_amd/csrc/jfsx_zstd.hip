@@ -73,8 +73,28 @@ struct DevEnv {
         const uint64_t hi = dw(d + 2);
         return (lo >> (8 * s)) | (hi << (64 - 8 * s));
     }
+    // bytes [i, i + 8), all inside the input: three scalar dword loads
+    __device__ __forceinline__ uint64_t in64u(int32_t i) const {
+        const uintptr_t a = (uintptr_t)src + (uint32_t)i;
+        const uintptr_t al = a & ~(uintptr_t)3;
+        const uint32_t sh = 8 * (uint32_t)(a & 3);
+        const uint64_t lo = (uint64_t)ZD_U32(*(ccu32 *)al) | ((uint64_t)ZD_U32(*(ccu32 *)(al + 4)) << 32);
+        // the third dword holds an input byte only when a is unaligned
+        const uint64_t hi = ZD_U32(*(ccu32 *)(al + (sh ? 8 : 4)));
+        return (lo >> sh) | ((hi << 32) << (32 - sh));
+    }
     __device__ __forceinline__ void lit_put(uint32_t i, uint32_t b) const {
         if (lane == 0) *(gu8z *)(lit + i) = (uint8_t)b;
+    }
+    // 4 × 4 literal bytes: w_j's bytes at o_j .. o_j + 3 (lanes 0-15, one store)
+    __device__ __forceinline__ void lit_put4(uint32_t o0, uint32_t w0, uint32_t o1, uint32_t w1, uint32_t o2,
+                                             uint32_t w2, uint32_t o3, uint32_t w3) const {
+        if (lane < 16) {
+            const uint32_t j = lane >> 2, i = lane & 3;
+            const uint32_t o = j == 0 ? o0 : j == 1 ? o1 : j == 2 ? o2 : o3;
+            const uint32_t w = j == 0 ? w0 : j == 1 ? w1 : j == 2 ? w2 : w3;
+            *(gu8z *)(lit + o + i) = (uint8_t)(w >> (8 * i));
+        }
     }
     __device__ __forceinline__ void lit_fill(uint32_t i, uint32_t b, uint32_t cnt) const {
         for (uint32_t j = lane; j < cnt; j += 64) *(gu8z *)(lit + i + j) = (uint8_t)b;

@@ -1,6 +1,7 @@
 // Host build of the engine's Zstandard decoder (juicefs_amd/csrc/jfsx_zstd.h,
 // the code the GPU kernel runs) for the CPU test suite: plain memory behind
 // the decoder's Env interface.  Built by tests/test_zstd_host.py with g++.
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 #include "../../juicefs_amd/csrc/jfsx_zstd.h"
@@ -17,7 +18,17 @@ struct HostEnv {
         for (int k = 0; k < 8; k++) v |= (uint64_t)in8(i + k) << (8 * k);
         return v;
     }
+    uint64_t in64u(int64_t i) const {  // the device reads these unchecked
+        if (i < 0 || i + 8 > n) abort();
+        return in64(i);
+    }
     void lit_put(uint64_t i, uint32_t b) const { lit[i] = (uint8_t)b; }
+    void lit_put4(uint32_t o0, uint32_t w0, uint32_t o1, uint32_t w1, uint32_t o2, uint32_t w2, uint32_t o3,
+                  uint32_t w3) const {
+        const uint32_t o[4] = {o0, o1, o2, o3}, w[4] = {w0, w1, w2, w3};
+        for (int j = 0; j < 4; j++)
+            for (int i = 0; i < 4; i++) lit[o[j] + i] = (uint8_t)(w[j] >> (8 * i));
+    }
     void lit_fill(uint64_t i, uint32_t b, uint64_t cnt) { memset(lit + i, (int)b, cnt); }
     void lit_sync() {}
     void stamp(int) {}
