@@ -58,10 +58,15 @@ constexpr uint32_t kHufLogMax = 12;          // HUF_TABLELOG_MAX
 constexpr uint32_t kMaxLL = 35, kMaxML = 52, kMaxOff = 31;
 constexpr uint32_t kLLLog = 9, kMLLog = 9, kOffLog = 8;
 
-struct SeqEnt {  // sequence FSE decoding entry (ZSTD_seqSymbol)
-    uint32_t base;
-    uint16_t next;
-    uint8_t nbBits, addBits;
+// sequence FSE decoding entry (ZSTD_seqSymbol), packed into 32 bits so the
+// tables take 5 KiB of LDS: next state base [8:0], state bits [12:9], extra
+// bits [17:13], value base as m << e in [23:18] and [27:24] (ML: + 3; OF:
+// 1 << extra bits, not stored)
+struct SeqEnt {
+    uint32_t v;
+};
+struct SeqDec {
+    uint32_t base, next, nbBits, addBits;
 };
 
 // Per-frame decoding state that persists across blocks; in LDS on the device.
@@ -268,21 +273,21 @@ ZD_HD inline bool fse_spread(Tables &t, uint32_t maxsv, uint32_t tlog) {
     return pos == 0;
 }
 
-// a table entry as wave-uniform values
-ZD_HD inline SeqEnt ld_seq(const SeqEnt *p) {
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(p);
-    const uint32_t a = ZD_U32(w[0]), b = ZD_U32(w[1]);
-    SeqEnt d;
-    d.base = a;
-    d.next = (uint16_t)(b & 0xffff);
-    d.nbBits = (uint8_t)((b >> 16) & 255);
-    d.addBits = (uint8_t)(b >> 24);
+// a table entry as wave-uniform values (kind: 0 LL, 1 ML, 2 OF)
+template <uint32_t KIND>
+ZD_HD inline SeqDec ld_seq(const SeqEnt *p) {
+    const uint32_t w = ZD_U32(p->v);
+    SeqDec d;
+    d.next = w & 511u;
+    d.nbBits = (w >> 9) & 15u;
+    d.addBits = (w >> 13) & 31u;
+    d.base = KIND == 2 ? 1u << d.addBits : (((w >> 18) & 63u) << ((w >> 24) & 15u)) + (KIND == 1 ? 3u : 0u);
     return d;
 }
 
 // sequence table from counts (ZSTD_buildFSETable) into dt[1 << tlog]
-ZD_HD inline uint32_t code_base(uint32_t kind, uint32_t s);
 ZD_HD inline uint32_t code_bits(uint32_t kind, uint32_t s);
+ZD_HD inline SeqEnt seq_pack(uint32_t kind, uint32_t s, uint32_t nb, uint32_t next);
 ZD_HD inline void build_seq(Tables &t, SeqEnt *dt, uint32_t maxsv, uint32_t tlog, uint32_t kind) {
     fse_spread(t, maxsv, tlog);
     const uint32_t size = 1u << tlog;
@@ -291,12 +296,7 @@ ZD_HD inline void build_seq(Tables &t, SeqEnt *dt, uint32_t maxsv, uint32_t tlog
         const uint32_t nx = ZD_U32(t.snext[s]);
         ZD_ONE(t.snext[s] = (uint16_t)(nx + 1));
         const uint32_t nb = tlog - highbit(nx);
-        SeqEnt d;
-        d.nbBits = (uint8_t)nb;
-        d.next = (uint16_t)((nx << nb) - size);
-        d.addBits = (uint8_t)code_bits(kind, s);
-        d.base = code_base(kind, s);
-        ZD_ONE(dt[u] = d);
+        ZD_ONE(dt[u] = seq_pack(kind, s, nb, (nx << nb) - size));
     }
 }
 
@@ -319,21 +319,29 @@ constexpr int16_t kMLDef[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 
                                 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
 constexpr int16_t kOFDef[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
 
-// code -> (base, extra bits); offset codes: base 1 << c, c bits (the offset
+// code -> extra bits (offset codes: c bits over a base of 1 << c, the offset
 // value before the repeat rules)
-ZD_HD inline uint32_t code_base(uint32_t kind, uint32_t s);
 ZD_HD inline uint32_t code_bits(uint32_t kind, uint32_t s);
 
 enum Kind : uint32_t { KLL = 0, KML = 1, KOF = 2 };
+
+ZD_HD inline SeqEnt seq_pack(uint32_t kind, uint32_t s, uint32_t nb, uint32_t next) {
+    // LL and ML - 3 bases are m << e with m < 64 exactly (kLLBase, kMLBase)
+    uint32_t m = kind == KLL ? kLLBase[s] : kind == KML ? kMLBase[s] - 3 : 0, e = 0;
+    while (m >= 64) {
+        m >>= 1;
+        e++;
+    }
+    SeqEnt d;
+    d.v = next | nb << 9 | code_bits(kind, s) << 13 | m << 18 | e << 24;
+    return d;
+}
 
 ZD_HD inline void kind_params(uint32_t kind, uint32_t &maxsv, uint32_t &maxlog) {
     maxsv = kind == KLL ? kMaxLL : kind == KML ? kMaxML : kMaxOff;
     maxlog = kind == KLL ? kLLLog : kind == KML ? kMLLog : kOffLog;
 }
 
-ZD_HD inline uint32_t code_base(uint32_t kind, uint32_t s) {
-    return kind == KLL ? kLLBase[s] : kind == KML ? kMLBase[s] : (1u << s);
-}
 ZD_HD inline uint32_t code_bits(uint32_t kind, uint32_t s) {
     return kind == KLL ? kLLBits[s] : kind == KML ? kMLBits[s] : s;
 }
@@ -358,12 +366,7 @@ ZD_HD int32_t seq_table(const Env &e, Tables &t, Mode &m, uint32_t kind, uint32_
         if (p >= end) return -1;
         const uint32_t s = e.in8(p);
         if (s > maxsv) return -1;
-        SeqEnt d;
-        d.base = code_base(kind, s);
-        d.addBits = (uint8_t)code_bits(kind, s);
-        d.nbBits = 0;
-        d.next = 0;
-        ZD_ONE(dt[0] = d);
+        ZD_ONE(dt[0] = seq_pack(kind, s, 0, 0));
         logr = 0;
         return 1;
     }
@@ -692,7 +695,7 @@ ZD_HD int32_t block(Env &e, Tables &t, Mode &m, int32_t p, int32_t n, uint32_t f
         uint32_t sl = (uint32_t)b.read(m.llLog), so = (uint32_t)b.read(m.ofLog), sm = (uint32_t)b.read(m.mlLog);
         for (uint32_t k = 0; k < nbSeq; k++) {
             if (b.rem < 0) return ZD_EFORMAT;  // BIT_reloadDStream overflow before a sequence
-            const SeqEnt dl = ld_seq(t.ll + sl), dm = ld_seq(t.ml + sm), dof = ld_seq(t.of + so);
+            const SeqDec dl = ld_seq<KLL>(t.ll + sl), dm = ld_seq<KML>(t.ml + sm), dof = ld_seq<KOF>(t.of + so);
             e.stamp(5);  // table reads
             const uint32_t ofc = dof.addBits;  // the offset takes ofc bits (1 for ofc == 1)
             const uint32_t ll0 = dl.base == 0 && dl.addBits == 0 ? 1u : 0u;
