@@ -73,12 +73,13 @@ struct SeqDec {
 struct Tables {
     uint16_t huf[1u << kHufLogMax];  // Huffman X1: symbol | nbBits << 8
     SeqEnt ll[1u << kLLLog], ml[1u << kMLLog], of[1u << kOffLog];
-    uint32_t fw[64];                 // Huffman-weight FSE table: sym | nb << 8 | next << 16
+    union {
+        uint32_t fw[64];                // Huffman-weight FSE table: sym | nb << 8 | next << 16
+        uint32_t rank[kHufLogMax + 2];  // then: Huffman weight counts, then rank starts
+    };
     uint8_t w[256];                  // Huffman weights
     int16_t norm[256];
     uint16_t snext[256];
-    uint8_t sym[1u << kLLLog];       // spread symbols
-    uint32_t rank[kHufLogMax + 2];   // Huffman weight counts, then rank starts
 };
 
 // Frame-to-frame state (registers): which tables the repeat modes reuse.
@@ -246,16 +247,17 @@ ZD_HD int32_t read_ncount(const Env &e, int32_t base, int32_t n, int16_t *norm, 
     return used;
 }
 
-// FSE spread of the symbols (FSE_buildDTable / ZSTD_buildFSETable): t.sym[u]
-// = symbol of state u, t.snext[s] = first "next state" of symbol s.  Returns
-// false when the spread does not close on position 0.
-ZD_HD inline bool fse_spread(Tables &t, uint32_t maxsv, uint32_t tlog) {
+// FSE spread of the symbols (FSE_buildDTable / ZSTD_buildFSETable): out[u]
+// = symbol of state u (the table being built, converted in place after),
+// t.snext[s] = first "next state" of symbol s.  Returns false when the
+// spread does not close on position 0.
+ZD_HD inline bool fse_spread(Tables &t, uint32_t *out, uint32_t maxsv, uint32_t tlog) {
     const uint32_t size = 1u << tlog;
     uint32_t high = size - 1;
     for (uint32_t s = 0; s <= maxsv; s++) {
         const int32_t ns = (int16_t)ZD_U32((uint16_t)t.norm[s]);
         if (ns == -1) {
-            ZD_ONE(t.sym[high] = (uint8_t)s);
+            ZD_ONE(out[high] = s);
             high--;
             ZD_ONE(t.snext[s] = 1);
         } else {
@@ -266,7 +268,7 @@ ZD_HD inline bool fse_spread(Tables &t, uint32_t maxsv, uint32_t tlog) {
     uint32_t pos = 0;
     for (uint32_t s = 0; s <= maxsv; s++)
         for (int32_t i = 0, ns = (int16_t)ZD_U32((uint16_t)t.norm[s]); i < ns; i++) {
-            ZD_ONE(t.sym[pos] = (uint8_t)s);
+            ZD_ONE(out[pos] = s);
             pos = (pos + step) & mask;
             while (pos > high) pos = (pos + step) & mask;
         }
@@ -289,10 +291,10 @@ ZD_HD inline SeqDec ld_seq(const SeqEnt *p) {
 ZD_HD inline uint32_t code_bits(uint32_t kind, uint32_t s);
 ZD_HD inline SeqEnt seq_pack(uint32_t kind, uint32_t s, uint32_t nb, uint32_t next);
 ZD_HD inline void build_seq(Tables &t, SeqEnt *dt, uint32_t maxsv, uint32_t tlog, uint32_t kind) {
-    fse_spread(t, maxsv, tlog);
+    fse_spread(t, &dt->v, maxsv, tlog);
     const uint32_t size = 1u << tlog;
     for (uint32_t u = 0; u < size; u++) {
-        const uint32_t s = ZD_U32(t.sym[u]);
+        const uint32_t s = ZD_U32(dt[u].v);
         const uint32_t nx = ZD_U32(t.snext[s]);
         ZD_ONE(t.snext[s] = (uint16_t)(nx + 1));
         const uint32_t nb = tlog - highbit(nx);
@@ -406,10 +408,10 @@ ZD_HD int32_t huf_table(const Env &e, Tables &t, int32_t p, int32_t n, uint32_t 
         uint32_t mx = 255, tlog;
         const int32_t hs = read_ncount(e, q, isize, t.norm, mx, tlog);
         if (hs < 0 || tlog > 6) return -1;
-        if (!fse_spread(t, mx, tlog)) return -1;
+        if (!fse_spread(t, t.fw, mx, tlog)) return -1;
         const uint32_t size = 1u << tlog;
         for (uint32_t u = 0; u < size; u++) {
-            const uint32_t s = ZD_U32(t.sym[u]);
+            const uint32_t s = ZD_U32(t.fw[u]);
             const uint32_t nx = ZD_U32(t.snext[s]);
             ZD_ONE(t.snext[s] = (uint16_t)(nx + 1));
             const uint32_t nb = tlog - highbit(nx);
