@@ -292,8 +292,10 @@ void launch_gen_synthetic_batch(hipStream_t s, uint8_t *dst, uint64_t stride, in
 constexpr size_t kLz4TabBytes = 16384;
 void launch_lz4_compress(hipStream_t s, int n, const ZDev *blks, ZOut *outs, uint32_t *tabs);
 void launch_lz4_decompress(hipStream_t s, int n, const ZDev *blks, ZOut *outs);
-// Zstandard frames (jfsx_zstd.hip): scratch = n x kZstdScratch bytes (literal buffers)
-constexpr size_t kZstdScratch = 128 * 1024 + 320;  // + the literal window's read-ahead
+// Zstandard frames (jfsx_zstd.hip): scratch = n x kZstdScratch bytes (literal
+// buffer + the literal window's read-ahead, then a log-12 Huffman table)
+constexpr size_t kZstdHufOff = 128 * 1024 + 320;
+constexpr size_t kZstdScratch = kZstdHufOff + 8192;
 void launch_zstd_decompress(hipStream_t s, int n, const ZDev *blks, ZOut *outs, uint8_t *scratch);
 // batched RSA-OAEP unwrap (jfsx_rsa.hip): key = device jfsx_rsa::Key
 void async_detach(jfsx_ctx *c);  // jfsx_agg.cpp

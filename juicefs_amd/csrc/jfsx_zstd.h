@@ -55,6 +55,7 @@ enum : int { ZD_OK = 0, ZD_EFORMAT = -1, ZD_EDSTSIZE = -2 };
 
 constexpr uint32_t kBlockMax = 128 * 1024;  // ZSTD_BLOCKSIZE_MAX
 constexpr uint32_t kHufLogMax = 12;          // HUF_TABLELOG_MAX
+constexpr uint32_t kHufLogTab = 11;          // larger tables (log 12) live in Env::huf_g()
 constexpr uint32_t kMaxLL = 35, kMaxML = 52, kMaxOff = 31;
 constexpr uint32_t kLLLog = 9, kMLLog = 9, kOffLog = 8;
 
@@ -71,7 +72,7 @@ struct SeqDec {
 
 // Per-frame decoding state that persists across blocks; in LDS on the device.
 struct Tables {
-    uint16_t huf[1u << kHufLogMax];  // Huffman X1: symbol | nbBits << 8
+    uint16_t huf[1u << kHufLogTab];  // Huffman X1: symbol | nbBits << 8 (log <= 11)
     SeqEnt ll[1u << kLLLog], ml[1u << kMLLog], of[1u << kOffLog];
     union {
         uint32_t fw[64];                // Huffman-weight FSE table: sym | nb << 8 | next << 16
@@ -485,60 +486,61 @@ ZD_HD int32_t huf_table(const Env &e, Tables &t, int32_t p, int32_t n, uint32_t 
         const uint32_t len = (1u << wv) >> 1;
         const uint16_t ent = (uint16_t)(s | ((tl + 1 - wv) << 8));
         const uint32_t st = ZD_U32(rank[wv]);
-        e.huf_fill(t.huf + st, ent, len);
+        e.huf_fill((tl <= kHufLogTab ? t.huf : e.huf_g()) + st, ent, len);
         ZD_ONE(rank[wv] = st + len);
     }
+    if (tl > kHufLogTab) e.huf_sync();
     hlog = tl;
     return isize + 1;
 }
 
 // Huffman symbols [k, cnt) of one stream into the literal buffer at o + k,
 // bit by bit (the tail of a stream, and over-reads past its start)
-template <class Env>
-ZD_HD void huf_tail(const Env &e, Tables &t, Bwd<Env> &b, uint32_t hlog, uint32_t o, uint32_t k, uint32_t cnt) {
+template <class Env, class H>
+ZD_HD void huf_tail(const Env &e, const H &h, Bwd<Env> &b, uint32_t hlog, uint32_t o, uint32_t k, uint32_t cnt) {
     for (; k < cnt; k++) {
-        const uint32_t ent = ZD_U32(t.huf[b.peek(hlog)]);
+        const uint32_t ent = h(b.peek(hlog));
         b.rem -= ent >> 8;
         e.lit_put(o + k, ent & 255);
     }
 }
 
 // one symbol from an ensure()d window: returns it, consumes its bits
-template <class Env>
-ZD_HD uint32_t huf_sym(const Tables &t, Bwd<Env> &b, uint32_t hlog) {
-    const uint32_t ent = ZD_U32(t.huf[(uint32_t)(b.cont >> ((uint32_t)(b.rem - (int32_t)hlog - b.cb * 8) & 63u)) &
-                                       ((1u << hlog) - 1u)]);
+template <class Env, class H>
+ZD_HD uint32_t huf_sym(const H &h, Bwd<Env> &b, uint32_t hlog) {
+    const uint32_t ent =
+        h((uint32_t)(b.cont >> ((uint32_t)(b.rem - (int32_t)hlog - b.cb * 8) & 63u)) & ((1u << hlog) - 1u));
     b.rem -= ent >> 8;
     return ent & 255;
 }
 
 // four symbols of one stream, packed little-endian (window ensure()d for 4 * hlog bits)
-template <class Env>
-ZD_HD uint32_t huf_sym4(const Tables &t, Bwd<Env> &b, uint32_t hlog) {
-    uint32_t w = huf_sym(t, b, hlog);
-    w |= huf_sym(t, b, hlog) << 8;
-    w |= huf_sym(t, b, hlog) << 16;
-    return w | huf_sym(t, b, hlog) << 24;
+template <class Env, class H>
+ZD_HD uint32_t huf_sym4(const H &h, Bwd<Env> &b, uint32_t hlog) {
+    uint32_t w = huf_sym(h, b, hlog);
+    w |= huf_sym(h, b, hlog) << 8;
+    w |= huf_sym(h, b, hlog) << 16;
+    return w | huf_sym(h, b, hlog) << 24;
 }
 
 // one Huffman stream [p, p + n) into the literal buffer [o, o + cnt)
-template <class Env>
-ZD_HD bool huf_stream(const Env &e, Tables &t, uint32_t hlog, int32_t p, int32_t n, uint32_t o, uint32_t cnt) {
+template <class Env, class H>
+ZD_HD bool huf_stream(const Env &e, const H &h, uint32_t hlog, int32_t p, int32_t n, uint32_t o, uint32_t cnt) {
     Bwd<Env> b;
     if (!bwd_init(b, e, p, n)) return false;
     uint32_t k = 0;
     for (; k + 4 <= cnt && b.ensure(4 * hlog); k += 4) {
-        const uint32_t w = huf_sym4(t, b, hlog);
+        const uint32_t w = huf_sym4(h, b, hlog);
         e.lit_put4(o + k, w, o + k, w, o + k, w, o + k, w);
     }
-    huf_tail(e, t, b, hlog, o, k, cnt);
+    huf_tail(e, h, b, hlog, o, k, cnt);
     return b.rem == 0;
 }
 
 // the four streams of a 4-stream literal section, decoded interleaved (four
 // independent table-lookup chains) into [0, seg), [seg, 2 seg), ...
-template <class Env>
-ZD_HD bool huf_streams4(const Env &e, Tables &t, uint32_t hlog, int32_t s1, int32_t l1, int32_t s2, int32_t l2,
+template <class Env, class H>
+ZD_HD bool huf_streams4(const Env &e, const H &h, uint32_t hlog, int32_t s1, int32_t l1, int32_t s2, int32_t l2,
                         int32_t s3, int32_t l3, int32_t s4, int32_t l4, uint32_t seg, uint32_t c4) {
     Bwd<Env> b0, b1, b2, b3;
     if (!bwd_init(b0, e, s1, l1) || !bwd_init(b1, e, s2, l2) || !bwd_init(b2, e, s3, l3) || !bwd_init(b3, e, s4, l4))
@@ -548,17 +550,17 @@ ZD_HD bool huf_streams4(const Env &e, Tables &t, uint32_t hlog, int32_t s1, int3
     for (; k + 4 <= c4 && b0.ensure(need) && b1.ensure(need) && b2.ensure(need) && b3.ensure(need); k += 4) {
         uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
         for (uint32_t i = 0; i < 4; i++) {
-            w0 |= huf_sym(t, b0, hlog) << (8 * i);
-            w1 |= huf_sym(t, b1, hlog) << (8 * i);
-            w2 |= huf_sym(t, b2, hlog) << (8 * i);
-            w3 |= huf_sym(t, b3, hlog) << (8 * i);
+            w0 |= huf_sym(h, b0, hlog) << (8 * i);
+            w1 |= huf_sym(h, b1, hlog) << (8 * i);
+            w2 |= huf_sym(h, b2, hlog) << (8 * i);
+            w3 |= huf_sym(h, b3, hlog) << (8 * i);
         }
         e.lit_put4(k, w0, seg + k, w1, 2 * seg + k, w2, 3 * seg + k, w3);
     }
-    huf_tail(e, t, b0, hlog, 0, k, seg);
-    huf_tail(e, t, b1, hlog, seg, k, seg);
-    huf_tail(e, t, b2, hlog, 2 * seg, k, seg);
-    huf_tail(e, t, b3, hlog, 3 * seg, k, c4);
+    huf_tail(e, h, b0, hlog, 0, k, seg);
+    huf_tail(e, h, b1, hlog, seg, k, seg);
+    huf_tail(e, h, b2, hlog, 2 * seg, k, seg);
+    huf_tail(e, h, b3, hlog, 3 * seg, k, c4);
     return b0.rem == 0 && b1.rem == 0 && b2.rem == 0 && b3.rem == 0;
 }
 
@@ -636,8 +638,13 @@ ZD_HD int32_t block(Env &e, Tables &t, Mode &m, int32_t p, int32_t n, uint32_t f
             q += hs;
             qn -= hs;
         }
+        // the Huffman table: LDS (log <= 11) or Env::huf_g() (log 12)
+        auto hufL = [&](uint32_t i) -> uint32_t { return ZD_U32(t.huf[i]); };
+        auto hufG = [&](uint32_t i) -> uint32_t { return e.huf_ld(i); };
         if (single) {
-            if (!huf_stream(e, t, m.hufLog, q, qn, 0, litSize)) return ZD_EFORMAT;
+            if (!(m.hufLog <= kHufLogTab ? huf_stream(e, hufL, m.hufLog, q, qn, 0, litSize)
+                                         : huf_stream(e, hufG, m.hufLog, q, qn, 0, litSize)))
+                return ZD_EFORMAT;
         } else {
             if (litSize == 0) return ZD_EFORMAT;
             if (qn < 10) return ZD_EFORMAT;
@@ -652,7 +659,9 @@ ZD_HD int32_t block(Env &e, Tables &t, Mode &m, int32_t p, int32_t n, uint32_t f
                 return ZD_EFORMAT;
             }
             const int32_t s1 = q + 6, s2 = s1 + l1, s3 = s2 + l2, s4 = s3 + l3;
-            if (!huf_streams4(e, t, m.hufLog, s1, l1, s2, l2, s3, l3, s4, l4, seg, litSize - 3 * seg))
+            if (!(m.hufLog <= kHufLogTab
+                      ? huf_streams4(e, hufL, m.hufLog, s1, l1, s2, l2, s3, l3, s4, l4, seg, litSize - 3 * seg)
+                      : huf_streams4(e, hufG, m.hufLog, s1, l1, s2, l2, s3, l3, s4, l4, seg, litSize - 3 * seg)))
                 return ZD_EFORMAT;
         }
         lused = lh + litC;

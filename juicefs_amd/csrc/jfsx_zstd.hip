@@ -110,6 +110,12 @@ struct DevEnv {
     __device__ __forceinline__ void huf_fill(uint16_t *p, uint16_t v, uint32_t cnt) const {
         for (uint32_t j = lane; j < cnt; j += 64) p[j] = v;
     }
+    // log-12 Huffman tables (none from libzstd's encoder): global scratch
+    __device__ __forceinline__ uint16_t *huf_g() const { return (uint16_t *)(lit + kZstdHufOff); }
+    __device__ __forceinline__ void huf_sync() const { fence(); }
+    __device__ __forceinline__ uint32_t huf_ld(uint32_t i) const {
+        return ZD_U32(*(const __attribute__((address_space(1))) uint16_t *)(lit + kZstdHufOff + 2 * i));
+    }
     __device__ __forceinline__ void out_sync() const { fence(); }
     __device__ __forceinline__ void out_from_in(uint32_t o, int32_t i, uint32_t cnt) const {
         for (uint32_t j = lane; j < cnt; j += 64) *(gu8z *)(dst + o + j) = (uint8_t)in8_v(i + (int32_t)j);

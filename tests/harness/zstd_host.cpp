@@ -32,9 +32,13 @@ struct HostEnv {
     void lit_fill(uint64_t i, uint32_t b, uint64_t cnt) { memset(lit + i, (int)b, cnt); }
     void lit_sync() {}
     void stamp(int) {}
+    uint16_t *hufg;
     void huf_fill(uint16_t *p, uint16_t v, uint32_t cnt) const {
         for (uint32_t j = 0; j < cnt; j++) p[j] = v;
     }
+    uint16_t *huf_g() const { return hufg; }
+    void huf_sync() const {}
+    uint32_t huf_ld(uint32_t i) const { return hufg[i]; }
     void out_sync() {}
     void out_from_in(uint64_t o, int64_t i, uint64_t cnt) { memcpy(dst + o, src + i, cnt); }
     void out_from_lit(uint64_t o, uint64_t i, uint64_t cnt) { memcpy(dst + o, lit + i, cnt); }
@@ -53,7 +57,8 @@ struct HostEnv {
 extern "C" int64_t zstd_host_decompress(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap) {
     static thread_local jzd::Tables t;
     std::vector<uint8_t> litbuf(jzd::kBlockMax + 64);
-    HostEnv e{src, n, dst, litbuf.data()};
+    std::vector<uint16_t> hufbuf(1u << jzd::kHufLogMax);
+    HostEnv e{src, n, dst, litbuf.data(), hufbuf.data()};
     // out64 may read up to 7 bytes past the output: decode into a padded copy
     std::vector<uint8_t> pad((size_t)cap + 8);
     e.dst = pad.data();
