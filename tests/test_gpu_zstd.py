@@ -171,3 +171,21 @@ def test_per_block_calls_through_the_aggregator_and_mctx():
         assert all(arr[i].status == E.OK and outs[i].tobytes() == srcs[i] for i in range(T))
     finally:
         m.close()
+
+
+def test_log12_huffman_table(eng):
+    """Log-12 Huffman tables (read from global scratch, not LDS), one and
+    four streams, beside log-11 frames in the same batch."""
+    rng = np.random.default_rng(12)
+    frames, want = [], []
+    for four in (False, True):
+        for n in (4, 37, 200, 255):
+            syms = bytes(int(x) for x in rng.integers(0, 14, n))
+            frames.append(zstd_lib.huf12_frame(list(syms), four))
+            want.append(syms)
+            src = lz4_data.sample("text", 5000 + n, seed=n)
+            frames.append(zstd_lib.compress(src, 1))
+            want.append(src)
+    got = eng.zstd_decompress(frames, [1000 if len(w) < 256 else len(w) for w in want])
+    for i, (w, (st, d)) in enumerate(zip(want, got)):
+        assert st == E.OK and d == w, i

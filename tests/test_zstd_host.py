@@ -88,3 +88,16 @@ def test_malformed_agrees_with_library(host):
         else:
             assert got == ref, (trial, kind, n, m, cap)
     assert rejects > 1000
+
+
+def test_log12_huffman_table(host):
+    """Literals under a log-12 Huffman table: the decoder keeps tables up to
+    log 11 in LDS and reads log-12 ones from global scratch."""
+    rng = np.random.default_rng(12)
+    for four in (False, True):
+        for n in (4, 37, 200, 255):
+            syms = [int(x) for x in rng.integers(0, 14, n)]
+            fr = zstd_lib.huf12_frame(syms, four)
+            want = zstd_lib.decompress(fr, 1000)
+            assert want == (n, bytes(syms)), (four, n, want[0])
+            assert host(fr, 1000) == want

@@ -62,3 +62,40 @@ def decompress(frame, cap):
 def skippable(payload, nibble=0):
     """A skippable frame (magic 0x184D2A50 + nibble) carrying payload."""
     return (0x184D2A50 + nibble).to_bytes(4, "little") + len(payload).to_bytes(4, "little") + bytes(payload)
+
+
+def huf12_frame(syms, four):
+    """A frame whose only block holds Huffman-coded literals (no sequences)
+    under a log-12 table: weights 11, 11, 11, 10, ..., 1 for symbols 0..12
+    and an implied 1 for symbol 13 (codes of 2 to 12 bits).  libzstd's
+    encoder never writes log 12; its decoder takes it (HUF_TABLELOG_MAX 12).
+    syms: values 0..13, 4..255 of them; four: four streams (else one)."""
+    w = [11, 11, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1, 1]
+    code, start = {}, 0
+    for wv in range(1, 12):  # X1 layout: by weight, then symbol
+        for s, ws in enumerate(w):
+            if ws == wv:
+                nb = 13 - wv
+                code[s] = format(start >> (12 - nb), "0%db" % nb)
+                start += 1 << (wv - 1)
+    assert start == 4096
+
+    def stream(part):
+        bits = "".join(code[s] for s in part)
+        v = (1 << len(bits)) | (int(bits, 2) if bits else 0)
+        return v.to_bytes((len(bits) + 8) // 8, "little")
+
+    n = len(syms)
+    ew = w[:-1] + [0]
+    tree = bytes([127 + 13]) + bytes((ew[k] << 4) | ew[k + 1] for k in range(0, 14, 2))
+    if four:
+        seg = (n + 3) // 4
+        parts = [stream(syms[k * seg:(k + 1) * seg]) for k in range(3)] + [stream(syms[3 * seg:])]
+        body = b"".join(len(p).to_bytes(2, "little") for p in parts[:3]) + b"".join(parts)
+    else:
+        body = stream(syms)
+    litc = len(tree) + len(body)
+    lh = 2 | ((1 if four else 0) << 2) | (n << 4) | (litc << 14)
+    block = lh.to_bytes(3, "little") + tree + body + b"\x00"
+    bh = (len(block) << 3) | (2 << 1) | 1
+    return b"\x28\xb5\x2f\xfd" + bytes([0x20, n]) + bh.to_bytes(3, "little") + block
