@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define JFSX_ABI_VERSION 5
+#define JFSX_ABI_VERSION 6
 
 /* algorithms (encrypt.go:142-145) */
 #define JFSX_AES256GCM 0     /* "aes256gcm-rsa" (also the "" default)   */
@@ -72,7 +72,8 @@ extern "C" {
 #define JFSX_ETAG 1 /* AEAD authentication failed (Go: cipher's errOpen)      */
 #define JFSX_ECRC 2 /* "data checksum %d != expect %d" (disk_cache.go:1324)   */
 #define JFSX_EOF 3  /* jfsx_cache_verify: short read (File.ReadAt's io.EOF)    */
-#define JFSX_EFORMAT 4 /* malformed LZ4 block (lz4.DecompressSafe's error)      */
+#define JFSX_EFORMAT 4 /* malformed LZ4 block / zstd frame (the library's error) */
+#define JFSX_EDSTSIZE 5 /* zstd: the frames decode to more than dst_cap bytes */
 
 /* batch-level errors */
 #define JFSX_EINVAL (-22)
@@ -123,6 +124,16 @@ typedef struct jfsx_range {
 
 int jfsx_abi_version(void);
 int jfsx_device_count(int *n);
+
+/* Diagnostics for a batch-level JFSX_EIO / JFSX_ENOMEM: the HIP failure behind
+ * it, as its hipError_t value and "name (text) at file:line in call", for the
+ * calls made on ctx (from any thread, the aggregator's dispatchers and the
+ * async queue's worker included) or, with ctx NULL, for the calling thread.
+ * hip_error 0 and an empty msg when none was recorded; a newer failure
+ * replaces an older one.  A sticky device fault (hipErrorIllegalAddress and
+ * the like) leaves the context unusable: close it and fall back.  The Go shim
+ * logs this text before it falls back to the CPU path. */
+int jfsx_last_error(jfsx_ctx *ctx, int *hip_error, char *msg, size_t cap);
 
 /* context = one GPU + one HIP stream + device workspace + pinned staging.
  * flags: 0, or JFSX_CTX_BITSLICE: AES-256-GCM computes the keystream of whole
@@ -326,8 +337,9 @@ int jfsx_mctx_lz4_decompress_batch(jfsx_mctx *m, int n, jfsx_zblk *blks, int mem
  * out_len = decoded bytes; status JFSX_EFORMAT where ZSTD_decompress returns
  * an error (malformed frame, dictionary id, checksum mismatch, or output
  * larger than dst_cap); dst_cap < 2^31, src_len <= 0x7E000000 (JFSX_EINVAL
- * otherwise).  Compression ("zstd" Compress, level 1) stays on the host's
- * libzstd. */
+ * otherwise).  A frame that is well formed as far as it was decoded but does
+ * not fit in dst_cap gets JFSX_EDSTSIZE (ZSTD_decompress's
+ * dstSize_tooSmall): the caller can retry with the frame content size. */
 int jfsx_zstd_decompress_batch(jfsx_ctx *ctx, int n, jfsx_zblk *blks, int mem);
 /* per block through the aggregator, and over a multi-device context */
 int jfsx_agg_zstd_decompress(jfsx_agg *agg, jfsx_zblk *blk, int mem);

@@ -319,6 +319,12 @@ int agg_start(std::vector<jfsx_ctx *> cs, int max_blocks, uint64_t max_bytes, ui
     *out = a;
     return 0;
 }
+// device pointers belong to one GPU: over a multi-device context any
+// dispatcher may take a group, so only host memory is accepted there (as the
+// jfsx_mctx_*_batch entry points do)
+bool agg_mem_ok(const jfsx_agg *a, int mem) {
+    return valid_mem(mem) && !(mem == JFSX_MEM_DEVICE && a->cs.size() > 1);
+}
 }  // namespace
 
 extern "C" {
@@ -349,37 +355,37 @@ int jfsx_agg_dev_batches(jfsx_agg *a, int i, uint64_t *batches) {
 }
 
 int jfsx_agg_seal(jfsx_agg *a, int algo, jfsx_blk *blk, int crc_mode, int mem) {
-    if (!a || !blk || !valid_algo(algo) || !valid_mem(mem)) return JFSX_EINVAL;
+    if (!a || !blk || !valid_algo(algo) || !agg_mem_ok(a, mem)) return JFSX_EINVAL;
     Req r{kSeal, algo, crc_mode, mem, blk, nullptr, nullptr, blk->len};
     return a->submit(r);
 }
 
 int jfsx_agg_open(jfsx_agg *a, int algo, jfsx_blk *blk, int crc_mode, int mem) {
-    if (!a || !blk || !valid_algo(algo) || !valid_mem(mem)) return JFSX_EINVAL;
+    if (!a || !blk || !valid_algo(algo) || !agg_mem_ok(a, mem)) return JFSX_EINVAL;
     Req r{kOpen, algo, crc_mode, mem, blk, nullptr, nullptr, blk->len};
     return a->submit(r);
 }
 
 int jfsx_agg_crc32c(jfsx_agg *a, jfsx_range *range, int mode, int mem) {
-    if (!a || !range || !valid_mem(mem) || (mode != JFSX_CRC_GEN && mode != JFSX_CRC_VERIFY)) return JFSX_EINVAL;
+    if (!a || !range || !agg_mem_ok(a, mem) || (mode != JFSX_CRC_GEN && mode != JFSX_CRC_VERIFY)) return JFSX_EINVAL;
     Req r{kCrc, 0, mode, mem, nullptr, range, nullptr, range->len};
     return a->submit(r);
 }
 
 int jfsx_agg_lz4_compress(jfsx_agg *a, jfsx_zblk *z, int mem) {
-    if (!a || !z || !valid_mem(mem)) return JFSX_EINVAL;
+    if (!a || !z || !agg_mem_ok(a, mem)) return JFSX_EINVAL;
     Req r{kLz4c, 0, 0, mem, nullptr, nullptr, z, z->src_len};
     return a->submit(r);
 }
 
 int jfsx_agg_lz4_decompress(jfsx_agg *a, jfsx_zblk *z, int mem) {
-    if (!a || !z || !valid_mem(mem)) return JFSX_EINVAL;
+    if (!a || !z || !agg_mem_ok(a, mem)) return JFSX_EINVAL;
     Req r{kLz4d, 0, 0, mem, nullptr, nullptr, z, z->dst_cap};
     return a->submit(r);
 }
 
 int jfsx_agg_zstd_decompress(jfsx_agg *a, jfsx_zblk *z, int mem) {
-    if (!a || !z || !valid_mem(mem)) return JFSX_EINVAL;
+    if (!a || !z || !agg_mem_ok(a, mem)) return JFSX_EINVAL;
     Req r{kZstdd, 0, 0, mem, nullptr, nullptr, z, z->dst_cap};
     return a->submit(r);
 }

@@ -18,12 +18,43 @@
 
 using namespace jfsx;
 
-#define HIP_OK(x)                                      \
-    do {                                               \
-        if ((x) != hipSuccess) return JFSX_EIO;        \
+// Every HIP failure is recorded with its call site before the engine returns
+// JFSX_EIO, so a caller can tell a device fault from an out-of-resources
+// launch or a bad copy (jfsx_last_error).
+#define HIP_OK(x)                                                      \
+    do {                                                               \
+        const hipError_t e_ = (x);                                     \
+        if (e_ != hipSuccess) {                                        \
+            note_hip_error(e_, __FILE__, __LINE__, #x);                \
+            return JFSX_EIO;                                           \
+        }                                                              \
     } while (0)
 
 namespace {
+
+// last failure: per calling thread, and per context for calls made on one
+struct ErrRec {
+    int hip = 0;
+    char msg[320] = {0};
+};
+thread_local ErrRec tl_err;
+thread_local jfsx_ctx *tl_ctx = nullptr;  // context of the entry point running on this thread
+void note_ctx_error(jfsx_ctx *c, const ErrRec &e);
+
+void note_hip_error(hipError_t e, const char *file, int line, const char *expr) {
+    const char *base = strrchr(file, '/');
+    snprintf(tl_err.msg, sizeof(tl_err.msg), "%s (%s) at %s:%d in %s", hipGetErrorName(e), hipGetErrorString(e),
+             base ? base + 1 : file, line, expr);
+    tl_err.hip = (int)e;
+    if (tl_ctx) note_ctx_error(tl_ctx, tl_err);
+}
+
+// an entry point's scope: failures inside it are also kept on the context
+struct CtxScope {
+    jfsx_ctx *prev;
+    explicit CtxScope(jfsx_ctx *c) : prev(tl_ctx) { tl_ctx = c; }
+    ~CtxScope() { tl_ctx = prev; }
+};
 
 // ---------------------------------------------------------------------------
 // table construction (host)
@@ -165,7 +196,16 @@ struct jfsx_ctx {
     std::mutex arena_mu;     // cache-verify staging (jfsx_cache_verify)
     char *arena = nullptr;   // pinned, grow-only
     size_t arena_cap = 0;
+    std::mutex err_mu;       // last HIP failure on this context (jfsx_last_error)
+    ErrRec err;
 };
+
+namespace {
+void note_ctx_error(jfsx_ctx *c, const ErrRec &e) {
+    std::lock_guard<std::mutex> g(c->err_mu);
+    c->err = e;
+}
+}  // namespace
 
 namespace {
 
@@ -179,7 +219,11 @@ int ensure_dev(jfsx_ctx *c, char **buf, size_t *cap, size_t need) {
     }
     size_t n = std::max(need, (size_t)1 << 20);
     n = (n + 0xFFFFF) & ~(size_t)0xFFFFF;
-    if (hipMalloc((void **)buf, n) != hipSuccess) return JFSX_ENOMEM;
+    const hipError_t e = hipMalloc((void **)buf, n);
+    if (e != hipSuccess) {
+        note_hip_error(e, __FILE__, __LINE__, "hipMalloc(workspace)");
+        return JFSX_ENOMEM;
+    }
     *cap = n;
     return 0;
 }
@@ -194,7 +238,11 @@ int ensure_host(char **buf, size_t *cap, size_t need) {
     }
     size_t n = std::max(need, (size_t)1 << 20);
     n = (n + 0xFFFFF) & ~(size_t)0xFFFFF;
-    if (hipHostMalloc((void **)buf, n, hipHostMallocDefault) != hipSuccess) return JFSX_ENOMEM;
+    const hipError_t e = hipHostMalloc((void **)buf, n, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        note_hip_error(e, __FILE__, __LINE__, "hipHostMalloc(staging)");
+        return JFSX_ENOMEM;
+    }
     *cap = n;
     return 0;
 }
@@ -789,6 +837,22 @@ extern "C" {
 
 int jfsx_abi_version(void) { return JFSX_ABI_VERSION; }
 
+int jfsx_last_error(jfsx_ctx *c, int *hip_error, char *msg, size_t cap) {
+    ErrRec e;
+    if (c) {
+        std::lock_guard<std::mutex> g(c->err_mu);
+        e = c->err;
+    } else {
+        e = tl_err;
+    }
+    if (hip_error) *hip_error = e.hip;
+    if (msg && cap) {
+        strncpy(msg, e.msg, cap - 1);
+        msg[cap - 1] = 0;
+    }
+    return 0;
+}
+
 int jfsx_device_count(int *n) {
     if (!n) return JFSX_EINVAL;
     if (hipGetDeviceCount(n) != hipSuccess) {
@@ -876,6 +940,7 @@ int jfsx_ctx_close(jfsx_ctx *c) {
 
 int jfsx_ctx_sync(jfsx_ctx *c) {
     if (!c) return JFSX_EINVAL;
+    CtxScope es_(c);
     HIP_OK(hipStreamSynchronize(c->stream));
     HIP_OK(hipStreamSynchronize(c->s_in));
     HIP_OK(hipStreamSynchronize(c->s_out));
@@ -885,6 +950,7 @@ int jfsx_ctx_sync(jfsx_ctx *c) {
 int jfsx_ctx_set_slot_bytes(jfsx_ctx *c, uint64_t bytes) {
     if (!c || bytes < (1u << 20)) return JFSX_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
+    CtxScope es_(c);
     c->slot_bytes = (size_t)bytes;
     return 0;
 }
@@ -894,6 +960,7 @@ void *jfsx_ctx_stream(jfsx_ctx *c) { return c ? (void *)c->stream : nullptr; }
 int jfsx_ctx_set_timing(jfsx_ctx *c, int enable) {
     if (!c) return JFSX_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
+    CtxScope es_(c);
     c->timing = enable != 0;
     return 0;
 }
@@ -901,6 +968,7 @@ int jfsx_ctx_set_timing(jfsx_ctx *c, int enable) {
 int jfsx_ctx_kernel_time(jfsx_ctx *c, double *ms_total, uint64_t *launches, int reset) {
     if (!c) return JFSX_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
+    CtxScope es_(c);
     if (ms_total) *ms_total = c->ms_total;
     if (launches) *launches = c->launches;
     if (reset) {
@@ -912,9 +980,13 @@ int jfsx_ctx_kernel_time(jfsx_ctx *c, double *ms_total, uint64_t *launches, int 
 
 int jfsx_alloc_pinned(jfsx_ctx *c, size_t bytes, void **p) {
     if (!c || !p) return JFSX_EINVAL;
+    CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
     // portable: the multi-device context's other GPUs DMA from it as well
-    return hipHostMalloc(p, bytes, hipHostMallocPortable) == hipSuccess ? 0 : JFSX_ENOMEM;
+    const hipError_t e = hipHostMalloc(p, bytes, hipHostMallocPortable);
+    if (e == hipSuccess) return 0;
+    note_hip_error(e, __FILE__, __LINE__, "hipHostMalloc(pinned)");
+    return JFSX_ENOMEM;
 }
 int jfsx_free_pinned(jfsx_ctx *c, void *p) {
     if (!c) return JFSX_EINVAL;
@@ -923,8 +995,12 @@ int jfsx_free_pinned(jfsx_ctx *c, void *p) {
 }
 int jfsx_alloc_device(jfsx_ctx *c, size_t bytes, void **p) {
     if (!c || !p) return JFSX_EINVAL;
+    CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
-    return hipMalloc(p, bytes) == hipSuccess ? 0 : JFSX_ENOMEM;
+    const hipError_t e = hipMalloc(p, bytes);
+    if (e == hipSuccess) return 0;
+    note_hip_error(e, __FILE__, __LINE__, "hipMalloc(device buffer)");
+    return JFSX_ENOMEM;
 }
 int jfsx_free_device(jfsx_ctx *c, void *p) {
     if (!c) return JFSX_EINVAL;
@@ -934,6 +1010,7 @@ int jfsx_free_device(jfsx_ctx *c, void *p) {
 int jfsx_memcpy_h2d(jfsx_ctx *c, void *dst, const void *src, size_t bytes) {
     if (!c) return JFSX_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
+    CtxScope es_(c);
     HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
     return 0;
@@ -941,6 +1018,7 @@ int jfsx_memcpy_h2d(jfsx_ctx *c, void *dst, const void *src, size_t bytes) {
 int jfsx_memcpy_d2h(jfsx_ctx *c, void *dst, const void *src, size_t bytes) {
     if (!c) return JFSX_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
+    CtxScope es_(c);
     HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(hipStreamSynchronize(c->stream));
     return 0;
@@ -949,6 +1027,7 @@ int jfsx_memcpy_d2h(jfsx_ctx *c, void *dst, const void *src, size_t bytes) {
 int jfsx_seal_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *blks, int crc_mode, int mem) {
     if (!c || (n > 0 && !blks)) return JFSX_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
+    CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
     return mem == JFSX_MEM_HOST ? run_aead_host(c, algo, false, n, blks, crc_mode)
                                 : run_aead(c, algo, false, n, blks, crc_mode);
@@ -957,6 +1036,7 @@ int jfsx_seal_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *blks, int crc_mode, 
 int jfsx_open_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *blks, int crc_mode, int mem) {
     if (!c || (n > 0 && !blks)) return JFSX_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
+    CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
     return mem == JFSX_MEM_HOST ? run_aead_host(c, algo, true, n, blks, crc_mode)
                                 : run_aead(c, algo, true, n, blks, crc_mode);
@@ -965,6 +1045,7 @@ int jfsx_open_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *blks, int crc_mode, 
 int jfsx_crc32c_segments(jfsx_ctx *c, int n, jfsx_range *ranges, int mode, int mem) {
     if (!c || (n > 0 && !ranges)) return JFSX_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
+    CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
     return mem == JFSX_MEM_HOST ? run_crc_host(c, n, ranges, mode) : run_crc(c, n, ranges, mode);
 }
@@ -974,6 +1055,7 @@ uint64_t jfsx_lz4_bound(uint64_t n) { return lz4_bound(n); }
 int jfsx_lz4_compress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
     if (!c || (n > 0 && !blks)) return JFSX_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
+    CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
     return run_lz4(c, n, blks, mem, true);
 }
@@ -981,6 +1063,7 @@ int jfsx_lz4_compress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
 int jfsx_lz4_decompress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
     if (!c || (n > 0 && !blks)) return JFSX_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
+    CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
     return run_lz4(c, n, blks, mem, false);
 }
@@ -988,6 +1071,7 @@ int jfsx_lz4_decompress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
 int jfsx_zstd_decompress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
     if (!c || (n > 0 && !blks)) return JFSX_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
+    CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
     return run_lz4(c, n, blks, mem, false, true);
 }
@@ -1083,6 +1167,7 @@ int jfsx_cache_verify(jfsx_ctx *c, const void *file, uint64_t file_size, uint64_
                 int e;
                 {
                     std::lock_guard<std::mutex> g(c->mu);
+    CtxScope es_(c);
                     HIP_OK(hipSetDevice(c->device));
                     if ((e = ensure_host(&c->arena, &c->arena_cap, clen))) return e;
                 }
@@ -1262,6 +1347,7 @@ int jfsx_data_decrypt(jfsx_ctx *c, int algo, const uint8_t key[32], const void *
 int jfsx_gen_synthetic(jfsx_ctx *c, void *dst, uint64_t len, uint64_t seed, uint64_t block) {
     if (!c || (len && !dst) || !aligned16(dst)) return JFSX_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
+    CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
     if (len) launch_gen_synthetic(c->stream, (uint8_t *)dst, len, seed, block);
     HIP_OK(hipGetLastError());
@@ -1275,6 +1361,7 @@ int jfsx_gen_synthetic_batch(jfsx_ctx *c, void *dst, uint64_t stride, int n, con
         if (lens[i] > stride && n > 1) return JFSX_EINVAL;
     if (n == 0) return 0;
     std::lock_guard<std::mutex> g(c->mu);
+    CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
     Workspace &w = c->ws[0];
     int rc;
@@ -1333,6 +1420,7 @@ int jfsx_rsa_key_new(jfsx_ctx *c, const uint8_t *p, const uint8_t *q, const uint
     const uint8_t empty = 0;
     if (!jfsx_rsa::key_setup(k, p, q, dp, dq, qinv, label_len ? label : &empty, label_len)) return JFSX_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
+    CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
     jfsx_rsa_key *rk = new jfsx_rsa_key();
     rk->device = c->device;
@@ -1367,6 +1455,7 @@ int jfsx_rsa_oaep_decrypt_batch(jfsx_ctx *c, const jfsx_rsa_key *k, int n, const
                  o_len = o_em + align256(K * n), dbytes = o_len + align256(4 * (size_t)n);
     const size_t hbytes = align256(K * n) + align256(4 * (size_t)n);
     std::lock_guard<std::mutex> g(c->mu);
+    CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
     int rc;
     if ((rc = ensure_dev(c, &c->rsa_d, &c->rsa_dcap, dbytes))) return rc;

@@ -825,13 +825,15 @@ ZD_HD uint64_t xxh64(const Env &e, uint32_t fo, uint32_t len) {
         h ^= xround(0, e.out64(fo + i));
         h = rotl64(h, 27) * P1 + P4;
     }
+    // the tail reads only bytes below fo + len (the output may end at the
+    // end of its allocation)
     if (i + 4 <= len) {
-        h ^= (uint64_t)(uint32_t)e.out64(fo + i) * P1;
+        h ^= (uint64_t)e.out32(fo + i) * P1;
         h = rotl64(h, 23) * P2 + P3;
         i += 4;
     }
     for (; i < len; i++) {
-        h ^= (e.out64(fo + i) & 255) * P5;
+        h ^= (uint64_t)e.out8(fo + i) * P5;
         h = rotl64(h, 11) * P1;
     }
     h ^= h >> 33;

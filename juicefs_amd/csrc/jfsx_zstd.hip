@@ -165,6 +165,12 @@ struct DevEnv {
         for (uint32_t k = 0; k < 8; k++) v |= (uint64_t)(*(gcu8z *)(dst + o + k)) << (8 * k);
         return v;
     }
+    __device__ __forceinline__ uint32_t out32(uint32_t o) const {
+        uint32_t v = 0;
+        for (uint32_t k = 0; k < 4; k++) v |= (uint32_t)(*(gcu8z *)(dst + o + k)) << (8 * k);
+        return v;
+    }
+    __device__ __forceinline__ uint32_t out8(uint32_t o) const { return *(gcu8z *)(dst + o); }
 };
 
 }  // namespace
@@ -185,7 +191,8 @@ namespace jfsx {
 
 // One wave per object.  ZDev.len = compressed bytes, ZDev.cap = dst capacity;
 // ZOut.out_len = decoded bytes, status JFSX_EFORMAT for a frame
-// ZSTD_decompress rejects (or one that does not fit in cap).
+// ZSTD_decompress rejects, JFSX_EDSTSIZE for one whose output does not fit in
+// cap (ZSTD_decompress's dstSize_tooSmall).
 __global__ __launch_bounds__(64) void zstd_decompress_k(const ZDev *__restrict__ blks, ZOut *__restrict__ outs,
                                                         uint8_t *__restrict__ scratch) {
     __shared__ jzd::Tables T;
@@ -202,7 +209,7 @@ __global__ __launch_bounds__(64) void zstd_decompress_k(const ZDev *__restrict__
 #endif
     if (threadIdx.x == 0) {
         outs[blockIdx.x].out_len = r < 0 ? 0 : (uint64_t)r;
-        outs[blockIdx.x].status = r < 0 ? JFSX_EFORMAT : JFSX_OK;
+        outs[blockIdx.x].status = r >= 0 ? JFSX_OK : r == jzd::ZD_EDSTSIZE ? JFSX_EDSTSIZE : JFSX_EFORMAT;
     }
 }
 

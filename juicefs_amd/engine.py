@@ -21,7 +21,8 @@ CTX_BITSLICE = 1  # context flag: AES-GCM keystream from the bitsliced AES (VALU
 MEM_DEVICE, MEM_HOST = 0, 1
 OK, ETAG, ECRC = 0, 1, 2
 EOF = 3  # jfsx_cache_verify: short read
-EFORMAT = 4  # malformed LZ4 block (lz4.DecompressSafe error)
+EFORMAT = 4  # malformed LZ4 block / zstd frame (the library's error)
+EDSTSIZE = 5  # zstd: the output does not fit in dst_cap
 EINVAL, ENODEV, EIO, ENOMEM, EMISFORMED, EAGAIN = -22, -19, -5, -12, -74, -11
 SEG = 32 << 10
 
@@ -41,13 +42,35 @@ EXPORTS = [
     "jfsx_agg_dev_batches", "jfsx_lz4_bound", "jfsx_lz4_compress_batch", "jfsx_lz4_decompress_batch",
     "jfsx_agg_lz4_compress", "jfsx_agg_lz4_decompress", "jfsx_mctx_lz4_compress_batch", "jfsx_mctx_lz4_decompress_batch",
     "jfsx_zstd_decompress_batch", "jfsx_agg_zstd_decompress", "jfsx_mctx_zstd_decompress_batch",
+    "jfsx_last_error",
 ]
 
 
 class EngineError(RuntimeError):
-    def __init__(self, code, what):
-        super().__init__("%s failed: jfsx error %d" % (what, code))
+    """A batch-level failure; for JFSX_EIO / JFSX_ENOMEM the message carries
+    the HIP error and call site the engine recorded (jfsx_last_error)."""
+
+    def __init__(self, code, what, hip_error=0, detail=""):
+        msg = "%s failed: jfsx error %d" % (what, code)
+        if detail:
+            msg += " [%s]" % detail
+        super().__init__(msg)
         self.code = code
+        self.hip_error = hip_error
+        self.detail = detail
+
+
+def last_error(ctx=None):
+    """(hipError_t value, text) of the last HIP failure on ctx (None: this thread)."""
+    e = ctypes.c_int()
+    buf = ctypes.create_string_buffer(320)
+    load_library().jfsx_last_error(ctx, ctypes.byref(e), buf, len(buf))
+    return e.value, buf.value.decode(errors="replace")
+
+
+def _raise(ctx, rc, what):
+    he, txt = last_error(ctx) if rc in (EIO, ENOMEM) else (0, "")
+    raise EngineError(rc, what, he, txt)
 
 
 class jfsx_blk(ctypes.Structure):
@@ -92,6 +115,7 @@ def load_library(path=LIB_PATH):
         PP = ctypes.POINTER(ctypes.c_void_p)
         sig = {
             "jfsx_abi_version": (I, []),
+            "jfsx_last_error": (I, [P, ctypes.POINTER(I), ctypes.c_char_p, SZ]),
             "jfsx_device_count": (I, [ctypes.POINTER(I)]),
             "jfsx_ctx_open": (I, [I, U32, PP]),
             "jfsx_ctx_close": (I, [P]),
@@ -274,7 +298,11 @@ class Engine:
 
     def _check(self, rc, what):
         if rc:
-            raise EngineError(rc, what)
+            _raise(self.ctx, rc, what)
+
+    def last_error(self):
+        """(hipError_t, text) of the last HIP failure on this context."""
+        return last_error(self.ctx)
 
     # -- memory ----------------------------------------------------------
     def alloc(self, nbytes):
@@ -600,7 +628,7 @@ class MultiEngine:
 
     def _check(self, rc, what):
         if rc:
-            raise EngineError(rc, what)
+            _raise(None, rc, what)
 
     def seal_batch(self, algo, blks, n, crc_mode=CRC_GEN, mem=MEM_HOST):
         self._check(self.L.jfsx_mctx_seal_batch(self.m, algo, n, blks, crc_mode, mem), "jfsx_mctx_seal_batch")

@@ -51,6 +51,12 @@ struct HostEnv {
         memcpy(&v, dst + o, 8);
         return v;
     }
+    uint32_t out32(uint64_t o) const {
+        uint32_t v;
+        memcpy(&v, dst + o, 4);
+        return v;
+    }
+    uint32_t out8(uint64_t o) const { return dst[o]; }
 };
 }  // namespace
 
@@ -59,10 +65,11 @@ extern "C" int64_t zstd_host_decompress(const uint8_t *src, int64_t n, uint8_t *
     std::vector<uint8_t> litbuf(jzd::kBlockMax + 64);
     std::vector<uint16_t> hufbuf(1u << jzd::kHufLogMax);
     HostEnv e{src, n, dst, litbuf.data(), hufbuf.data()};
-    // out64 may read up to 7 bytes past the output: decode into a padded copy
-    std::vector<uint8_t> pad((size_t)cap + 8);
-    e.dst = pad.data();
+    // decode into an exactly sized heap copy, so ASan builds of this harness
+    // see any read past the output's end
+    std::vector<uint8_t> out((size_t)cap);
+    e.dst = out.data();
     const int64_t r = jzd::decompress(e, t, (uint64_t)n, (uint64_t)cap);
-    if (r > 0) memcpy(dst, pad.data(), (size_t)r);
+    if (r > 0) memcpy(dst, out.data(), (size_t)r);
     return r;
 }

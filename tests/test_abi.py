@@ -23,7 +23,7 @@ def test_library_exports_every_symbol():
     L = engine.load_library()
     for name in _declared():
         assert hasattr(L, name), name
-    assert L.jfsx_abi_version() == 5
+    assert L.jfsx_abi_version() == 6
 
 
 def test_struct_layout_matches_header():
@@ -56,3 +56,8 @@ def test_parse_header():
     assert L.jfsx_parse_header(obj, len(obj), ctypes.byref(kl), ctypes.byref(nl)) == 0
     assert (kl.value, nl.value) == (256, 12)
     assert L.jfsx_parse_header(obj[:271], 271, ctypes.byref(kl), ctypes.byref(nl)) == engine.EMISFORMED
+
+
+def test_last_error_is_empty_without_a_failure():
+    # jfsx_last_error(NULL, ...): the calling thread's record; nothing failed here
+    assert engine.last_error(None) == (0, "")

@@ -434,3 +434,31 @@ def test_mctx_lz4_split_over_devices(H):
     nb = H.harness_batch_devs(dev, first, 16)
     assert sorted(dev[:nb]) == [0, 1, 2, 3]
     assert H.jfsx_mctx_close(m) == 0
+
+
+def test_agg_over_devices_rejects_device_memory(H):
+    """device pointers belong to one GPU, and any dispatcher of a
+    multi-device aggregator may take a group, so JFSX_MEM_DEVICE requests are
+    rejected there (as jfsx_mctx_*_batch do); a one-device aggregator keeps
+    accepting them."""
+    H.harness_reset(0)
+    m = mctx(H)
+    h = ctypes.c_void_p()
+    assert H.jfsx_agg_new_mctx(m, 8, 0, 100, ctypes.byref(h)) == 0
+    b, _ = mkblk(0, 4096)
+    r = E.jfsx_range()
+    z = E.jfsx_zblk()
+    assert H.jfsx_agg_seal(h, 0, ctypes.byref(b), E.CRC_GEN, E.MEM_DEVICE) == E.EINVAL
+    assert H.jfsx_agg_open(h, 0, ctypes.byref(b), E.CRC_NONE, E.MEM_DEVICE) == E.EINVAL
+    assert H.jfsx_agg_crc32c(h, ctypes.byref(r), E.CRC_GEN, E.MEM_DEVICE) == E.EINVAL
+    for f in (H.jfsx_agg_lz4_compress, H.jfsx_agg_lz4_decompress, H.jfsx_agg_zstd_decompress):
+        assert f(h, ctypes.byref(z), E.MEM_DEVICE) == E.EINVAL
+    assert H.jfsx_agg_seal(h, 0, ctypes.byref(b), E.CRC_GEN, E.MEM_HOST) == 0
+    assert stats(H, h)[0] == 1  # the rejected calls never reached the queue
+    H.jfsx_agg_free(h)
+    H.jfsx_mctx_close(m)
+    one = mctx(H, 0b0001)
+    assert H.jfsx_agg_new_mctx(one, 8, 0, 100, ctypes.byref(h)) == 0
+    assert H.jfsx_agg_seal(h, 0, ctypes.byref(b), E.CRC_GEN, E.MEM_DEVICE) == 0
+    H.jfsx_agg_free(h)
+    H.jfsx_mctx_close(one)

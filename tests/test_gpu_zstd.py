@@ -47,7 +47,7 @@ def test_concatenated_skippable_and_edges(eng):
                                                                                   len(a) - 1])
     assert got[0] == (E.OK, a + b)
     assert got[1] == (E.OK, b"")
-    assert got[2][0] == E.EFORMAT and got[3][0] == E.EFORMAT
+    assert got[2][0] == E.EFORMAT and got[3][0] == E.EDSTSIZE
 
 
 def test_device_batch_unaligned(eng):
@@ -97,7 +97,7 @@ def test_malformed_agrees_with_library(eng):
     for (st, d), (rc, r) in zip(got, ref):
         if rc < 0:
             rejects += 1
-            assert st == E.EFORMAT
+            assert st in (E.EFORMAT, E.EDSTSIZE)
         else:
             assert st == E.OK and d == r
     assert rejects > 200
@@ -189,3 +189,21 @@ def test_log12_huffman_table(eng):
     got = eng.zstd_decompress(frames, [1000 if len(w) < 256 else len(w) for w in want])
     for i, (w, (st, d)) in enumerate(zip(want, got)):
         assert st == E.OK and d == w, i
+
+
+def test_checksum_tail_reads_inside_output(eng):
+    # the XXH64 tail read 8 bytes per step past the decoded end.
+    # Checksummed frames whose lengths are not multiples of 8, each decoded
+    # into its own device buffer of exactly the decoded size.
+    for n in (1, 3, 7, 9, 13, 31, 33, 1001, 4099, 65537, 131075):
+        src = lz4_data.sample("text", n, seed=n)
+        fr = zstd_lib.compress(src, 1, True)
+        inb = eng.alloc(len(fr))
+        inb.upload(np.frombuffer(fr, np.uint8))
+        outb = eng.alloc(n)
+        arr, k = eng.make_zblocks([(inb.ptr, len(fr), outb.ptr, n)])
+        eng.zstd_decompress_batch(arr, k, E.MEM_DEVICE)
+        assert arr[0].status == E.OK and arr[0].out_len == n, n
+        assert outb.download(n).tobytes() == src, n
+        inb.free()
+        outb.free()

@@ -44,3 +44,13 @@ def test_scheduler_under_tsan(tmp_path):
                 "-o", exe, os.path.join(HERE, "harness", "agg_tsan.cpp"), "-lpthread"], exe,
                env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1"))
     assert "scheduler sanitizer run ok" in out
+
+
+def test_zstd_decoder_under_asan(tmp_path):
+    # checksummed frames decoded into exactly sized outputs: the XXH64 tail
+    # must not read past the decoded bytes (jfsx_zstd.h xxh64)
+    exe = str(tmp_path / "zstd_asan")
+    out = _run(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
+                "-fno-omit-frame-pointer", "-o", exe, os.path.join(HERE, "harness", "zstd_asan.cpp"), "-ldl"], exe,
+               env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0"))
+    assert "zstd sanitizer run ok" in out

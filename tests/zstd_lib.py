@@ -49,6 +49,21 @@ def compress(src, level=1, checksum=False):
     return out.raw[:r]
 
 
+def compress_simple(src, level=1):
+    """ZSTD_compress(dst, bound, src, n, level): the one-shot call
+    zstd.CompressLevel (DataDog/zstd, compress.go:82-91) makes -- the bytes
+    the engine's level-1 encoder must reproduce."""
+    z = lib()
+    z.ZSTD_compress.restype = ctypes.c_size_t
+    z.ZSTD_compress.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int]
+    cap = z.ZSTD_compressBound(len(src))
+    out = ctypes.create_string_buffer(max(cap, 1))
+    r = z.ZSTD_compress(out, cap, bytes(src), len(src), int(level))
+    if z.ZSTD_isError(r):
+        raise RuntimeError("ZSTD_compress failed")
+    return out.raw[:r]
+
+
 def decompress(frame, cap):
     """ZSTD_decompress into cap bytes: (rc, bytes) with rc < 0 on error."""
     z = lib()
