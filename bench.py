@@ -37,7 +37,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--blocks", type=int, default=16384, help="4 MiB blocks per GPU (16384 = 64 GiB)")
     ap.add_argument("--block-bytes", type=int, default=BLOCK)
-    ap.add_argument("--mode", choices=["seal", "open", "crc", "decrypt", "agg", "lz4", "unlz4", "unzstd"], default="seal",
+    ap.add_argument("--mode", choices=["seal", "open", "crc", "decrypt", "agg", "lz4", "unlz4", "zstd", "unzstd"], default="seal",
                     help="decrypt = dataEncryptor.Decrypt end to end: batched RSA-OAEP key unwrap + Open + CRC verify; "
                          "agg = one-block Seal calls from --threads threads on pinned host blocks, through the "
                          "aggregator (jfsx_agg) and, for comparison, as direct one-block batches")
@@ -126,39 +126,57 @@ def host_cores():
     return aff, "%d-CPU affinity mask" % aff
 
 
-def cpu_baseline(args):
-    """The reference's per-block CPU work (checksum() + aead.Seal, one worker
-    per core) timed on this host over a bounded sample of the same workload:
-    the AEAD through OpenSSL EVP (AES-NI/VAES + VPCLMULQDQ stitched GCM, SIMD
-    ChaCha20-Poly1305), the CRC32C as 3-stream SSE4.2 like Go's
-    castagnoliSSE42Triple.  Falls back to the oracle's AES-NI port if
-    libcrypto is not loadable."""
-    from oracle import oracle as orc
-    threads, note = host_cores()
-    algo = orc.AES256GCM if args.algo == "aes256gcm" else orc.CHACHA20P1305
-    nblk = 256  # 1 GiB: BASELINE.json configs[0]
-    fn, impl = orc.bench_seal_crc_evp, "OpenSSL EVP"
-    secs, _ = fn(algo, threads, nblk, BLOCK, SEED)
-    if secs < 0:
-        fn, impl = orc.bench_seal_crc, "oracle AES-NI/PCLMUL port"
-        secs, _ = fn(algo, threads, nblk, BLOCK, SEED)
-    reps = max(1, min(64, int(args.cpu_seconds / max(secs, 1e-3))))
-    total_s, total_b = 0.0, 0
-    for r in range(reps):
-        s, _ = fn(algo, threads, nblk, BLOCK, SEED + r)
-        total_s += s
-        total_b += nblk * BLOCK
-    model = ""
+def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
-                model = line.split(":", 1)[1].strip()
-                break
+                return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return {"value": round(total_b / total_s / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": "%d x 1 GiB (256 x 4 MiB blocks) %s seal (%s) + CRC32C full (3-stream SSE4.2), "
-                      "%d threads (%s), %s" % (reps, args.algo, impl, threads, note, model)}
+    return ""
+
+
+def cpu_baseline(args, mode="seal", lens=None):
+    """The reference's per-block CPU work, one worker per core, timed on this
+    host over a bounded sample of the same workload (about --cpu-seconds):
+      seal  checksum() + aead.Seal            (encrypt.go:192, disk_cache.go:1218-1231)
+      open  aead.Open + the ReadAt CRC verify (encrypt.go:215, disk_cache.go:1315-1327)
+      crc   the ReadAt CRC verify alone       (a cache hit)
+    The AEAD runs through OpenSSL EVP (AES-NI/VAES + VPCLMULQDQ stitched GCM,
+    SIMD ChaCha20-Poly1305: the class of Go's assembly), the
+    CRC32C as 3-stream SSE4.2 like Go's castagnoliSSE42Triple.  lens: the
+    bench's own ragged lengths (configs[4]); else 4 MiB blocks."""
+    from oracle import oracle as orc
+    threads, note = host_cores()
+    algo = orc.AES256GCM if args.algo == "aes256gcm" else orc.CHACHA20P1305
+    bmode = {"seal": orc.BASE_SEAL, "open": orc.BASE_OPEN, "crc": orc.BASE_CRC}[mode]
+    sample = [int(x) for x in lens[:256]] if lens is not None else None
+    nblk = len(sample) if sample else 256  # 1 GiB of 4 MiB blocks: BASELINE.json configs[0]
+    nbytes = sum(sample) if sample else nblk * BLOCK
+    impl = "OpenSSL EVP"
+    secs, _ = orc.bench_baseline(algo, bmode, threads, nblk, BLOCK, SEED, sample)
+    if secs == -1.0 and mode == "seal" and not sample:
+        impl = "oracle AES-NI/PCLMUL port"
+        secs, _ = orc.bench_seal_crc(algo, threads, nblk, BLOCK, SEED)
+    if secs < 0:
+        raise SystemExit("bench: CPU baseline failed (%s, rc %s)" % (mode, secs))
+    reps = max(1, min(64, int(args.cpu_seconds / max(secs, 1e-3))))
+    total_s = 0.0
+    for r in range(reps):
+        if impl == "OpenSSL EVP":
+            s_, _ = orc.bench_baseline(algo, bmode, threads, nblk, BLOCK, SEED + r, sample)
+        else:
+            s_, _ = orc.bench_seal_crc(algo, threads, nblk, BLOCK, SEED + r)
+        if s_ < 0:
+            raise SystemExit("bench: CPU baseline failed (%s, rc %s)" % (mode, s_))
+        total_s += s_
+    what = {"seal": "%s seal (%s) + CRC32C full (3-stream SSE4.2)" % (args.algo, impl),
+            "open": "%s open (%s, tag checked) + CRC32C verify against the stored CRCs" % (args.algo, impl),
+            "crc": "CRC32C verify against the stored CRCs (3-stream SSE4.2)"}[mode]
+    blocks = ("%d ragged blocks (the bench's own lengths, %.3f GiB)" % (nblk, nbytes / 2**30) if sample
+              else "1 GiB (256 x 4 MiB blocks)")
+    return {"value": round(reps * nbytes / total_s / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": "%d x %s %s, %d threads (%s), %s" % (reps, blocks, what, threads, note, cpu_model())}
 
 
 def dry_run(args, world, rank, local, dist):
@@ -199,6 +217,8 @@ def main():
         return lz4_bench(args, world, rank, local, dist, eng)
     if args.mode == "unzstd":
         return zstd_bench(args, world, rank, local, dist, eng)
+    if args.mode == "zstd":
+        return zstdc_bench(args, world, rank, local, dist, eng)
     if args.mem == "host":
         return host_ingest(args, world, rank, local, dist, eng)
     nb, L = args.blocks, args.block_bytes
@@ -338,8 +358,16 @@ def main():
     value = total_plain / el / 1e9
     achieved = algo_bytes / (k_avg_ms / 1e3) / 1e9 if k_n else None
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu and args.mode == "seal":
-        cpu = cpu_baseline(args)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args, "open" if args.mode in ("open", "decrypt") else args.mode,
+                           lens if args.ragged else None)
+        if args.mode == "decrypt" and rsa:
+            # each object also pays one RSA-OAEP private-key unwrap on the host
+            # (encrypt.go:207-210): per thread, block time + unwrap time
+            per_block = cpu["cores"] * BLOCK / (cpu["value"] * 1e9)
+            cpu["value"] = round(cpu["cores"] * BLOCK / (per_block + rsa["host_us_per_unwrap_1thread"] * 1e-6) / 1e9, 3)
+            cpu["sample"] += "; plus one libcrypto RSA-OAEP unwrap per block (%.1f us, measured on 1 thread)" % (
+                rsa["host_us_per_unwrap_1thread"])
     traffic, traffic_src = pmc_traffic(args, sum(lens)) if not args.ragged else (None, None)
     if rank == 0:
         line = {
@@ -469,6 +497,7 @@ def host_ingest(args, world, rank, local, dist, eng):
                 raise SystemExit("bench: block %d differs from the oracle" % b)
             verified += 1
     value = world * nb * L * args.steps / el / 1e9
+    cpu = cpu_baseline(args, "seal") if rank == 0 and world == 1 and not args.no_cpu else None
     if rank == 0:
         peak = min(pcie["h2d"], pcie["d2h"])
         print(json.dumps({
@@ -482,7 +511,7 @@ def host_ingest(args, world, rank, local, dist, eng):
             "roofline": {"bound": "pcie", "achieved": round(value, 2), "peak": peak, "unit": "GB/s",
                          "frac": round(value / peak, 4), "traffic": None, "pcie_measured": pcie,
                          "kernel_avg_ms": round(k_ms / max(k_n, 1), 3), "kernel_launches": k_n},
-            "cpu_baseline": None, "verified_blocks": verified}), flush=True)
+            "cpu_baseline": cpu, "verified_blocks": verified}), flush=True)
     eng.free_pinned(hin)
     eng.free_pinned(hout)
     eng.free_pinned(hcrc)
@@ -567,6 +596,7 @@ def agg_bench(args, world, rank, local, dist, eng):
                 raise SystemExit("bench: block %d differs from the oracle" % b)
             verified += 1
     value = world * nb * L * args.steps / el / 1e9
+    cpu = cpu_baseline(args, "seal") if rank == 0 and world == 1 and not args.no_cpu else None
     if rank == 0:
         print(json.dumps({
             "metric": "per-object sealed+checksummed GB/s, %d threads, 4 MiB host blocks (aggregator)" % T,
@@ -579,7 +609,7 @@ def agg_bench(args, world, rank, local, dist, eng):
             "aggregator": {"calls": c1 - c0, "batches": b1 - b0,
                            "mean_batch_blocks": round((k1 - k0) / max(b1 - b0, 1), 2)},
             "direct_one_block_calls_GBs": round(nb * L * d_steps / d_el / 1e9, 2),
-            "roofline": None, "cpu_baseline": None, "verified_blocks": verified}), flush=True)
+            "roofline": None, "cpu_baseline": cpu, "verified_blocks": verified}), flush=True)
     for h in (hin, hout, hcrc):
         eng.free_pinned(h)
     eng.close()
@@ -826,6 +856,108 @@ def zstd_bench(args, world, rank, local, dist, eng):
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(algo_bytes / (k_avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if k_n else None,
                          "traffic": None, "kernel": "zstd_decompress_k", "kernel_avg_ms": round(k_avg, 3),
+                         "algorithmic_bytes_per_launch": algo_bytes},
+            "cpu_baseline": cpu, "verified_blocks": verified}), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def zstdc_cpu_baseline(blocks, L):
+    """ZSTD_compress(level 1) of the system zstd library (the call
+    zstd.CompressLevel makes) over the sample blocks, one thread per core."""
+    import ctypes
+    from concurrent.futures import ThreadPoolExecutor
+    from tests import zstd_lib
+    z = zstd_lib.lib()
+    z.ZSTD_compress.restype = ctypes.c_size_t
+    z.ZSTD_compress.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int]
+    threads, note = host_cores()
+    cap = z.ZSTD_compressBound(L)
+    outs = [ctypes.create_string_buffer(cap) for _ in range(threads)]
+
+    def work(i):
+        return z.ZSTD_compress(outs[i % threads], cap, blocks[i % len(blocks)], L, 1)
+    reps = max(len(blocks), 4 * threads)
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(work, range(threads)))
+        t0 = time.perf_counter()
+        list(ex.map(work, range(reps)))
+        el = time.perf_counter() - t0
+    return {"value": round(reps * L / el / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": "%d x 4 MiB blocks (%d distinct), ZSTD_compress level 1 of the system libzstd %d (the C "
+                      "library github.com/DataDog/zstd binds), %d threads (%s)" % (reps, len(blocks),
+                                                                                  zstd_lib.version(), threads, note)}
+
+
+def zstdc_bench(args, world, rank, local, dist, eng):
+    """SURVEY 8f-4 / cachedStore.upload's Compress (cached_store.go:387) for
+    "zstd" volumes: a device-resident batch of 4 MiB blocks through
+    jfsx_zstd_compress_batch (zstd.CompressLevel(dst, src, 1) per block).
+    value = uncompressed GB/s."""
+    import numpy as np
+    from juicefs_amd import engine as E
+    from tests import zstd_lib
+    nb, L = args.blocks, args.block_bytes
+    base = rank * nb
+    bound = int(E.zstd_bound(L))
+    src = eng.alloc(nb * L)
+    if args.lz4_data == "text":
+        pool = _text_pool(16 << 20, SEED + rank)
+        for b in range(nb):
+            o = ((base + b) * 2654435761) % (pool.size - L)
+            src.upload(pool[o:o + L], b * L)
+    else:
+        eng.gen_synthetic_batch(src, L, [L] * nb, SEED, base)
+    cmp_ = eng.alloc(nb * bound)
+    arr, n = eng.make_zblocks((src.ptr + b * L, L, cmp_.ptr + b * bound, bound) for b in range(nb))
+
+    def step():
+        eng.zstd_compress_batch(arr, n, E.MEM_DEVICE)
+    for _ in range(args.warmup):
+        step()
+    eng.sync()
+    eng.kernel_time(reset=True)
+    eng.set_timing(True)
+    barrier(dist)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    eng.sync()
+    barrier(dist)
+    el = max_over_ranks(dist, time.perf_counter() - t0, local)
+    eng.set_timing(False)
+    k_ms, k_n = eng.kernel_time(reset=True)
+    k_avg = k_ms / max(k_n, 1)
+    clens = [arr[b].out_len for b in range(nb)]
+    verified = 0
+    if args.verify:
+        for b in range(0, nb, max(1, nb // args.verify))[:args.verify]:
+            p = src.download(L, b * L).tobytes()
+            if arr[b].status != E.OK or cmp_.download(clens[b], b * bound).tobytes() != zstd_lib.compress_simple(p, 1):
+                raise SystemExit("bench: block %d compresses differently from libzstd level 1" % b)
+            verified += 1
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sample = [src.download(L, b * L).tobytes() for b in range(min(nb, 64))]
+        cpu = zstdc_cpu_baseline(sample, L)
+    algo_bytes = nb * L + sum(clens)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "zstd level-1 compressed GB/s (uncompressed bytes), 4 MiB blocks",
+            "value": round(world * nb * L * args.steps / el / 1e9, 2), "unit": "GB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (%s), device-resident" % (
+                "zipf word text, 4 MiB windows of a 16 MiB pool" if args.lz4_data == "text" else "SplitMix64 blocks"),
+            "config": {"workload": "%s GiB device-resident batch of 4 MiB blocks per GPU, zstd level-1 compress" % (
+                round(nb * L / 2**30, 3)), "blocks_per_gpu": nb, "block_bytes": L, "mode": args.mode,
+                "data": args.lz4_data, "ratio": round(sum(clens) / (nb * L), 4),
+                "parallelism": "block-sharded x%d, no collective" % world},
+            "roofline": {"bound": "hbm", "achieved": round(algo_bytes / (k_avg / 1e3) / 1e9, 1) if k_n else None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(algo_bytes / (k_avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if k_n else None,
+                         "traffic": None, "kernel": "zstd_compress_k", "kernel_avg_ms": round(k_avg, 3),
                          "algorithmic_bytes_per_launch": algo_bytes},
             "cpu_baseline": cpu, "verified_blocks": verified}), flush=True)
     eng.close()

@@ -345,6 +345,20 @@ int jfsx_zstd_decompress_batch(jfsx_ctx *ctx, int n, jfsx_zblk *blks, int mem);
 int jfsx_agg_zstd_decompress(jfsx_agg *agg, jfsx_zblk *blk, int mem);
 int jfsx_mctx_zstd_decompress_batch(jfsx_mctx *m, int n, jfsx_zblk *blks, int mem);
 
+/* Zstandard compression (upload side of "zstd" volumes):
+ * ZStandard.Compress of pkg/compress (compress.go:82-91,
+ * zstd.CompressLevel(dst, src, 1) -> ZSTD_compress(dst, bound, src, n, 1)), as
+ * cachedStore.upload calls it before the Put (cached_store.go:371-392, :387).
+ * Each zblk's dst receives one level-1 frame, out_len bytes, byte for byte
+ * what the zstd library's one-shot level-1 compressor writes (checked against
+ * the system libzstd 1.4.8; see DESIGN.md for the 1.5.0 the reference pins).
+ * dst_cap >= jfsx_zstd_bound(src_len) (JFSX_EINVAL otherwise), as upload's
+ * CompressBound-sized buffer; src_len <= 0x7E000000. */
+uint64_t jfsx_zstd_bound(uint64_t n); /* ZSTD_compressBound */
+int jfsx_zstd_compress_batch(jfsx_ctx *ctx, int n, jfsx_zblk *blks, int mem);
+int jfsx_agg_zstd_compress(jfsx_agg *agg, jfsx_zblk *blk, int mem);
+int jfsx_mctx_zstd_compress_batch(jfsx_mctx *m, int n, jfsx_zblk *blks, int mem);
+
 /* header helper: returns wrapped-key length and offset/size of the nonce so a
  * caller can unwrap the key first (encrypt.go:197-205) */
 int jfsx_parse_header(const void *obj, uint64_t olen, int *klen, int *nlen);

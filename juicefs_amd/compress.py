@@ -6,6 +6,7 @@ decompress steps of the chunk store's block upload and load.
   noOp (copy; "buffer too short: %d < %d")                         compress.go:52-70
   LZ4 (lz4.CompressDefault / lz4.DecompressSafe;
        "decompress an empty input")                                compress.go:104-125
+  ZStandard.Compress (zstd.CompressLevel(dst, src, 1))             compress.go:82-91
   ZStandard.Decompress (zstd.Decompress; "buffer too short")       compress.go:93-102
   upload_block: CompressBound buffer, Compress, then Put           cached_store.go:371-392
   load_block: Get, Decompress into the block, "read %s fully"      cached_store.go:673-745
@@ -13,10 +14,10 @@ decompress steps of the chunk store's block upload and load.
 The LZ4 block codec runs on the HIP engine (jfsx_lz4_compress_batch /
 jfsx_lz4_decompress_batch, jfsx_lz4.hip), bit-exact to the LZ4 C library the
 reference binds; CompressBatch / DecompressBatch are the batched entry points
-(one engine call per batch).  Zstandard decompression runs on the engine
-too (jfsx_zstd_decompress_batch, jfsx_zstd.hip); Zstandard compression
-(zstd.CompressLevel at level 1) stays with the Go host's libzstd, so
-ZStandard.Compress raises NotImplementedError rather than run anywhere else.
+(one engine call per batch).  Zstandard runs on the engine both ways:
+jfsx_zstd_compress_batch (jfsx_zstdc.hip) writes the zstd library's level-1
+frames byte for byte, jfsx_zstd_decompress_batch (jfsx_zstd.hip) decodes as
+ZSTD_decompress.
 """
 from . import engine as E
 from .encrypt import default_engine
@@ -100,10 +101,14 @@ class LZ4:
 
 
 class ZStandard:
-    """The "zstd" compressor (DataDog/zstd v1.5.0, level 1).  Decompress runs on
-    the engine; Compress is the Go host's libzstd call."""
+    """The "zstd" compressor (DataDog/zstd v1.5.0, level 1): Compress and
+    Decompress both run on the engine (jfsx_zstd_compress_batch writes the
+    zstd library's level-1 frames byte for byte; jfsx_zstd_decompress_batch
+    decodes as ZSTD_decompress)."""
 
     def __init__(self, level=1, eng=None):
+        if level != 1:
+            raise ValueError("the engine implements zstd level 1 (compress.go:28 ZSTD_LEVEL)")
         self.level = level
         self._eng = eng
 
@@ -115,11 +120,18 @@ class ZStandard:
         return "Zstd"
 
     def CompressBound(self, n):
-        # ZSTD_COMPRESSBOUND(n)
-        return n + (n >> 8) + (((128 << 10) - n) >> 11 if n < (128 << 10) else 0)
+        return int(E.zstd_bound(n))  # ZSTD_COMPRESSBOUND(n)
 
     def Compress(self, dst, src):
-        raise NotImplementedError("zstd compression runs in the Go host's libzstd, not in the jfsx engine")
+        """compress.go:82-91: zstd.CompressLevel allocates a new buffer when
+        cap(dst) < CompressBound(len(src)), and Compress reports that as
+        "buffer too short: %d < %d" (cap(dst), cap(d))."""
+        bound = self.CompressBound(len(src))
+        if len(dst) < bound:
+            raise CompressError("buffer too short: %d < %d" % (len(dst), bound))
+        out = self.CompressBatch([src])[0]
+        dst[:len(out)] = out
+        return len(out)
 
     def Decompress(self, dst, src):
         d = self.DecompressBatch([src], [len(dst)])[0]
@@ -128,24 +140,67 @@ class ZStandard:
         dst[:len(d)] = d
         return len(d)
 
+    # -- batched: one GPU call for many blocks -----------------------------
+    def CompressBatch(self, blocks):
+        """blocks -> one level-1 frame per block (ZSTD_compress(level 1))."""
+        return self.eng.zstd_compress(blocks)
+
     def DecompressBatch(self, blobs, sizes):
         """(frames, destination size) per block -> decoded bytes, or a
-        CompressError: "buffer too short: %d < %d" where the frames decode but
-        not into the destination (zstd.Decompress then returns a larger
-        buffer, compress.go:98-100), else the decoder's error."""
-        res = self.eng.zstd_decompress(blobs, sizes)
-        out, retry = [], []
-        for i, (st, d) in enumerate(res):
-            out.append(d if st == E.OK else None)
-            if st != E.OK:
-                retry.append(i)
-        if retry:
-            big = self.eng.zstd_decompress([blobs[i] for i in retry],
-                                           [max(4 * sizes[i], 1 << 20) for i in retry])
-            for i, (st, d) in zip(retry, big):
-                out[i] = CompressError("buffer too short: %d < %d" % (sizes[i], len(d)) if st == E.OK
-                                       else "zstd: corrupted frame")
+        CompressError:
+          * an empty input: DataDog's ErrEmptySlice ("Bytes slice is empty");
+          * frames that decode, but not into the destination: zstd.Decompress
+            returns a larger buffer, which compress.go:98-100 reports as
+            "buffer too short: %d < %d" (len(dst), decoded size);
+          * anything else the decoder rejects: "zstd: corrupted frame"."""
+        out = [None] * len(blobs)
+        todo = []
+        for i, b in enumerate(blobs):
+            if len(b) == 0:
+                out[i] = CompressError("Bytes slice is empty")
+            else:
+                todo.append(i)
+        res = self.eng.zstd_decompress([blobs[i] for i in todo], [sizes[i] for i in todo]) if todo else []
+        short = []
+        for i, (st, d) in zip(todo, res):
+            if st == E.OK:
+                out[i] = d
+            elif st == E.EDSTSIZE:
+                short.append(i)
+            else:
+                out[i] = CompressError("zstd: corrupted frame")
+        # the decoded size of a frame that does not fit: its content size
+        # field when it has one, else doubling capacities (up to 2^31 - 1)
+        caps = {i: max(_frame_content_size(blobs[i]) or 0, 2 * sizes[i], 1 << 16) for i in short}
+        while short:
+            res = self.eng.zstd_decompress([blobs[i] for i in short], [min(caps[i], (1 << 31) - 1) for i in short])
+            again = []
+            for i, (st, d) in zip(short, res):
+                if st == E.OK:
+                    out[i] = CompressError("buffer too short: %d < %d" % (sizes[i], len(d)))
+                elif st == E.EDSTSIZE and caps[i] < (1 << 31) - 1:
+                    caps[i] *= 2
+                    again.append(i)
+                else:
+                    out[i] = CompressError("zstd: corrupted frame")
+            short = again
         return out
+
+
+def _frame_content_size(b):
+    """Frame_Content_Size of the first frame's header (RFC 8878 3.1.1.1), or
+    None when absent or unreadable."""
+    b = bytes(b[:18])
+    if len(b) < 6 or b[:4] != b"\x28\xb5\x2f\xfd":
+        return None
+    fhd = b[4]
+    single, fcs_id, did = (fhd >> 5) & 1, fhd >> 6, fhd & 3
+    pos = 5 + (0 if single else 1) + (0, 1, 2, 4)[did]
+    size = (1 if single else 0, 2, 4, 8)[fcs_id]
+    if size == 0 or len(b) < pos + size:
+        return None
+    v = int.from_bytes(b[pos:pos + size], "little")
+    return v + 256 if size == 2 else v
 
 
 def NewCompressor(algr, eng=None):
@@ -166,7 +221,7 @@ def NewCompressor(algr, eng=None):
 def upload_blocks(store, keys, blocks, compressor):
     """cachedStore.upload for a batch of blocks: compress each (into a
     CompressBound-sized buffer when the bound exceeds the block), then Put."""
-    if isinstance(compressor, LZ4):
+    if isinstance(compressor, (LZ4, ZStandard)):
         outs = compressor.CompressBatch(blocks)
     else:
         outs = []

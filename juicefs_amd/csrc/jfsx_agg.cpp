@@ -168,7 +168,7 @@ int jfsx_wait(jfsx_ctx *c, jfsx_ticket t, int timeout_ms) {
 
 namespace jfsx {
 
-enum AggOp { kSeal = 0, kOpen = 1, kCrc = 2, kLz4c = 3, kLz4d = 4, kZstdd = 5 };
+enum AggOp { kSeal = 0, kOpen = 1, kCrc = 2, kLz4c = 3, kLz4d = 4, kZstdd = 5, kZstdc = 6 };
 
 struct Req {
     int op, algo, mode, mem;
@@ -191,6 +191,7 @@ using jfsx::kCrc;
 using jfsx::kLz4c;
 using jfsx::kLz4d;
 using jfsx::kZstdd;
+using jfsx::kZstdc;
 
 struct jfsx_agg {
     std::vector<jfsx_ctx *> cs;  // one dispatcher thread per context (device)
@@ -212,6 +213,7 @@ struct jfsx_agg {
         if (h.op == kLz4c) return jfsx_lz4_compress_batch(c, (int)n, zs.data() + i0, h.mem);
         if (h.op == kLz4d) return jfsx_lz4_decompress_batch(c, (int)n, zs.data() + i0, h.mem);
         if (h.op == kZstdd) return jfsx_zstd_decompress_batch(c, (int)n, zs.data() + i0, h.mem);
+        if (h.op == kZstdc) return jfsx_zstd_compress_batch(c, (int)n, zs.data() + i0, h.mem);
         if (h.op == kSeal) return jfsx_seal_batch(c, h.algo, (int)n, blks.data() + i0, h.mode, h.mem);
         return jfsx_open_batch(c, h.algo, (int)n, blks.data() + i0, h.mode, h.mem);
     }
@@ -228,7 +230,7 @@ struct jfsx_agg {
         if (op == kCrc) {
             rng.resize(n);
             for (size_t i = 0; i < n; i++) rng[i] = *b[i]->range;
-        } else if (op == kLz4c || op == kLz4d || op == kZstdd) {
+        } else if (op == kLz4c || op == kLz4d || op == kZstdd || op == kZstdc) {
             zs.resize(n);
             for (size_t i = 0; i < n; i++) zs[i] = *b[i]->z;
         } else {
@@ -244,7 +246,7 @@ struct jfsx_agg {
         for (size_t i = 0; i < n; i++) {
             if (op == kCrc)
                 *b[i]->range = rng[i];
-            else if (op == kLz4c || op == kLz4d || op == kZstdd)
+            else if (op == kLz4c || op == kLz4d || op == kZstdd || op == kZstdc)
                 *b[i]->z = zs[i];
             else
                 *b[i]->blk = blks[i];
@@ -390,6 +392,12 @@ int jfsx_agg_zstd_decompress(jfsx_agg *a, jfsx_zblk *z, int mem) {
     return a->submit(r);
 }
 
+int jfsx_agg_zstd_compress(jfsx_agg *a, jfsx_zblk *z, int mem) {
+    if (!a || !z || !agg_mem_ok(a, mem)) return JFSX_EINVAL;
+    Req r{kZstdc, 0, 0, mem, nullptr, nullptr, z, z->src_len};
+    return a->submit(r);
+}
+
 int jfsx_agg_stats(jfsx_agg *a, uint64_t *calls, uint64_t *batches, uint64_t *blocks) {
     if (!a) return JFSX_EINVAL;
     std::lock_guard<std::mutex> g(a->mu);
@@ -521,7 +529,8 @@ static int mctx_lz4(jfsx_mctx *m, int op, int n, jfsx_zblk *z, int mem) {
     return fan_out(cut, [&](int k, int b0, int b1) {
         return op == kLz4c   ? jfsx_lz4_compress_batch(m->cs[k], b1 - b0, z + b0, mem)
                : op == kLz4d ? jfsx_lz4_decompress_batch(m->cs[k], b1 - b0, z + b0, mem)
-                             : jfsx_zstd_decompress_batch(m->cs[k], b1 - b0, z + b0, mem);
+               : op == kZstdc ? jfsx_zstd_compress_batch(m->cs[k], b1 - b0, z + b0, mem)
+                              : jfsx_zstd_decompress_batch(m->cs[k], b1 - b0, z + b0, mem);
     });
 }
 
@@ -531,6 +540,10 @@ int jfsx_mctx_lz4_decompress_batch(jfsx_mctx *m, int n, jfsx_zblk *blks, int mem
 }
 int jfsx_mctx_zstd_decompress_batch(jfsx_mctx *m, int n, jfsx_zblk *blks, int mem) {
     return mctx_lz4(m, kZstdd, n, blks, mem);
+}
+
+int jfsx_mctx_zstd_compress_batch(jfsx_mctx *m, int n, jfsx_zblk *blks, int mem) {
+    return mctx_lz4(m, kZstdc, n, blks, mem);
 }
 
 int jfsx_agg_new_mctx(jfsx_mctx *m, int max_blocks, uint64_t max_bytes, uint32_t window_us, jfsx_agg **out) {

@@ -47,7 +47,13 @@ void note_hip_error(hipError_t e, const char *file, int line, const char *expr) 
              base ? base + 1 : file, line, expr);
     tl_err.hip = (int)e;
     if (tl_ctx) note_ctx_error(tl_ctx, tl_err);
+    (void)hipGetLastError();  // a handled failure must not resurface at the next launch check
 }
+
+// hipGetLastError() after a launch also returns the error of any earlier
+// failed HIP call of this thread (a handled hipMalloc failure, say): clear the
+// slot before launching, so the check that follows sees only the launch
+inline void launch_begin() { (void)hipGetLastError(); }
 
 // an entry point's scope: failures inside it are also kept on the context
 struct CtxScope {
@@ -409,6 +415,7 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, int k, int algo, bool
     BlkOut *dout = (BlkOut *)(d + o_out);
     if (gcm) {
         GcmSched *dsch = (GcmSched *)(d + o_sched);
+        launch_begin();
         launch_gcm_keysetup(s, n, dk, db, dsch, c->tabs);
         if (c->timing) HIP_OK(hipEventRecord(c->ev_k0[k], s));
         launch_gcm_main(s, (int)nt, c->ncu, (uint32_t *)(d + o_queue), open, crc_mode, c->bitslice, dt, db, dsch, dpart,
@@ -417,6 +424,7 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, int k, int algo, bool
         launch_gcm_finalize(s, n, open, crc_mode, db, dsch, dpart, dpexp, dout);
     } else {
         CpSched *dsch = (CpSched *)(d + o_sched);
+        launch_begin();
         launch_cp_keysetup(s, n, dk, db, dsch);
         if (c->timing) HIP_OK(hipEventRecord(c->ev_k0[k], s));
         launch_cp_main(s, (int)nt, c->ncu, (uint32_t *)(d + o_queue), open, crc_mode, dt, db, dsch, dpart, dpexp,
@@ -704,6 +712,7 @@ int run_crc(jfsx_ctx *c, int n, jfsx_range *r, int mode) {
     hipStream_t s = c->stream;
     HIP_OK(hipMemcpyAsync(d, h, h_bytes, hipMemcpyHostToDevice, s));
     if (c->timing) HIP_OK(hipEventRecord(c->ev_k0[0], s));
+    launch_begin();
     launch_crc_segments(s, (int)nt, (const Task *)(d + o_task), (const BlkDev *)(d + o_blk), c->tabs);
     if (c->timing) HIP_OK(hipEventRecord(c->ev_k1[0], s));
     launch_crc_finalize(s, n, mode, (const BlkDev *)(d + o_blk), (BlkOut *)(d + o_out));
@@ -759,25 +768,34 @@ int run_crc_host(jfsx_ctx *c, int n, jfsx_range *r, int mode) {
 
 constexpr uint64_t kLz4MaxInput = 0x7E000000ull;  // LZ4_MAX_INPUT_SIZE
 uint64_t lz4_bound(uint64_t n) { return n > kLz4MaxInput ? 0 : n + n / 255 + 16; }
+// ZSTD_compressBound
+uint64_t zstd_bound(uint64_t n) { return n + (n >> 8) + (n < (128u << 10) ? ((128u << 10) - n) >> 11 : 0); }
 
-// LZ4 stage (jfsx_lz4.hip): one wave per block.  Host-memory batches are
-// staged through the context's slot-0 staging buffer (inputs up, the
-// out_len bytes of each output down).
-int run_lz4(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, bool comp, bool zstd = false) {
+enum CodecOp { kLz4Comp, kLz4Decomp, kZstdDecomp, kZstdComp };
+
+// The codec stages (jfsx_lz4.hip, jfsx_zstd.hip, jfsx_zstdc.hip): one wave per
+// object.  Host-memory batches are staged through the context's slot-0
+// staging buffer (inputs up, the out_len bytes of each output down).
+int run_codec(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, CodecOp op) {
     if (n < 0 || (mem != JFSX_MEM_DEVICE && mem != JFSX_MEM_HOST)) return JFSX_EINVAL;
     for (int i = 0; i < n; i++) {
         if ((z[i].src_len && !z[i].src) || (z[i].dst_cap && !z[i].dst) || z[i].src_len > kLz4MaxInput ||
             z[i].dst_cap >= ((uint64_t)1 << 32))
             return JFSX_EINVAL;
-        if (comp && z[i].dst_cap < lz4_bound(z[i].src_len)) return JFSX_EINVAL;
-        if (zstd && z[i].dst_cap >= ((uint64_t)1 << 31)) return JFSX_EINVAL;  // 32-bit frame positions
+        if (op == kLz4Comp && z[i].dst_cap < lz4_bound(z[i].src_len)) return JFSX_EINVAL;
+        if (op == kZstdComp && z[i].dst_cap < zstd_bound(z[i].src_len)) return JFSX_EINVAL;
+        if (op == kZstdDecomp && z[i].dst_cap >= ((uint64_t)1 << 31)) return JFSX_EINVAL;  // 32-bit frame positions
     }
     if (n == 0) return 0;
     int rc;
     Workspace &w = c->ws[0];
+    const int zc_waves = std::min(n, c->ncu * kZcWavesPerCu);
     const size_t o_out = align256(sizeof(ZDev) * n), o_tab = o_out + align256(sizeof(ZOut) * n);
-    const size_t dbytes = o_tab + (comp ? kLz4TabBytes * (size_t)n : zstd ? kZstdScratch * (size_t)n : 0);
-    if ((rc = ensure_dev(c, &w.d, &w.dcap, dbytes))) return rc;
+    size_t extra = 0;
+    if (op == kLz4Comp) extra = kLz4TabBytes * (size_t)n;
+    else if (op == kZstdDecomp) extra = kZstdScratch * (size_t)n;
+    else if (op == kZstdComp) extra = 256 + kZstdcScratch * (size_t)zc_waves;  // queue, then per-wave scratch
+    if ((rc = ensure_dev(c, &w.d, &w.dcap, o_tab + extra))) return rc;
     if ((rc = ensure_host(&w.h, &w.hcap, o_tab))) return rc;  // descriptors and results only
     hipStream_t s = c->stream;
     ZDev *hz = (ZDev *)w.h;
@@ -801,16 +819,27 @@ int run_lz4(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, bool comp, bool zstd = fa
     }
     HIP_OK(hipMemcpyAsync(w.d, w.h, sizeof(ZDev) * n, hipMemcpyHostToDevice, s));
     if (c->timing) HIP_OK(hipEventRecord(c->ev_k0[0], s));
-    if (comp)
-        launch_lz4_compress(s, n, (const ZDev *)w.d, (ZOut *)(w.d + o_out), (uint32_t *)(w.d + o_tab));
-    else if (zstd)
-        launch_zstd_decompress(s, n, (const ZDev *)w.d, (ZOut *)(w.d + o_out), (uint8_t *)(w.d + o_tab));
-    else
-        launch_lz4_decompress(s, n, (const ZDev *)w.d, (ZOut *)(w.d + o_out));
+    const ZDev *dz = (const ZDev *)w.d;
+    ZOut *dout = (ZOut *)(w.d + o_out);
+    launch_begin();
+    switch (op) {
+    case kLz4Comp:
+        launch_lz4_compress(s, n, dz, dout, (uint32_t *)(w.d + o_tab));
+        break;
+    case kLz4Decomp:
+        launch_lz4_decompress(s, n, dz, dout);
+        break;
+    case kZstdDecomp:
+        launch_zstd_decompress(s, n, dz, dout, (uint8_t *)(w.d + o_tab));
+        break;
+    case kZstdComp:
+        launch_zstd_compress(s, n, zc_waves, dz, dout, (uint8_t *)(w.d + o_tab + 256), (uint32_t *)(w.d + o_tab));
+        break;
+    }
     if (c->timing) HIP_OK(hipEventRecord(c->ev_k1[0], s));
     HIP_OK(hipGetLastError());
     ZOut *ho = (ZOut *)(w.h + o_out);
-    HIP_OK(hipMemcpyAsync(ho, w.d + o_out, sizeof(ZOut) * n, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(ho, dout, sizeof(ZOut) * n, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
     if (c->timing) {
         float ms = 0;
@@ -1057,7 +1086,7 @@ int jfsx_lz4_compress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
     std::lock_guard<std::mutex> g(c->mu);
     CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
-    return run_lz4(c, n, blks, mem, true);
+    return run_codec(c, n, blks, mem, kLz4Comp);
 }
 
 int jfsx_lz4_decompress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
@@ -1065,7 +1094,7 @@ int jfsx_lz4_decompress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
     std::lock_guard<std::mutex> g(c->mu);
     CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
-    return run_lz4(c, n, blks, mem, false);
+    return run_codec(c, n, blks, mem, kLz4Decomp);
 }
 
 int jfsx_zstd_decompress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
@@ -1073,7 +1102,17 @@ int jfsx_zstd_decompress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
     std::lock_guard<std::mutex> g(c->mu);
     CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
-    return run_lz4(c, n, blks, mem, false, true);
+    return run_codec(c, n, blks, mem, kZstdDecomp);
+}
+
+uint64_t jfsx_zstd_bound(uint64_t n) { return zstd_bound(n); }
+
+int jfsx_zstd_compress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
+    if (!c || (n > 0 && !blks)) return JFSX_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    CtxScope es_(c);
+    HIP_OK(hipSetDevice(c->device));
+    return run_codec(c, n, blks, mem, kZstdComp);
 }
 
 int jfsx_checksum(jfsx_ctx *c, const void *data, uint64_t len, uint8_t *out) {
@@ -1349,6 +1388,7 @@ int jfsx_gen_synthetic(jfsx_ctx *c, void *dst, uint64_t len, uint64_t seed, uint
     std::lock_guard<std::mutex> g(c->mu);
     CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
+    launch_begin();
     if (len) launch_gen_synthetic(c->stream, (uint8_t *)dst, len, seed, block);
     HIP_OK(hipGetLastError());
     return 0;
@@ -1369,6 +1409,7 @@ int jfsx_gen_synthetic_batch(jfsx_ctx *c, void *dst, uint64_t stride, int n, con
     if ((rc = ensure_host(&w.h, &w.hcap, 8 * (size_t)n))) return rc;
     memcpy(w.h, lens, 8 * (size_t)n);
     HIP_OK(hipMemcpyAsync(w.d, w.h, 8 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    launch_begin();
     launch_gen_synthetic_batch(c->stream, (uint8_t *)dst, stride, n, (const uint64_t *)w.d, seed, block0);
     HIP_OK(hipGetLastError());
     HIP_OK(hipStreamSynchronize(c->stream));  // w.h/w.d are reused by the next batch
@@ -1470,6 +1511,7 @@ int jfsx_rsa_oaep_decrypt_batch(jfsx_ctx *c, const jfsx_rsa_key *k, int n, const
     }
     char *d = c->rsa_d;
     HIP_OK(hipMemcpyAsync(d + o_ct, c->rsa_h, K * n, hipMemcpyHostToDevice, c->stream));
+    launch_begin();
     launch_rsa_unwrap(c->stream, k->d_key, n, (const uint8_t *)(d + o_ct), (uint32_t *)(d + o_mh),
                       (uint8_t *)(d + o_em), (int32_t *)(d + o_len));
     HIP_OK(hipGetLastError());

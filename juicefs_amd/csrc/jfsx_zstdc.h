@@ -582,6 +582,8 @@ struct HufNode {
 struct HufWork {
     HufNode node0[512];
     uint8_t fseSym[64];
+    uint8_t weight[256];  // HUF_writeCTable's huffWeight
+    FseCT fct;            // HUF_compressWeights' table
 };
 
 // HUF_setMaxHeight
@@ -765,9 +767,8 @@ ZC_HD uint64_t huf_compress_weights(uint8_t *dst, uint64_t cap, const uint8_t *w
     int16_t norm[kHufLogMax + 1];
     if (fse_normalize(norm, tableLog, count, n, maxSym, false)) return 0;
     const uint32_t hs = fse_write_ncount(dst, norm, maxSym, tableLog);
-    FseCT ct;
-    fse_build_ctable(ct, norm, maxSym, tableLog, wk.fseSym);
-    const uint64_t cs = fse_compress_symbols(dst + hs, cap - hs, w, n, ct);
+    fse_build_ctable(wk.fct, norm, maxSym, tableLog, wk.fseSym);
+    const uint64_t cs = fse_compress_symbols(dst + hs, cap - hs, w, n, wk.fct);
     if (cs == 0) return 0;
     return hs + cs;
 }
@@ -776,7 +777,7 @@ ZC_HD uint64_t huf_compress_weights(uint8_t *dst, uint64_t cap, const uint8_t *w
 ZC_HD uint64_t huf_write_ctable(uint8_t *op, uint64_t cap, const HufCT &ct, uint32_t maxSym, uint32_t huffLog,
                                 HufWork &wk) {
     uint8_t bitsToWeight[kHufLogMax + 1];
-    uint8_t huffWeight[256];
+    uint8_t *const huffWeight = wk.weight;
     bitsToWeight[0] = 0;
     for (uint32_t n = 1; n < huffLog + 1; n++) bitsToWeight[n] = (uint8_t)(huffLog + 1 - n);
     for (uint32_t n = 0; n < maxSym; n++) huffWeight[n] = bitsToWeight[ct.nb[n]];
@@ -1131,6 +1132,7 @@ ZC_HD uint64_t compress_block_body(const HufState &prevHuf, HufState &nextHuf, S
         if (MLtype == kSetCompressed) lastNCount = op;
         op += t;
         *seqHead = (uint8_t)((LLtype << 6) + (OFtype << 4) + (MLtype << 2));
+        if ((uint64_t)(op - ostart) + 16 >= cap) return 0;  // no room left: stored raw (dstSize_tooSmall)
         const uint64_t bs = encode_sequences(op, cap - (uint64_t)(op - ostart), ss, sw);
         if (bs == 0) return 0;
         op += bs;
@@ -1189,10 +1191,17 @@ struct Work {
     uint32_t litCount[256];
 };
 
+// One compressed block body is built in a scratch buffer of kBodyCap bytes
+// and copied to the frame only when it is kept, so the frame never grows past
+// ZSTD_compressBound (the library's dstCapacity checks end in a raw block
+// exactly when the body would not be kept here).
+constexpr uint32_t kBodyCap = kBlockMax + 1024;
+
 // The whole ZSTD_compress(level 1) of src[0, n) into dst (capacity >= bound).
-// htab: (1 << kHashLogMax) words; seq / lit / codes: one block's worth.
+// htab: (1 << kHashLogMax) words; seq / lit / codes: one block's worth;
+// body: kBodyCap bytes.
 ZC_HD uint64_t compress_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *htab, SeqDef *seqs, uint8_t *lits,
-                              uint8_t *codes, Work &w) {
+                              uint8_t *codes, uint8_t *body, Work &w) {
     const Params P = level1_params(n);
     uint8_t *op = dst;
     op += write_frame_header(op, n, P);
@@ -1224,8 +1233,7 @@ ZC_HD uint64_t compress_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint
             const uint32_t lastLL = parse_fast(src, (int32_t)pos, (int32_t)(pos + bs), htab, P, nrep, ss);
             copy_bytes(ss.lit + ss.nlit, src + pos + bs - lastLL, lastLL);
             ss.nlit += lastLL;
-            cSize = compress_block_body(w.prev, w.next, ss, op + 3, kBlockMax + 1024, bs, w.litCount, w.hufScratch,
-                                        w.hw, w.sw);
+            cSize = compress_block_body(w.prev, w.next, ss, body, kBodyCap, bs, w.litCount, w.hufScratch, w.hw, w.sw);
             if (!first && cSize < kRleMaxLength && is_rle(ip, bs)) cSize = 1;
             if (cSize > 1) {
                 // ZSTD_confirmRepcodesAndEntropyTables: the parse's repcodes
@@ -1246,6 +1254,7 @@ ZC_HD uint64_t compress_frame(const uint8_t *src, uint64_t n, uint8_t *dst, uint
             op += 4;
         } else {
             wr24(op, last + (2u << 1) + ((uint32_t)cSize << 3));
+            copy_bytes(op + 3, body, (uint32_t)cSize);
             op += 3 + cSize;
         }
         pos += bs;

@@ -1,0 +1,451 @@
+// jfsx_zstdc.hip -- Zstandard level-1 compression on gfx950 (the upload side
+// of --compress zstd volumes).
+//
+// Replaces ZStandard.Compress = zstd.CompressLevel(dst, src, 1)
+// (pkg/compress/compress.go:82-91; DataDog/zstd v1.5.0 -> ZSTD_compress) as
+// called by cachedStore.upload (pkg/chunk/cached_store.go:371-392, :387).
+// The frame bytes are those of the zstd library's level-1 one-shot path
+// (jfsx_zstdc.h restates it; tests compare with the system libzstd 1.4.8).
+//
+// Decomposition: the greedy parse of a frame is sequential from its first
+// byte to its last (one hash table and one set of repcodes and entropy
+// tables carried over all 128 KiB blocks), so one wave owns one object.
+// Persistent waves take objects from a queue; each has a global scratch (hash
+// table, sequences, literals, codes) and its entropy tables in LDS.
+//
+// The parser (ZSTD_compressBlock_fast_generic) runs on the 64 lanes:
+//   * a search step evaluates 64 consecutive iterations of the serial loop at
+//     once -- lane j the positions p_j, p_j + 1 (hashes, table reads, 4-byte
+//     compares) and the repcode at p_j + 2.  The positions of a miss run are
+//     known in advance (step = (p - anchor) / 128 + 2).
+//   * iterations see the table writes of the iterations before them: when
+//     the first iteration does not already succeed on its own, 2 x hashLog
+//     ballots give every lane the lanes whose writes share its buckets; reads
+//     take the latest earlier writer, and only the last writer of a bucket
+//     (up to the first success) stores.
+//   * backward catch-up and the match-length count run 64 / 256 bytes per
+//     step with a ballot for the first difference.
+// The entropy stage of a block (literal Huffman coding, sequence FSE coding)
+// runs the library's serial code (jfsx_zstdc.h) on one lane.
+#include "jfsx_dev.h"
+#include "jfsx_zstdc.h"
+
+namespace jfsx {
+
+namespace {
+constexpr size_t kZcHtab = (size_t)4 << jzc::kHashLogMax;             // 128 KiB
+constexpr size_t kZcSeq = (size_t)jzc::kMaxSeq * sizeof(jzc::SeqDef);  // 256 KiB
+constexpr size_t kZcLit = (size_t)jzc::kBlockMax + 256;                // literals
+constexpr size_t kZcCodes = (size_t)3 * jzc::kMaxSeq;                  // ll / ml / of codes
+static_assert(kZcHtab + kZcSeq + kZcLit + kZcCodes + jzc::kBodyCap <= kZstdcScratch, "zstd compress scratch");
+
+typedef __attribute__((address_space(1))) const uint32_t gcu32z;
+typedef __attribute__((address_space(1))) const uint8_t gcu8c;
+typedef __attribute__((address_space(1))) uint8_t gu8c;
+typedef __attribute__((address_space(1))) uint32_t gu32c;
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int32_t unis(int32_t v) { return (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)v); }
+__device__ __forceinline__ uint64_t ballot(bool b) { return __ballot(b); }
+__device__ __forceinline__ uint32_t ld8(const uint8_t *p) { return *(gcu8c *)p; }
+__device__ __forceinline__ uint32_t ld32a(const uint8_t *p) { return *(gcu32z *)p; }
+// 4 bytes at any address: two aligned dword loads, each holding at least one
+// of the requested bytes (neither touches a page the bytes are not on)
+__device__ __forceinline__ uint32_t ld32u(const uint8_t *a) {
+    const uintptr_t x = (uintptr_t)a;
+    const uint8_t *b = (const uint8_t *)(x & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(x & 3);
+    const uint32_t w0 = ld32a(b), w1 = ld32a(sh ? b + 4 : b);
+    return __builtin_amdgcn_alignbyte(w1, w0, sh);
+}
+__device__ __forceinline__ uint32_t readlane(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ int32_t readlanes(int32_t v, int l) { return (int32_t)__builtin_amdgcn_readlane((uint32_t)v, l); }
+
+// jzc::hash_ptr of the 8 bytes w (little-endian) at a position
+__device__ __forceinline__ uint32_t hash_w(uint64_t w, uint32_t hlog, uint32_t mls) {
+    if (mls == 5) return (uint32_t)(((w << 24) * 889523592379ull) >> (64 - hlog));
+    if (mls == 6) return (uint32_t)(((w << 16) * 227718039650203ull) >> (64 - hlog));
+    if (mls == 7) return (uint32_t)(((w << 8) * 58295818150454627ull) >> (64 - hlog));
+    return ((uint32_t)w * 2654435761u) >> (32 - hlog);
+}
+
+// bytes [p, p + 8) and [p + 1, p + 9) from three aligned dwords (p + 8 must
+// lie inside the input)
+__device__ __forceinline__ void load9(const uint8_t *src, int32_t p, uint64_t &w0, uint64_t &w1) {
+    const uintptr_t x = (uintptr_t)(src + p);
+    const uint8_t *b = (const uint8_t *)(x & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(x & 3);
+    const uint32_t d0 = ld32a(b), d1 = ld32a(b + 4), d2 = ld32a(b + 8);
+    w0 = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32);
+    if (sh == 3) {
+        w1 = (uint64_t)d1 | ((uint64_t)d2 << 32);
+    } else {
+        w1 = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh + 1) |
+             ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh + 1) << 32);
+    }
+}
+
+__device__ __forceinline__ uint64_t ld64u(const uint8_t *p) {
+    return (uint64_t)ld32u(p) | ((uint64_t)ld32u(p + 4) << 32);
+}
+
+// ZSTD_count(a, b, lim) on the wave: 256 bytes per step (a > b)
+__device__ uint32_t count_wave(const uint8_t *a, const uint8_t *b, const uint8_t *lim, uint32_t lane) {
+    const uint32_t avail = (uint32_t)(lim - a);
+    for (uint32_t c = 0;; c += 256) {
+        if (c >= avail) return avail;
+        const uint32_t t = c + 4 * lane;
+        uint32_t stop = 0xffffffffu;
+        if (t + 4 <= avail) {
+            const uint32_t x = ld32u(a + t) ^ ld32u(b + t);
+            if (x) stop = t + ((uint32_t)__builtin_ctz(x) >> 3);
+        } else if (t < avail) {
+            stop = avail;
+            for (uint32_t k = t; k < avail; k++)
+                if (ld8(a + k) != ld8(b + k)) {
+                    stop = k;
+                    break;
+                }
+        }
+        const uint64_t sm = ballot(stop != 0xffffffffu);
+        if (sm) return uni(readlane(stop, __builtin_ctzll(sm)));
+    }
+}
+
+// how many of the bytes before a and b (at most lim) are equal, 64 per step
+__device__ uint32_t back_wave(const uint8_t *a, const uint8_t *b, uint32_t lim, uint32_t lane) {
+    for (uint32_t c = 0;; c += 64) {
+        if (c >= lim) return lim;
+        const uint32_t t = c + lane;
+        const bool diff = t < lim && ld8(a - 1 - t) != ld8(b - 1 - t);
+        const uint64_t sm = ballot(diff || t >= lim);
+        if (sm) return uni(c + (uint32_t)__builtin_ctzll(sm));
+    }
+}
+
+__device__ __forceinline__ uint64_t lanes_below(uint32_t lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
+__device__ __forceinline__ uint64_t lanes_above(uint32_t lane) { return lane == 63 ? 0ull : (~0ull << (lane + 1)); }
+
+struct WSeq {  // the wave's view of the block's sequence store
+    jzc::SeqDef *seq;
+    uint8_t *lit;
+    uint32_t nseq, nlit, long_id, long_pos;
+};
+
+// ZSTD_storeSeq: literals copied by the lanes, the record by lane 0
+__device__ __forceinline__ void store_seq_wave(WSeq &ss, const uint8_t *lits, uint32_t litLen, uint32_t offCode,
+                                               uint32_t mlBase, uint32_t lane) {
+    for (uint32_t o = lane; o < litLen; o += 64) *(gu8c *)(ss.lit + ss.nlit + o) = (uint8_t)ld8(lits + o);
+    if (litLen > 0xFFFF) ss.long_id = 1, ss.long_pos = ss.nseq;
+    if (mlBase > 0xFFFF) ss.long_id = 2, ss.long_pos = ss.nseq;
+    if (lane == 0) {
+        jzc::SeqDef d;
+        d.offset = offCode + 1;
+        d.ll = (uint16_t)litLen;
+        d.ml = (uint16_t)mlBase;
+        ss.seq[ss.nseq] = d;
+    }
+    ss.nseq++;
+    ss.nlit += litLen;
+}
+
+// jzc::parse_fast on the wave: same sequences, same table, same repcodes.
+__device__ uint32_t parse_fast_wave(const uint8_t *src, int32_t istart, int32_t iend, uint32_t *htab, jzc::Params P,
+                                    uint32_t rep[2], WSeq &ss, uint32_t lane) {
+    const uint32_t hlog = P.hlog, mls = P.mls;
+    const int32_t endIndex = iend + 1;
+    const int32_t prefixStartIndex = jzc::prefix_start_index(endIndex, P.wlog);
+    const int32_t prefixStart = prefixStartIndex - 1;
+    const int32_t ilimit = iend - 8;
+    int32_t ip0 = istart, anchor = istart;
+    uint32_t offset_1 = rep[0], offset_2 = rep[1], offsetSaved = 0;
+    ip0 += (ip0 == prefixStart);
+    {
+        const int32_t cur = ip0 + 1;
+        const int32_t windowLow = jzc::prefix_start_index(cur, P.wlog);
+        const uint32_t maxRep = (uint32_t)(cur - windowLow);
+        if (offset_2 > maxRep) offsetSaved = offset_2, offset_2 = 0;
+        if (offset_1 > maxRep) offsetSaved = offset_1, offset_1 = 0;
+    }
+    const uint8_t *const iendp = src + iend;
+    gu32c *const T = (gu32c *)htab;
+    while (ip0 + 1 < ilimit) {
+        // ---- one search step: iterations j = 0..63 of the serial loop ----
+        const int32_t d0 = ip0 - anchor;
+        int32_t d;
+        if (d0 < 2) {
+            d = d0 + 2 * (int32_t)lane;  // every step is 2 while d < 128
+        } else {
+            int32_t x = d0;
+            d = d0;
+            for (uint32_t j = 0; j < 64; j++) {
+                if (lane == j) d = x;
+                x += (x >> 7) + 2;
+            }
+        }
+        const int32_t p = anchor + d;
+        const bool valid = p + 1 < ilimit;
+        const uint64_t vmask = ballot(valid);
+        const int32_t pc = valid ? p : ip0;
+        uint64_t w0, w1;
+        load9(src, pc, w0, w1);
+        const uint32_t A = hash_w(w0, hlog, mls), B = hash_w(w1, hlog, mls);
+        const int32_t tA0 = (int32_t)T[A], tB0 = (int32_t)T[B];
+        const uint32_t v0 = (uint32_t)w0, v1 = (uint32_t)w1, r2 = (uint32_t)(w0 >> 16);
+        const bool okr = valid && offset_1 > 0 && ld32u(src + pc + 2 - (int32_t)offset_1) == r2;
+        bool ok0 = valid && tA0 > prefixStartIndex && ld32u(src + tA0 - 1) == v0;
+        bool ok1 = valid && tB0 > prefixStartIndex && ld32u(src + tB0 - 1) == v1;
+        int32_t tA = tA0, tB = tB0;
+        uint64_t sm = ballot(okr || ok0 || ok1);
+        uint64_t commit;
+        bool wA, wB;
+        if (sm & 1ull) {
+            // the first iteration succeeds on its own: it alone ran
+            commit = 1ull;
+            wA = lane == 0 && A != B;
+            wB = lane == 0;
+        } else {
+            // lanes whose writes share this lane's buckets (hashLog x 2 ballots)
+            uint64_t eqAA = ~0ull, eqBA = ~0ull, eqAB = ~0ull, eqBB = ~0ull;
+            for (uint32_t bit = 0; bit < hlog; bit++) {
+                const bool a = (A >> bit) & 1u, b = (B >> bit) & 1u;
+                const uint64_t bA = ballot(a), bB = ballot(b);
+                eqAA &= a ? bA : ~bA;
+                eqBA &= a ? bB : ~bB;
+                eqAB &= b ? bA : ~bA;
+                eqBB &= b ? bB : ~bB;
+            }
+            eqAA &= vmask;
+            eqBA &= vmask;
+            eqAB &= vmask;
+            eqBB &= vmask;
+            const uint64_t below = lanes_below(lane), above = lanes_above(lane);
+            // reads: the latest earlier write to the bucket (B after A within an iteration)
+            {
+                const uint64_t ea = eqAA & below, eb = eqBA & below;
+                const int ia = ea ? 63 - __builtin_clzll(ea) : -1, ib = eb ? 63 - __builtin_clzll(eb) : -1;
+                const int src_l = ib >= ia ? ib : ia;
+                const int32_t pv = __shfl(p, src_l < 0 ? (int)lane : src_l, 64);
+                if (src_l >= 0) tA = pv + (ib >= ia ? 2 : 1);
+            }
+            {
+                const uint64_t ea = eqAB & below, eb = eqBB & below;
+                const int ia = ea ? 63 - __builtin_clzll(ea) : -1, ib = eb ? 63 - __builtin_clzll(eb) : -1;
+                const int src_l = ib >= ia ? ib : ia;
+                const int32_t pv = __shfl(p, src_l < 0 ? (int)lane : src_l, 64);
+                if (src_l >= 0) tB = pv + (ib >= ia ? 2 : 1);
+            }
+            if (tA != tA0) ok0 = valid && tA > prefixStartIndex && ld32u(src + tA - 1) == v0;
+            if (tB != tB0) ok1 = valid && tB > prefixStartIndex && ld32u(src + tB - 1) == v1;
+            sm = ballot(okr || ok0 || ok1);
+            commit = sm ? ((sm & (0ull - sm)) << 1) - 1ull : vmask;  // iterations that ran
+            const bool in = (commit >> lane) & 1ull;
+            wA = in && A != B && !((eqAA | eqBA) & above & commit);
+            wB = in && !((eqAB | eqBB) & above & commit);
+        }
+        if (wA) T[A] = (uint32_t)(p + 1);
+        if (wB) T[B] = (uint32_t)(p + 2);
+        if (!sm) {
+            if (vmask != ~0ull) break;  // the serial loop ends inside this step
+            ip0 = anchor + unis(readlanes(d + (d >> 7) + 2, 63));
+            continue;
+        }
+        // ---- the match of the first successful iteration f ----
+        const int f = __builtin_ctzll(sm);
+        const int32_t pf = unis(readlanes(p, f));
+        const bool fr = (readlane((uint32_t)okr, f) & 1u) != 0, f0 = (readlane((uint32_t)ok0, f) & 1u) != 0;
+        const int32_t current0 = pf + 1;
+        int32_t match0;
+        uint32_t mLength, offcode;
+        if (fr) {
+            const int32_t ip2 = pf + 2, repMatch = ip2 - (int32_t)offset_1;
+            mLength = ld8(src + ip2 - 1) == ld8(src + repMatch - 1) ? 1u : 0u;
+            ip0 = ip2 - (int32_t)mLength;
+            match0 = repMatch - (int32_t)mLength;
+            mLength += 4;
+            offcode = 0;
+        } else {
+            if (f0) {
+                ip0 = pf;
+                match0 = unis(readlanes(tA, f)) - 1;
+            } else {
+                ip0 = pf + 1;
+                match0 = unis(readlanes(tB, f)) - 1;
+            }
+            offset_2 = offset_1;
+            offset_1 = (uint32_t)(ip0 - match0);
+            offcode = offset_1 + 2;
+            mLength = 4;
+            const uint32_t lim = (uint32_t)min(ip0 - anchor, match0 - prefixStart);
+            const uint32_t back = lim ? back_wave(src + ip0, src + match0, lim, lane) : 0u;
+            ip0 -= (int32_t)back;
+            match0 -= (int32_t)back;
+            mLength += back;
+        }
+        mLength += count_wave(src + ip0 + mLength, src + match0 + mLength, iendp, lane);
+        mLength = uni(mLength);
+        store_seq_wave(ss, src + anchor, (uint32_t)(ip0 - anchor), offcode, mLength - 3, lane);
+        ip0 += (int32_t)mLength;
+        anchor = ip0;
+        if (ip0 <= ilimit) {
+            if (lane == 0) {
+                T[hash_w(ld64u(src + current0 + 1), hlog, mls)] = (uint32_t)(current0 + 2);
+                T[hash_w(ld64u(src + ip0 - 2), hlog, mls)] = (uint32_t)(ip0 - 1);
+            }
+            while (ip0 <= ilimit && offset_2 > 0 && uni(ld32u(src + ip0)) == uni(ld32u(src + ip0 - (int32_t)offset_2))) {
+                const uint32_t rLength = uni(count_wave(src + ip0 + 4, src + ip0 + 4 - offset_2, iendp, lane)) + 4;
+                const uint32_t t = offset_2;
+                offset_2 = offset_1;
+                offset_1 = t;
+                if (lane == 0) T[hash_w(ld64u(src + ip0), hlog, mls)] = (uint32_t)(ip0 + 1);
+                ip0 += (int32_t)rLength;
+                store_seq_wave(ss, src + anchor, 0, 0, rLength - 3, lane);
+                anchor = ip0;
+            }
+        }
+    }
+    rep[0] = offset_1 ? offset_1 : offsetSaved;
+    rep[1] = offset_2 ? offset_2 : offsetSaved;
+    return (uint32_t)(iend - anchor);
+}
+
+// the entropy stage of one block, on one lane (called by lane 0 only)
+__device__ __noinline__ uint64_t block_body_lane(jzc::Work *W, jzc::SeqDef *seqs, uint8_t *lits, uint8_t *codes,
+                                                 uint32_t nseq, uint32_t nlit, uint32_t long_id, uint32_t long_pos,
+                                                 uint8_t *body, uint32_t bs) {
+    jzc::SeqStore ss;
+    ss.seq = seqs;
+    ss.lit = lits;
+    ss.llc = codes;
+    ss.mlc = codes + jzc::kMaxSeq;
+    ss.ofc = codes + 2 * jzc::kMaxSeq;
+    ss.nseq = nseq;
+    ss.nlit = nlit;
+    ss.long_id = long_id;
+    ss.long_pos = long_pos;
+    return jzc::compress_block_body(W->prev, W->next, ss, body, jzc::kBodyCap, bs, W->litCount, W->hufScratch, W->hw,
+                                    W->sw);
+}
+
+__device__ __noinline__ uint32_t frame_header_lane(uint8_t *dst, uint64_t n, jzc::Params P) {
+    return jzc::write_frame_header(dst, n, P);
+}
+
+// ZSTD_compress(level 1) of one object by the wave
+__device__ uint64_t compress_object(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *htab,
+                                    jzc::SeqDef *seqs, uint8_t *lits, uint8_t *codes, uint8_t *body, jzc::Work &W,
+                                    uint32_t lane) {
+    const jzc::Params P = jzc::level1_params(n);
+    __shared__ uint32_t bcast;
+    if (lane == 0) bcast = frame_header_lane(dst, n, P);
+    __syncthreads();
+    uint64_t op = uni(bcast);
+    if (n == 0) {
+        if (lane == 0) jzc::wr24(dst + op, 1);
+        return op + 3;
+    }
+    for (uint32_t i = 4 * lane; i < (1u << P.hlog); i += 256)
+        htab[i] = htab[i + 1] = htab[i + 2] = htab[i + 3] = 0;
+    for (uint32_t i = lane; i < 256; i += 64) W.prev.ct.nb[i] = 0, W.prev.ct.val[i] = 0;
+    if (lane == 0) W.prev.repeat = jzc::kHufNone;
+    uint32_t rep[2] = {1, 4};
+    const uint32_t blockMax = (1u << P.wlog) < jzc::kBlockMax ? (1u << P.wlog) : jzc::kBlockMax;
+    bool first = true;
+    for (uint64_t pos = 0; pos < n;) {
+        const uint32_t bs = (uint32_t)((n - pos) < blockMax ? (n - pos) : blockMax);
+        const uint32_t last = (pos + bs == n);
+        const uint8_t *ip = src + pos;
+        uint64_t cSize = 0;
+        if (bs >= 7) {
+            WSeq ss{seqs, lits, 0, 0, 0, 0};
+            uint32_t nrep[2] = {rep[0], rep[1]};
+            __syncthreads();  // the table clear / last block's work has landed
+            const uint32_t lastLL = parse_fast_wave(src, (int32_t)pos, (int32_t)(pos + bs), htab, P, nrep, ss, lane);
+            for (uint32_t o = lane; o < lastLL; o += 64)
+                *(gu8c *)(lits + ss.nlit + o) = (uint8_t)ld8(src + pos + bs - lastLL + o);
+            ss.nlit += lastLL;
+            __syncthreads();  // sequences and literals visible to lane 0
+            if (lane == 0)
+                bcast = (uint32_t)block_body_lane(&W, seqs, lits, codes, ss.nseq, ss.nlit, ss.long_id, ss.long_pos,
+                                                  body, bs);
+            __syncthreads();
+            cSize = uni(bcast);
+            if (!first && cSize < jzc::kRleMaxLength) {
+                const uint32_t b0 = ld8(ip);
+                bool diff = false;
+                for (uint32_t o = lane; o < bs; o += 64) diff |= ld8(ip + o) != b0;
+                if (!ballot(diff)) cSize = 1;
+            }
+            if (cSize > 1) {
+                rep[0] = uni(nrep[0]);
+                rep[1] = uni(nrep[1]);
+                // ZSTD_confirmRepcodesAndEntropyTables
+                for (uint32_t i = lane; i < 256; i += 64) W.prev.ct.nb[i] = W.next.ct.nb[i], W.prev.ct.val[i] = W.next.ct.val[i];
+                if (lane == 0) W.prev.repeat = W.next.repeat;
+            }
+        }
+        if (cSize == 0) {
+            if (lane == 0) jzc::wr24(dst + op, last + (bs << 3));
+            for (uint32_t o = lane; o < bs; o += 64) *(gu8c *)(dst + op + 3 + o) = (uint8_t)ld8(ip + o);
+            op += 3 + bs;
+        } else if (cSize == 1) {
+            if (lane == 0) {
+                jzc::wr24(dst + op, last + (1u << 1) + (bs << 3));
+                dst[op + 3] = ip[0];
+            }
+            op += 4;
+        } else {
+            if (lane == 0) jzc::wr24(dst + op, last + (2u << 1) + ((uint32_t)cSize << 3));
+            for (uint32_t o = lane; o < cSize; o += 64) *(gu8c *)(dst + op + 3 + o) = (uint8_t)ld8(body + o);
+            op += 3 + cSize;
+        }
+        pos += bs;
+        first = false;
+    }
+    return op;
+}
+}  // namespace
+
+// Persistent: wave w takes objects from *queue until none is left, so every
+// wave reaches the exit.  ZDev.len = input bytes, ZDev.cap >= ZSTD_compressBound.
+__global__ __launch_bounds__(64) void zstd_compress_k(const ZDev *__restrict__ blks, ZOut *__restrict__ outs,
+                                                      uint8_t *__restrict__ scratch, uint32_t *queue, int n) {
+    __shared__ jzc::Work W;
+    __shared__ int next;
+    const uint32_t lane = threadIdx.x;
+    uint8_t *const sc = scratch + (size_t)blockIdx.x * kZcScratchStride;
+    uint32_t *const htab = (uint32_t *)sc;
+    jzc::SeqDef *const seqs = (jzc::SeqDef *)(sc + kZcHtab);
+    uint8_t *const lits = sc + kZcHtab + kZcSeq;
+    uint8_t *const codes = lits + kZcLit;
+    uint8_t *const body = codes + kZcCodes;
+    for (;;) {
+        if (lane == 0) next = (int)atomicAdd(queue, 1u);
+        __syncthreads();
+        const int obj = unis(next);
+        __syncthreads();
+        if (obj >= n) break;
+        const ZDev b = blks[obj];
+#ifdef JFSX_ZC_SCALAR
+        if (lane == 0) {
+            outs[obj].out_len = jzc::compress_frame(b.src, b.len, b.dst, htab, seqs, lits, codes, body, W);
+            outs[obj].status = JFSX_OK;
+        }
+#else
+        const uint64_t r = compress_object(b.src, b.len, b.dst, htab, seqs, lits, codes, body, W, lane);
+        if (lane == 0) {
+            outs[obj].out_len = r;
+            outs[obj].status = JFSX_OK;
+        }
+#endif
+    }
+}
+
+void launch_zstd_compress(hipStream_t s, int n, int waves, const ZDev *blks, ZOut *outs, uint8_t *scratch,
+                          uint32_t *queue) {
+    if (n <= 0) return;
+    (void)hipMemsetAsync(queue, 0, 4, s);
+    hipLaunchKernelGGL(zstd_compress_k, dim3(waves), dim3(64), 0, s, blks, outs, scratch, queue, n);
+}
+
+}  // namespace jfsx

@@ -42,7 +42,8 @@ EXPORTS = [
     "jfsx_agg_dev_batches", "jfsx_lz4_bound", "jfsx_lz4_compress_batch", "jfsx_lz4_decompress_batch",
     "jfsx_agg_lz4_compress", "jfsx_agg_lz4_decompress", "jfsx_mctx_lz4_compress_batch", "jfsx_mctx_lz4_decompress_batch",
     "jfsx_zstd_decompress_batch", "jfsx_agg_zstd_decompress", "jfsx_mctx_zstd_decompress_batch",
-    "jfsx_last_error",
+    "jfsx_last_error", "jfsx_zstd_bound", "jfsx_zstd_compress_batch", "jfsx_agg_zstd_compress",
+    "jfsx_mctx_zstd_compress_batch",
 ]
 
 
@@ -178,6 +179,10 @@ def load_library(path=LIB_PATH):
             "jfsx_zstd_decompress_batch": (I, [P, I, ctypes.POINTER(jfsx_zblk), I]),
             "jfsx_agg_zstd_decompress": (I, [P, ctypes.POINTER(jfsx_zblk), I]),
             "jfsx_mctx_zstd_decompress_batch": (I, [P, I, ctypes.POINTER(jfsx_zblk), I]),
+            "jfsx_zstd_bound": (U64, [U64]),
+            "jfsx_zstd_compress_batch": (I, [P, I, ctypes.POINTER(jfsx_zblk), I]),
+            "jfsx_agg_zstd_compress": (I, [P, ctypes.POINTER(jfsx_zblk), I]),
+            "jfsx_mctx_zstd_compress_batch": (I, [P, I, ctypes.POINTER(jfsx_zblk), I]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -227,6 +232,11 @@ def lz4_bound(n):
     return load_library().jfsx_lz4_bound(n)
 
 
+def zstd_bound(n):
+    """ZSTD_compressBound (compress.go:80 CompressBound)."""
+    return load_library().jfsx_zstd_bound(n)
+
+
 def device_count():
     n = ctypes.c_int()
     rc = load_library().jfsx_device_count(ctypes.byref(n))
@@ -242,7 +252,7 @@ class DeviceBuffer:
         p = ctypes.c_void_p()
         rc = eng.L.jfsx_alloc_device(eng.ctx, max(self.nbytes, 16), ctypes.byref(p))
         if rc:
-            raise EngineError(rc, "jfsx_alloc_device(%d)" % nbytes)
+            _raise(eng.ctx, rc, "jfsx_alloc_device(%d)" % nbytes)
         self.ptr = p.value
 
     def free(self):
@@ -404,6 +414,18 @@ class Engine:
     # -- Zstandard decompression (jfsx_zstd_decompress_batch) -------------
     def zstd_decompress_batch(self, zblks, n, mem=MEM_DEVICE):
         self._check(self.L.jfsx_zstd_decompress_batch(self.ctx, n, zblks, mem), "jfsx_zstd_decompress_batch")
+
+    def zstd_compress_batch(self, zblks, n, mem=MEM_DEVICE):
+        self._check(self.L.jfsx_zstd_compress_batch(self.ctx, n, zblks, mem), "jfsx_zstd_compress_batch")
+
+    def zstd_compress(self, datas):
+        """Host buffers in; list of level-1 zstd frames out (one GPU batch)."""
+        srcs = [_u8(d) for d in datas]
+        caps = [int(zstd_bound(s.size)) for s in srcs]
+        dsts = [np.empty(max(c, 1), np.uint8) for c in caps]
+        arr, n = self.make_zblocks((s.ctypes.data, s.size, d.ctypes.data, c) for s, d, c in zip(srcs, dsts, caps))
+        self.zstd_compress_batch(arr, n, MEM_HOST)
+        return [d[:arr[i].out_len].tobytes() for i, d in enumerate(dsts)]
 
     def zstd_decompress(self, datas, caps):
         """Host buffers of zstd frames in; list of (status, bytes) out (dst of caps[i] bytes)."""
@@ -648,6 +670,9 @@ class MultiEngine:
     def zstd_decompress_batch(self, zblks, n, mem=MEM_HOST):
         self._check(self.L.jfsx_mctx_zstd_decompress_batch(self.m, n, zblks, mem), "jfsx_mctx_zstd_decompress_batch")
 
+    def zstd_compress_batch(self, zblks, n, mem=MEM_HOST):
+        self._check(self.L.jfsx_mctx_zstd_compress_batch(self.m, n, zblks, mem), "jfsx_mctx_zstd_compress_batch")
+
 
 class Aggregator:
     """jfsx_agg: per-block calls from many threads coalesced into batches
@@ -710,6 +735,10 @@ class Aggregator:
 
     def zstd_decompress(self, z, mem=MEM_HOST):
         self.eng._check(self.L.jfsx_agg_zstd_decompress(self.h, ctypes.byref(z), mem), "jfsx_agg_zstd_decompress")
+
+    def zstd_compress(self, z, mem=MEM_HOST):
+        """z: a jfsx_zblk, dst_cap >= zstd_bound(src_len)."""
+        self.eng._check(self.L.jfsx_agg_zstd_compress(self.h, ctypes.byref(z), mem), "jfsx_agg_zstd_compress")
 
     def stats(self):
         """(calls, batches, blocks carried by those batches)"""

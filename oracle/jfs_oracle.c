@@ -1118,3 +1118,156 @@ ORC_EXPORT double orc_bench_seal_crc_evp(int algo, int nthreads, uint64_t nblock
     if (digest) *digest = dg;
     return rc ? -1.0 : el;
 }
+
+/* ------------------------------------------------------------------ */
+/* CPU baselines for every BASELINE config (bench.py cpu_baseline):    */
+/*   mode 0  seal: checksum(p) + EVP Seal         (configs[1], [2], [4]) */
+/*   mode 1  open: EVP Open (tag checked) + checksum(p) compared with   */
+/*           the stored CRCs, as cacheFile.ReadAt's verify does         */
+/*           (encrypt.go:196-216 + disk_cache.go:1315-1327; configs[3])  */
+/*   mode 2  CRC verify only (cache hit, disk_cache.go:1255-1329)        */
+/* Block b has lens[b] bytes (lens NULL: blen each; configs[4] ragged).  */
+/* Inputs (and, for open, the sealed images) are made before the clock */
+/* starts.  Returns wall seconds, -1 without libcrypto (modes 0/1), -2  */
+/* if any block failed to open or verify.                               */
+/* ------------------------------------------------------------------ */
+typedef int (*evp_dinit_t)(void *, const void *, void *, const uint8_t *, const uint8_t *);
+typedef int (*evp_dupdate_t)(void *, uint8_t *, int *, const uint8_t *, int);
+typedef int (*evp_dfinal_t)(void *, uint8_t *, int *);
+static evp_dinit_t evp_dinit;
+static evp_dupdate_t evp_dupdate;
+static evp_dfinal_t evp_dfinal;
+
+static int evp_load_open(void) {
+    if (!evp_load()) return 0;
+    if (!evp_dinit) {
+        void *h = dlopen("libcrypto.so.3", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return 0;
+        evp_dinit = (evp_dinit_t)dlsym(h, "EVP_DecryptInit_ex");
+        evp_dupdate = (evp_dupdate_t)dlsym(h, "EVP_DecryptUpdate");
+        evp_dfinal = (evp_dfinal_t)dlsym(h, "EVP_DecryptFinal_ex");
+    }
+    return evp_dinit && evp_dupdate && evp_dfinal;
+}
+
+/* one Open through EVP: 0 ok, -1 tag mismatch or error */
+static int evp_open(void *ctx, int algo, const uint8_t key[32], const uint8_t nonce[12], const uint8_t *c,
+                    uint64_t len, const uint8_t tag[16], uint8_t *p) {
+    if (evp_dinit(ctx, algo == ALGO_AES256GCM ? evp.gcm() : evp.chacha(), NULL, key, nonce) != 1) return -1;
+    uint64_t off = 0;
+    while (off < len) {
+        int chunk = len - off > (1u << 30) ? (1 << 30) : (int)(len - off), out = 0;
+        if (evp_dupdate(ctx, p + off, &out, c + off, chunk) != 1) return -1;
+        off += (uint64_t)chunk;
+    }
+    if (evp.ctrl(ctx, 0x11 /* EVP_CTRL_AEAD_SET_TAG */, 16, (void *)tag) != 1) return -1;
+    int fin = 0;
+    return evp_dfinal(ctx, p + len, &fin) == 1 ? 0 : -1;
+}
+
+typedef struct {
+    int algo, mode;
+    uint64_t seed, b0, b1, maxlen;
+    const uint64_t *lens;
+    uint8_t *in, *work, *tags, *crcs;  /* per block: maxlen bytes of input, 16-B tag, CRC array */
+    uint64_t crcstride;
+    uint32_t digest;
+    int bad;
+} base_job;
+
+static uint64_t base_len(const base_job *j, uint64_t b) { return j->lens ? j->lens[b] : j->maxlen; }
+
+static void *base_worker(void *arg) {
+    base_job *j = (base_job *)arg;
+    void *ctx = j->mode == 2 ? NULL : evp.ctx_new();
+    uint8_t *mycrc = (uint8_t *)malloc((size_t)j->crcstride);
+    uint32_t dg = 0;
+    for (uint64_t b = j->b0; b < j->b1; b++) {
+        const uint64_t n = base_len(j, b), k = b - j->b0;
+        uint8_t key[32], nonce[12], tag[16];
+        orc_gen_key(j->seed, b, key, nonce);
+        uint8_t *in = j->in + k * j->maxlen;
+        if (j->mode == 0) {
+            orc_checksum(in, (int64_t)n, mycrc, 1);
+            if (evp_seal(ctx, j->algo, key, nonce, in, n, j->work, tag)) j->bad = 1;
+            dg ^= le32(tag) ^ le32(mycrc);
+        } else if (j->mode == 1) {
+            if (evp_open(ctx, j->algo, key, nonce, in, n, j->tags + 16 * k, j->work)) j->bad = 1;
+            const int64_t cl = orc_checksum(j->work, (int64_t)n, mycrc, 1);
+            if (memcmp(mycrc, j->crcs + k * j->crcstride, (size_t)cl)) j->bad = 1;
+            dg ^= le32(mycrc);
+        } else {
+            const int64_t cl = orc_checksum(in, (int64_t)n, mycrc, 1);
+            if (memcmp(mycrc, j->crcs + k * j->crcstride, (size_t)cl)) j->bad = 1;
+            dg ^= le32(mycrc);
+        }
+    }
+    if (ctx) evp.ctx_free(ctx);
+    free(mycrc);
+    j->digest = dg;
+    return NULL;
+}
+
+ORC_EXPORT double orc_bench_baseline(int algo, int mode, int nthreads, uint64_t nblocks, const uint64_t *lens,
+                                     uint64_t blen, uint64_t seed, uint32_t *digest) {
+    if (mode < 0 || mode > 2) return -3.0;
+    if (mode != 2 && !evp_load_open()) return -1.0;
+    if (nthreads < 1) nthreads = 1;
+    uint64_t maxlen = blen;
+    if (lens)
+        for (uint64_t b = 0; b < nblocks; b++) maxlen = lens[b] > maxlen ? lens[b] : maxlen;
+    const uint64_t crcstride = (uint64_t)orc_checksum_len((int64_t)maxlen);
+    base_job *jobs = (base_job *)calloc((size_t)nthreads, sizeof(base_job));
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    const uint64_t per = (nblocks + nthreads - 1) / nthreads;
+    void *sctx = mode == 1 ? evp.ctx_new() : NULL;
+    for (int t = 0; t < nthreads; t++) {
+        base_job *j = &jobs[t];
+        j->algo = algo;
+        j->mode = mode;
+        j->seed = seed;
+        j->lens = lens;
+        j->maxlen = maxlen;
+        j->crcstride = crcstride;
+        j->b0 = (uint64_t)t * per < nblocks ? (uint64_t)t * per : nblocks;
+        j->b1 = j->b0 + per < nblocks ? j->b0 + per : nblocks;
+        const uint64_t nb = j->b1 - j->b0;
+        j->in = (uint8_t *)malloc(nb ? nb * maxlen : 1);
+        j->work = (uint8_t *)malloc(maxlen + 16);
+        j->tags = (uint8_t *)malloc(nb ? 16 * nb : 1);
+        j->crcs = (uint8_t *)malloc(nb ? nb * crcstride : 1);
+        for (uint64_t b = j->b0; b < j->b1; b++) {
+            const uint64_t n = base_len(j, b), k = b - j->b0;
+            uint8_t *in = j->in + k * maxlen;
+            orc_gen_block(seed, b, in, n);
+            orc_checksum(in, (int64_t)n, j->crcs + k * crcstride, 1);  /* the cache file's stored CRCs */
+            if (mode == 1) {  /* stored object: seal it, keep ciphertext and tag */
+                uint8_t key[32], nonce[12];
+                orc_gen_key(seed, b, key, nonce);
+                if (evp_seal(sctx, algo, key, nonce, in, n, j->work, j->tags + 16 * k)) j->bad = 1;
+                memcpy(in, j->work, (size_t)n);
+            }
+        }
+    }
+    if (sctx) evp.ctx_free(sctx);
+    double t0 = now_s();
+    for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, base_worker, &jobs[t]);
+    uint32_t dg = 0;
+    int bad = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        dg ^= jobs[t].digest;
+        bad |= jobs[t].bad;
+    }
+    double el = now_s() - t0;
+    for (int t = 0; t < nthreads; t++) {
+        free(jobs[t].in);
+        free(jobs[t].work);
+        free(jobs[t].tags);
+        free(jobs[t].crcs);
+    }
+    free(jobs);
+    free(th);
+    if (digest) *digest = dg;
+    return bad ? -2.0 : el;
+}

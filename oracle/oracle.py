@@ -60,6 +60,7 @@ def lib():
             "orc_data_encrypt": (I64, [I, P, P, P, I, P, U64, P]),
             "orc_data_decrypt": (I64, [I, P, P, I64, P]),
             "orc_bench_seal_crc": (ctypes.c_double, [I, I, U64, U64, U64, P]),
+            "orc_bench_baseline": (ctypes.c_double, [I, I, I, U64, P, U64, U64, P]),
             "orc_lz4_bound": (I, [I]),
             "orc_lz4_compress": (I, [P, I, P, I]),
             "orc_lz4_decompress": (I, [P, I, P, I]),
@@ -249,6 +250,21 @@ def bench_seal_crc_evp(algo, nthreads, nblocks, blen, seed):
     """(seconds, digest), seconds < 0 if libcrypto is absent."""
     dg = ctypes.c_uint32()
     secs = lib().orc_bench_seal_crc_evp(algo, nthreads, nblocks, blen, seed, ctypes.byref(dg))
+    return secs, dg.value
+
+
+BASE_SEAL, BASE_OPEN, BASE_CRC = 0, 1, 2
+
+
+def bench_baseline(algo, mode, nthreads, nblocks, blen, seed, lens=None):
+    """(seconds, digest) of the CPU baseline for mode BASE_SEAL (checksum +
+    EVP Seal), BASE_OPEN (EVP Open + CRC verify against the stored CRCs) or
+    BASE_CRC (CRC verify only) over nblocks synthetic blocks of blen bytes
+    (or lens[b]); seconds -1 without libcrypto, -2 if a block failed."""
+    dg = ctypes.c_uint32()
+    ln = np.asarray(lens, np.uint64) if lens is not None else None
+    secs = lib().orc_bench_baseline(algo, mode, nthreads, nblocks, ln.ctypes.data if ln is not None else None, blen,
+                                    seed, ctypes.byref(dg))
     return secs, dg.value
 
 

@@ -102,6 +102,16 @@ int jfsx_zstd_decompress_batch(jfsx_ctx *c, int n, jfsx_zblk *z, int mem) {
     return 0;
 }
 
+// fake zstd compress: out_len = src_len / 3 + 9
+int jfsx_zstd_compress_batch(jfsx_ctx *c, int n, jfsx_zblk *z, int mem) {
+    stub(c, 6, n, 0, n ? z[0].src_len : 0);
+    for (int i = 0; i < n; i++) {
+        z[i].out_len = z[i].src_len / 3 + 9;
+        z[i].status = JFSX_OK;
+    }
+    return 0;
+}
+
 int jfsx_device_count(int *n) {
     *n = h_ndev;
     return h_ndev ? 0 : JFSX_ENODEV;

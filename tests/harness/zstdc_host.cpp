@@ -13,12 +13,12 @@ extern "C" int64_t zstdc_host_compress(const uint8_t *src, int64_t n, uint8_t *d
     if ((uint64_t)cap < jzc::compress_bound((uint64_t)n)) return -1;
     static thread_local std::vector<uint32_t> htab(1u << jzc::kHashLogMax);
     static thread_local std::vector<jzc::SeqDef> seqs(jzc::kMaxSeq);
-    static thread_local std::vector<uint8_t> lits(jzc::kBlockMax + 64), codes(3 * jzc::kMaxSeq);
+    static thread_local std::vector<uint8_t> lits(jzc::kBlockMax + 64), codes(3 * jzc::kMaxSeq), body(jzc::kBodyCap);
     static thread_local jzc::Work w;
     // exactly sized copies, so an ASan build sees any read past the input
     std::vector<uint8_t> in(src, src + n);
     return (int64_t)jzc::compress_frame(in.data(), (uint64_t)n, dst, htab.data(), seqs.data(), lits.data(),
-                                        codes.data(), w);
+                                        codes.data(), body.data(), w);
 }
 
 extern "C" uint64_t zstdc_host_bound(uint64_t n) { return jzc::compress_bound(n); }

@@ -25,18 +25,24 @@ def test_failed_allocation_names_the_hip_error(eng):
     assert err.code == E.ENOMEM
     assert err.hip_error != 0 and "hipMalloc" in err.detail and "jfsx_api.cpp" in err.detail
     assert eng.last_error() == (err.hip_error, err.detail)
-    # the context stays usable after a failed allocation
+    # the context stays usable after a failed allocation, and the handled
+    # failure does not resurface as the next batch's launch error (a stale
+    # hipGetLastError() once turned it into JFSX_EIO)
     buf = eng.alloc(1 << 20)
     buf.free()
+    assert eng.lz4_compress([b"abcd" * 100]) == [orc.lz4_compress(b"abcd" * 100)]
+    assert eng.zstd_compress([b"zstd" * 100])[0][:4] == b"\x28\xb5\x2f\xfd"
 
 
 def test_lz4_match_in_first_bytes():
     # jfsx_lz4.hip count_and_back: with the 4-byte test and the count in one
-    # round of loads (skip = 0), a match candidate at block positions 0..2 put
-    # lane 0's match dword before byte 0 (an unsigned wrap to src + ~4 GiB);
-    # the intermediate build of 84c5bd5 faulted there (gpurun_out/lz4cab_c2:
-    # jfsx error -5 on test_golden_batch_host).  Blocks that open with repeats
-    # of period 1..4, across the small-table boundary.
+    # round of loads (skip = 0), a match candidate at block positions 0..2
+    # puts lane 0's match dword before byte 0; 84c5bd5 guards it (mps < 0).
+    # The r2 JFSX_EIO (gpurun_out/lz4cab_c2, an uncommitted build between
+    # 31a22e9 and 84c5bd5) came back cleanly in 1.3 s, with no memory-access
+    # fault abort, so it was an API-level error; this covers the
+    # inputs that guard is for.  Blocks that open with repeats of period 1..4,
+    # across the small-table boundary.
     e = E.Engine(0)
     try:
         srcs = []

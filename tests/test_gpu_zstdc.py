@@ -1,0 +1,103 @@
+"""GPU Zstandard level-1 compression (jfsx_zstd_compress_batch,
+jfsx_zstdc.hip) against the system zstd library: every frame equals
+ZSTD_compress(src, level 1) byte for byte -- what zstd.CompressLevel writes
+for the "zstd" Compressor (pkg/compress/compress.go:82-91) -- over the data
+kinds and sizes of the host test, mixed inputs with matches and repcodes at
+the 512 KiB window edge, device-resident unaligned buffers, and through the
+compress.go mirror and the chunk-store upload step."""
+import numpy as np
+import pytest
+
+from juicefs_amd import engine as E
+from tests import lz4_data, zstd_lib
+from tests.test_zstdc_host import SIZES, mixed
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = E.Engine(0)
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("kind", lz4_data.KINDS)
+def test_frames_equal_libzstd_level1(eng, kind):
+    srcs = [lz4_data.sample(kind, n, seed=n + 1) for n in SIZES]
+    got = eng.zstd_compress(srcs)
+    for n, s, g in zip(SIZES, srcs, got):
+        assert g == zstd_lib.compress_simple(s, 1), (kind, n)
+
+
+def test_mixed_inputs_equal_libzstd_level1(eng):
+    srcs = []
+    for seed in range(12):
+        rng = np.random.default_rng(seed + 1000)
+        n = int(rng.choice([rng.integers(1, 5000), rng.integers(5000, 300000), rng.integers(300000, 4 << 20)]))
+        srcs.append(mixed(seed, n))
+    got = eng.zstd_compress(srcs)
+    for seed, (s, g) in enumerate(zip(srcs, got)):
+        assert g == zstd_lib.compress_simple(s, 1), seed
+
+
+def test_device_batch_unaligned_and_round_trip(eng):
+    rng = np.random.default_rng(11)
+    n = 40
+    lens = [int(x) for x in rng.integers(0, 600000, n)]
+    srcs = [lz4_data.sample(lz4_data.KINDS[i % 6], lens[i], seed=70 + i) for i in range(n)]
+    caps = [int(E.zstd_bound(L)) for L in lens]
+    inb = eng.alloc(sum(L + 8 for L in lens) + 16)
+    outb = eng.alloc(sum(c + 8 for c in caps) + 16)
+    ioff, ooff, specs = 3, 5, []
+    for s, L, c in zip(srcs, lens, caps):
+        inb.upload(np.frombuffer(s, np.uint8), ioff) if L else None
+        specs.append((inb.ptr + ioff, L, outb.ptr + ooff, c))
+        ioff += L + 7
+        ooff += c + 5
+    arr, k = eng.make_zblocks(specs)
+    eng.zstd_compress_batch(arr, k, E.MEM_DEVICE)
+    frames = []
+    for i, s in enumerate(srcs):
+        assert arr[i].status == E.OK
+        f = outb.download(arr[i].out_len, specs[i][2] - outb.ptr).tobytes()
+        assert f == zstd_lib.compress_simple(s, 1), i
+        frames.append(f)
+    back = eng.zstd_decompress(frames, lens)
+    assert all(st == E.OK and d == s for (st, d), s in zip(back, srcs))
+
+
+def test_capacity_below_bound_is_rejected(eng):
+    src = np.frombuffer(lz4_data.sample("text", 5000, seed=1), np.uint8)
+    dst = np.empty(int(E.zstd_bound(5000)), np.uint8)
+    arr, k = eng.make_zblocks([(src.ctypes.data, 5000, dst.ctypes.data, dst.size - 1)])
+    with pytest.raises(E.EngineError) as ei:
+        eng.zstd_compress_batch(arr, k, E.MEM_HOST)
+    assert ei.value.code == E.EINVAL
+
+
+def test_mirror_compress_and_upload_blocks(eng):
+    """compress.go:82-91 (ZStandard.Compress) and cachedStore.upload's
+    compress step (cached_store.go:371-392) through the engine."""
+    from juicefs_amd import compress as C
+    z = C.NewCompressor("zstd", eng)
+    src = lz4_data.sample("text", 300000, seed=9)
+    dst = bytearray(z.CompressBound(len(src)))
+    n = z.Compress(dst, src)
+    assert bytes(dst[:n]) == zstd_lib.compress_simple(src, 1)
+
+    class Store:
+        def __init__(self):
+            self.d = {}
+
+        def Put(self, k, v):
+            self.d[k] = bytes(v)
+
+        def Get(self, k, off, lim):
+            return self.d[k]
+    st = Store()
+    blocks = [lz4_data.sample(k, 4 << 20, seed=i) for i, k in enumerate(("text", "runs", "random"))]
+    keys = ["chunks/0/0/%d_0_%d" % (i, len(b)) for i, b in enumerate(blocks)]
+    outs = C.upload_blocks(st, keys, blocks, z)
+    assert outs == [zstd_lib.compress_simple(b, 1) for b in blocks]
+    assert C.load_blocks(st, keys, [len(b) for b in blocks], z) == blocks
