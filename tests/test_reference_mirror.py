@@ -113,5 +113,11 @@ def test_compress_bounds_and_noop_errors():
     assert nop.Decompress(bytearray(4), b"abcd") == 4
     with pytest.raises(C.CompressError, match="decompress an empty input"):
         lz.Decompress(bytearray(10), b"")
-    with pytest.raises(NotImplementedError):
-        C.ZStandard().Compress(bytearray(10), b"x")
+    # zstd.CompressLevel allocates its own buffer below CompressBound, which
+    # compress.go:87-89 reports; an empty frame input is DataDog's empty-slice
+    # error (both decided before any engine call)
+    z = C.ZStandard()
+    with pytest.raises(C.CompressError, match="buffer too short: 10 < %d" % z.CompressBound(1)):
+        z.Compress(bytearray(10), b"x")
+    with pytest.raises(C.CompressError, match="Bytes slice is empty"):
+        z.Decompress(bytearray(10), b"")
