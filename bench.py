@@ -37,11 +37,14 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--blocks", type=int, default=16384, help="4 MiB blocks per GPU (16384 = 64 GiB)")
     ap.add_argument("--block-bytes", type=int, default=BLOCK)
-    ap.add_argument("--mode", choices=["seal", "open", "crc", "decrypt", "agg", "lz4", "unlz4", "zstd", "unzstd"], default="seal",
+    ap.add_argument("--mode", choices=["seal", "open", "crc", "decrypt", "agg", "aggcodec", "lz4", "unlz4", "zstd", "unzstd"], default="seal",
                     help="decrypt = dataEncryptor.Decrypt end to end: batched RSA-OAEP key unwrap + Open + CRC verify; "
                          "agg = one-block Seal calls from --threads threads on pinned host blocks, through the "
                          "aggregator (jfsx_agg) and, for comparison, as direct one-block batches")
     ap.add_argument("--threads", type=int, default=32, help="agg: submitting threads (reference: goroutines)")
+    ap.add_argument("--codec", choices=["lz4", "unlz4", "zstd", "unzstd"], default="zstd",
+                    help="aggcodec: the Compress / Decompress call of cachedStore.upload / load measured in the "
+                         "reference's call shape")
     ap.add_argument("--agg-window-us", type=int, default=500, help="agg: aggregation window")
     ap.add_argument("--algo", choices=["aes256gcm", "chacha20poly1305"], default="aes256gcm")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
@@ -213,6 +216,8 @@ def main():
     eng = E.Engine(local, E.CTX_BITSLICE if args.aes == "bitslice" else 0)
     if args.mode == "agg":
         return agg_bench(args, world, rank, local, dist, eng)
+    if args.mode == "aggcodec":
+        return aggcodec_bench(args, world, rank, local, dist, eng)
     if args.mode in ("lz4", "unlz4"):
         return lz4_bench(args, world, rank, local, dist, eng)
     if args.mode == "unzstd":
@@ -368,7 +373,7 @@ def main():
             cpu["value"] = round(cpu["cores"] * BLOCK / (per_block + rsa["host_us_per_unwrap_1thread"] * 1e-6) / 1e9, 3)
             cpu["sample"] += "; plus one libcrypto RSA-OAEP unwrap per block (%.1f us, measured on 1 thread)" % (
                 rsa["host_us_per_unwrap_1thread"])
-    traffic, traffic_src = pmc_traffic(args, sum(lens)) if not args.ragged else (None, None)
+    traffic, traffic_src, binding = pmc_traffic(args, sum(lens))
     if rank == 0:
         line = {
             "metric": ("sealed+checksummed GB/s, %s" if args.mode == "seal" else
@@ -392,7 +397,8 @@ def main():
                          "traffic_source": traffic_src,
                          "kernel": ("crc_segments_k" if args.mode == "crc" else
                                     ("gcm_main_k" if args.algo == "aes256gcm" else "cp_main_k")),
-                         "kernel_avg_ms": round(k_avg_ms, 3), "algorithmic_bytes_per_launch": algo_bytes},
+                         "kernel_avg_ms": round(k_avg_ms, 3), "algorithmic_bytes_per_launch": algo_bytes,
+                         "plain_bytes_per_launch": sum(lens), "binding": binding},
             "cpu_baseline": cpu,
             "verified_blocks": verified,
             **({"rsa_unwrap": rsa} if rsa else {}),
@@ -403,23 +409,49 @@ def main():
         dist.destroy_process_group()
 
 
-PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r2", "pmc_traffic.json")
+PMC_R3 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r3", "pmc_r3.json")
+
+
+def pmc_variant(args):
+    """The key of this bench line in profiles/r3/pmc_r3.json."""
+    if args.mode == "crc":
+        return "crc_verify"
+    if args.mode in ("lz4", "unlz4", "zstd", "unzstd"):
+        return "%s_%s" % (args.mode, args.lz4_data)
+    if args.mode not in ("seal", "open", "decrypt"):
+        return None
+    algo = "gcm" if args.algo == "aes256gcm" else "chacha"
+    if args.mem == "host":
+        return "ingest_" + algo
+    v = "%s_%s" % ("seal" if args.mode == "seal" else "open", algo)
+    if algo == "gcm" and args.aes == "bitslice":
+        v += "_bitslice"
+    return v + ("_ragged" if args.ragged else "")
 
 
 def pmc_traffic(args, plain_per_launch):
-    """HBM bytes per launch of the dominant kernel from the committed PMC passes
-    (FETCH_SIZE/WRITE_SIZE of the same kernel on a 4 GiB batch, corrected as the
-    MI355X guide prescribes, scaled per plaintext byte); None when no pass
-    covers this variant."""
-    key = {("seal", "aes256gcm"): "gcm_" + args.aes, ("seal", "chacha20poly1305"): "chacha"}.get(
-        (args.mode, args.algo), "crc_verify" if args.mode == "crc" else None)
+    """(traffic, source, binding) of the dominant kernel from the committed
+    round-3 PMC passes (scripts/pmc_r3.py): traffic = HBM bytes per launch
+    (FETCH_SIZE / WRITE_SIZE of the same variant's 64 GiB pass, or its own
+    batch size where stated, corrected as the MI355X guide prescribes, per
+    plaintext byte x this launch's plaintext bytes); binding = the LDS and
+    VALU busy fractions of the same kernel (SQ counters, 4 GiB pass).  None
+    where no pass covers this variant."""
+    key = pmc_variant(args)
     try:
-        k = json.load(open(PMC_TRAFFIC))["kernels"][key]
-    except (OSError, KeyError, ValueError):
-        return None, None
-    if args.crc != "full":
-        return None, None
-    return int(k["bytes_per_plain_byte"] * plain_per_launch), "profiles/r2/pmc_traffic.json (%s, %s)" % (k["kernel"], k.get("batch", ""))
+        v = json.load(open(PMC_R3))["variants"][key]
+    except (OSError, KeyError, ValueError, TypeError):
+        return None, None, None
+    if args.crc != "full" and args.mode == "seal":
+        return None, None, None
+    traffic = src = binding = None
+    if "bytes_per_plain_byte" in v:
+        traffic = int(v["bytes_per_plain_byte"] * plain_per_launch)
+        src = "profiles/r3/pmc_r3.json %s (%s; %s)" % (key, v.get("fetch_pass"), v.get("write_pass"))
+    if "lds_busy" in v or "valu_issue" in v:
+        binding = {k: v[k] for k in ("lds_busy", "valu_issue", "lds_conflict_share") if k in v}
+        binding["source"] = "profiles/r3/pmc_r3.json %s (%s)" % (key, v.get("lds_pass") or v.get("valu_pass"))
+    return traffic, src, binding
 
 
 def pcie_probe(eng, nbytes=1 << 30):
@@ -498,6 +530,8 @@ def host_ingest(args, world, rank, local, dist, eng):
             verified += 1
     value = world * nb * L * args.steps / el / 1e9
     cpu = cpu_baseline(args, "seal") if rank == 0 and world == 1 and not args.no_cpu else None
+    plain_launch = int(nb * L * args.steps / max(k_n, 1))
+    traffic, traffic_src, binding = pmc_traffic(args, plain_launch)
     if rank == 0:
         peak = min(pcie["h2d"], pcie["d2h"])
         print(json.dumps({
@@ -509,8 +543,10 @@ def host_ingest(args, world, rank, local, dist, eng):
                                    "3-slot H2D|transform|D2H ring" % (nb * L / 2**30, args.steps, args.algo),
                        "blocks_per_gpu": nb, "block_bytes": L, "algo": args.algo, "mem": "host"},
             "roofline": {"bound": "pcie", "achieved": round(value, 2), "peak": peak, "unit": "GB/s",
-                         "frac": round(value / peak, 4), "traffic": None, "pcie_measured": pcie,
-                         "kernel_avg_ms": round(k_ms / max(k_n, 1), 3), "kernel_launches": k_n},
+                         "frac": round(value / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
+                         "traffic_note": "HBM bytes per launch of gcm_main_k (one launch per ring slot)",
+                         "pcie_measured": pcie, "kernel_avg_ms": round(k_ms / max(k_n, 1), 3),
+                         "kernel_launches": k_n, "plain_bytes_per_launch": plain_launch, "binding": binding},
             "cpu_baseline": cpu, "verified_blocks": verified}), flush=True)
     eng.free_pinned(hin)
     eng.free_pinned(hout)
@@ -611,6 +647,132 @@ def agg_bench(args, world, rank, local, dist, eng):
             "direct_one_block_calls_GBs": round(nb * L * d_steps / d_el / 1e9, 2),
             "roofline": None, "cpu_baseline": cpu, "verified_blocks": verified}), flush=True)
     for h in (hin, hout, hcrc):
+        eng.free_pinned(h)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def aggcodec_bench(args, world, rank, local, dist, eng):
+    """The codec stage in the reference's call shape: cachedStore.upload /
+    load call Compress / Decompress once per block, from up to max-uploads
+    (default 20, cmd/flags.go:125-128) goroutines (cached_store.go:387, :738).
+    Blocks are 4 MiB of word text in pinned host memory.  value = uncompressed
+    GB/s of one-block calls through the aggregator (jfsx_agg) from --threads
+    threads; beside it the same blocks as one 256-block batch call and as
+    one-block calls on the context (no aggregator), and the C library on
+    every host core."""
+    import ctypes
+    import threading
+    import numpy as np
+    from juicefs_amd import engine as E
+    from tests import zstd_lib
+    L = args.block_bytes
+    nb = min(args.blocks, 256)
+    codec = args.codec
+    comp = codec in ("lz4", "zstd")
+    bound = int(E.lz4_bound(L) if codec in ("lz4", "unlz4") else E.zstd_bound(L))
+    pool = _text_pool(16 << 20, SEED + rank)
+    raw = eng.alloc_pinned(nb * L)
+    cmp_ = eng.alloc_pinned(nb * bound)
+    out = eng.alloc_pinned(nb * L)
+    rawv = np.ctypeslib.as_array((ctypes.c_uint8 * (nb * L)).from_address(raw))
+    for b in range(nb):
+        o = ((rank * nb + b) * 2654435761) % (pool.size - L)
+        rawv[b * L:(b + 1) * L] = pool[o:o + L]
+    carr, _ = eng.make_zblocks((raw + b * L, L, cmp_ + b * bound, bound) for b in range(nb))
+    if codec in ("lz4", "unlz4"):
+        eng.lz4_compress_batch(carr, nb, E.MEM_HOST)
+    else:
+        eng.zstd_compress_batch(carr, nb, E.MEM_HOST)
+    clens = [carr[b].out_len for b in range(nb)]
+    if comp:
+        arr, _ = eng.make_zblocks((raw + b * L, L, cmp_ + b * bound, bound) for b in range(nb))
+    else:
+        arr, _ = eng.make_zblocks((cmp_ + b * bound, clens[b], out + b * L, L) for b in range(nb))
+    batch_fn = {"lz4": eng.L.jfsx_lz4_compress_batch, "unlz4": eng.L.jfsx_lz4_decompress_batch,
+                "zstd": eng.L.jfsx_zstd_compress_batch, "unzstd": eng.L.jfsx_zstd_decompress_batch}[codec]
+    T = args.threads
+
+    def run(call, steps):
+        errs = []
+
+        def worker(t):
+            try:
+                for _ in range(steps):
+                    for b in range(t, nb, T):
+                        call(b)
+            except BaseException as e:  # noqa: B902 -- reported below
+                errs.append(e)
+        ts = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+        t0 = time.perf_counter()
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        if errs:
+            raise errs[0]
+        return time.perf_counter() - t0
+
+    def direct(b):
+        eng._check(batch_fn(eng.ctx, 1, ctypes.byref(arr[b]), E.MEM_HOST), "one-block " + codec)
+    batch_fn(eng.ctx, nb, arr, E.MEM_HOST)  # warm the workspace
+    t0 = time.perf_counter()
+    eng._check(batch_fn(eng.ctx, nb, arr, E.MEM_HOST), codec + " batch")
+    batch_s = time.perf_counter() - t0
+    d_el = run(direct, 1)
+    with E.Aggregator(eng, window_us=args.agg_window_us) as agg:
+        f = {"lz4": agg.lz4_compress, "unlz4": agg.lz4_decompress, "zstd": agg.zstd_compress,
+             "unzstd": agg.zstd_decompress}[codec]
+        run(lambda b: f(arr[b]), args.warmup)
+        c0, b0, k0 = agg.stats()
+        barrier(dist)
+        el = max_over_ranks(dist, run(lambda b: f(arr[b]), args.steps), local)
+        c1, b1, k1 = agg.stats()
+    # every call's result: compressed bytes equal to the library's, or the block back
+    verified = 0
+    for b in range(0, nb, max(1, nb // max(args.verify, 1)))[:max(args.verify, 1)]:
+        src_b = rawv[b * L:(b + 1) * L].tobytes()
+        if arr[b].status != E.OK:
+            raise SystemExit("bench: block %d status %d" % (b, arr[b].status))
+        if comp:
+            got = np.ctypeslib.as_array((ctypes.c_uint8 * arr[b].out_len).from_address(cmp_ + b * bound)).tobytes()
+            if codec == "zstd" and got != zstd_lib.compress_simple(src_b, 1):
+                raise SystemExit("bench: block %d differs from libzstd level 1" % b)
+            if codec == "lz4":
+                from oracle import oracle as orc
+                if got != orc.lz4_compress(src_b):
+                    raise SystemExit("bench: block %d differs from the LZ4 library" % b)
+        else:
+            got = np.ctypeslib.as_array((ctypes.c_uint8 * L).from_address(out + b * L)).tobytes()
+            if got != src_b:
+                raise SystemExit("bench: block %d does not decode" % b)
+        verified += 1
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sample = [rawv[b * L:(b + 1) * L].tobytes() for b in range(min(nb, 64))]
+        if codec in ("lz4", "unlz4"):
+            cpu = lz4_cpu_baseline(sample, L, decompress=codec == "unlz4")
+        elif codec == "zstd":
+            cpu = zstdc_cpu_baseline(sample, L)
+        else:
+            cpu = zstd_cpu_baseline([zstd_lib.compress_simple(x, 1) for x in sample], L)
+    value = world * nb * L * args.steps / el / 1e9
+    if rank == 0:
+        print(json.dumps({
+            "metric": "per-call %s GB/s (uncompressed bytes), %d threads, 4 MiB host blocks (aggregator)" % (codec, T),
+            "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic (zipf word text), pinned host memory",
+            "config": {"workload": "%d one-block %s calls per step from %d threads, JFSX_MEM_HOST" % (nb, codec, T),
+                       "blocks_per_gpu": nb, "block_bytes": L, "mode": "aggcodec", "codec": codec,
+                       "window_us": args.agg_window_us, "ratio": round(sum(clens) / (nb * L), 4)},
+            "aggregator": {"calls": c1 - c0, "batches": b1 - b0,
+                           "mean_batch_blocks": round((k1 - k0) / max(b1 - b0, 1), 2)},
+            "batch_%d_blocks_GBs" % nb: round(nb * L / batch_s / 1e9, 3),
+            "direct_one_block_calls_GBs": round(nb * L / d_el / 1e9, 3),
+            "roofline": None, "cpu_baseline": cpu, "verified_blocks": verified}), flush=True)
+    for h in (raw, cmp_, out):
         eng.free_pinned(h)
     eng.close()
     if dist is not None:
@@ -749,8 +911,10 @@ def lz4_bench(args, world, rank, local, dist, eng):
             "roofline": {"bound": "hbm", "achieved": round(algo_bytes / (k_avg / 1e3) / 1e9, 1) if k_n else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(algo_bytes / (k_avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if k_n else None,
-                         "traffic": None, "kernel": "lz4_compress_k" if args.mode == "lz4" else "lz4_decompress_k",
-                         "kernel_avg_ms": round(k_avg, 3), "algorithmic_bytes_per_launch": algo_bytes},
+                         "traffic": pmc_traffic(args, nb * L)[0], "traffic_source": pmc_traffic(args, nb * L)[1],
+                         "kernel": "lz4_compress_k" if args.mode == "lz4" else "lz4_decompress_k",
+                         "kernel_avg_ms": round(k_avg, 3), "algorithmic_bytes_per_launch": algo_bytes,
+                         "plain_bytes_per_launch": nb * L},
             "cpu_baseline": cpu, "verified_blocks": verified}), flush=True)
     eng.close()
     if dist is not None:
@@ -855,8 +1019,9 @@ def zstd_bench(args, world, rank, local, dist, eng):
             "roofline": {"bound": "hbm", "achieved": round(algo_bytes / (k_avg / 1e3) / 1e9, 1) if k_n else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(algo_bytes / (k_avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if k_n else None,
-                         "traffic": None, "kernel": "zstd_decompress_k", "kernel_avg_ms": round(k_avg, 3),
-                         "algorithmic_bytes_per_launch": algo_bytes},
+                         "traffic": pmc_traffic(args, nb * L)[0], "traffic_source": pmc_traffic(args, nb * L)[1],
+                         "kernel": "zstd_decompress_k", "kernel_avg_ms": round(k_avg, 3),
+                         "algorithmic_bytes_per_launch": algo_bytes, "plain_bytes_per_launch": nb * L},
             "cpu_baseline": cpu, "verified_blocks": verified}), flush=True)
     eng.close()
     if dist is not None:
@@ -957,8 +1122,9 @@ def zstdc_bench(args, world, rank, local, dist, eng):
             "roofline": {"bound": "hbm", "achieved": round(algo_bytes / (k_avg / 1e3) / 1e9, 1) if k_n else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(algo_bytes / (k_avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if k_n else None,
-                         "traffic": None, "kernel": "zstd_compress_k", "kernel_avg_ms": round(k_avg, 3),
-                         "algorithmic_bytes_per_launch": algo_bytes},
+                         "traffic": pmc_traffic(args, nb * L)[0], "traffic_source": pmc_traffic(args, nb * L)[1],
+                         "kernel": "zstd_compress_k", "kernel_avg_ms": round(k_avg, 3),
+                         "algorithmic_bytes_per_launch": algo_bytes, "plain_bytes_per_launch": nb * L},
             "cpu_baseline": cpu, "verified_blocks": verified}), flush=True)
     eng.close()
     if dist is not None:

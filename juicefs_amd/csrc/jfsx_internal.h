@@ -300,7 +300,7 @@ void launch_zstd_decompress(hipStream_t s, int n, const ZDev *blks, ZOut *outs, 
 // Zstandard level-1 compression (jfsx_zstdc.hip): `waves` persistent
 // one-wave workgroups take objects from *queue (4 device bytes, zeroed on s);
 // each owns kZstdcScratch bytes of scratch (hash table, sequences, literals)
-constexpr size_t kZstdcScratch = 768 * 1024;
+constexpr size_t kZstdcScratch = 960 * 1024;
 constexpr size_t kZcScratchStride = kZstdcScratch;
 constexpr int kZcWavesPerCu = 8;
 void launch_zstd_compress(hipStream_t s, int n, int waves, const ZDev *blks, ZOut *outs, uint8_t *scratch,

@@ -37,7 +37,9 @@ constexpr size_t kZcHtab = (size_t)4 << jzc::kHashLogMax;             // 128 KiB
 constexpr size_t kZcSeq = (size_t)jzc::kMaxSeq * sizeof(jzc::SeqDef);  // 256 KiB
 constexpr size_t kZcLit = (size_t)jzc::kBlockMax + 256;                // literals
 constexpr size_t kZcCodes = (size_t)3 * jzc::kMaxSeq;                  // ll / ml / of codes
-static_assert(kZcHtab + kZcSeq + kZcLit + kZcCodes + jzc::kBodyCap <= kZstdcScratch, "zstd compress scratch");
+constexpr size_t kZcBody = (size_t)jzc::kBodyCap;                      // one block body
+constexpr size_t kZcRec = (size_t)6 * jzc::kMaxSeq;                    // FSE state-chain outputs (3 x u16)
+static_assert(kZcHtab + kZcSeq + kZcLit + kZcCodes + kZcBody + kZcRec <= kZstdcScratch, "zstd compress scratch");
 
 typedef __attribute__((address_space(1))) const uint32_t gcu32z;
 typedef __attribute__((address_space(1))) const uint8_t gcu8c;
@@ -331,10 +333,392 @@ __device__ __noinline__ uint32_t frame_header_lane(uint8_t *dst, uint64_t n, jzc
     return jzc::write_frame_header(dst, n, P);
 }
 
+// ---------------------------------------------------------------------------
+// The entropy stage on the wave.  Table building (Huffman tree, FSE
+// normalisation and spreads: a few hundred entries) stays on lane 0 with the
+// library's serial code; the per-symbol work is spread over the lanes:
+// histograms (LDS atomics), the sequence codes, the Huffman streams and the
+// sequence bit stream.  A bit stream is the concatenation, in emission order,
+// of fixed bit strings, so each lane emits its own run of symbols at an
+// offset from a suffix scan of the runs' lengths, OR-ing 32-bit words into a
+// zeroed destination.
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(1))) uint16_t gu16c;
+
+// exclusive suffix sum within groups of w lanes: sum of x over the group's
+// higher lanes
+__device__ __forceinline__ uint32_t suffix_excl(uint32_t x, uint32_t lane, uint32_t w) {
+    uint32_t v = x;
+    for (uint32_t d = 1; d < w; d <<= 1) {
+        const uint32_t y = __shfl_down(v, d, (int)w);
+        if ((lane % w) + d < w) v += y;
+    }
+    return v - x;
+}
+
+// OR the low nb bits of v into the bit stream at bit q (words of base)
+__device__ __forceinline__ void or_bits(uint32_t *base, uint64_t q, uint64_t v, uint32_t nb) {
+    if (!nb) return;
+    v &= nb >= 64 ? ~0ull : ((1ull << nb) - 1);
+    const uint32_t sh = (uint32_t)(q & 31);
+    uint32_t *w = base + (q >> 5);
+    const uint64_t lo = v << sh;
+    atomicOr(w, (uint32_t)lo);
+    if (sh + nb > 32) atomicOr(w + 1, (uint32_t)(lo >> 32));
+    if (sh + nb > 64) atomicOr(w + 2, (uint32_t)(v >> (64 - sh)));
+}
+
+// zero exactly the bytes [a, b) of the word-aligned body (the bytes around
+// belong to headers already written)
+__device__ __forceinline__ void zero_range(uint8_t *body, uint32_t a, uint32_t b, uint32_t lane) {
+    const uint32_t wa = min((a + 3) & ~3u, b), wb = max(b & ~3u, wa);
+    if (lane < wa - a) *(gu8c *)(body + a + lane) = 0;
+    if (lane < b - wb) *(gu8c *)(body + wb + lane) = 0;
+    for (uint32_t i = wa + 4 * lane; i < wb; i += 256) *(gu32c *)(body + i) = 0;
+}
+
+__device__ __forceinline__ void wave_sync() { __syncthreads(); }
+
+// HUF_compress_internal without the encoding: 0 not compressible, 1 RLE,
+// 2 encode with the old table (W->next.ct), 3 encode with the new table
+// (header of *hSize bytes written at hdr; W->next.ct = the new table)
+__device__ __noinline__ uint32_t huf_plan_lane(jzc::Work *W, uint8_t *hdr, uint64_t cap, uint32_t n, uint32_t maxSym,
+                                               uint32_t largest, bool preferRepeat, uint32_t *hSizeOut,
+                                               uint32_t *repeatOut) {
+    uint32_t repeat = W->prev.repeat;
+    *repeatOut = repeat;
+    *hSizeOut = 0;
+    if (preferRepeat && repeat == jzc::kHufValid) return 2;
+    if (largest == n) return 1;
+    if (largest <= (n >> 7) + 4) return 0;
+    if (repeat == jzc::kHufCheck) {
+        bool bad = false;
+        for (uint32_t s = 0; s <= maxSym; s++) bad |= (W->litCount[s] != 0) & (W->next.ct.nb[s] == 0);
+        if (bad) repeat = jzc::kHufNone;
+    }
+    *repeatOut = repeat;
+    if (preferRepeat && repeat != jzc::kHufNone) return 2;
+    uint32_t huffLog = jzc::fse_optimal_table_log(jzc::kHufLogDefault, n, maxSym, 1);
+    huffLog = jzc::huf_build_ctable(W->hufScratch, W->litCount, maxSym, huffLog, W->hw);
+    const uint64_t hSize = jzc::huf_write_ctable(hdr, cap, W->hufScratch, maxSym, huffLog, W->hw);
+    if (hSize == 0) return 0;
+    if (repeat != jzc::kHufNone) {
+        uint64_t oldBits = 0, newBits = 0;
+        for (uint32_t s = 0; s <= maxSym; s++) {
+            oldBits += (uint64_t)W->next.ct.nb[s] * W->litCount[s];
+            newBits += (uint64_t)W->hufScratch.nb[s] * W->litCount[s];
+        }
+        if ((oldBits >> 3) <= hSize + (newBits >> 3) || hSize + 12 >= n) return 2;
+    }
+    if (hSize + 12 >= n) return 0;
+    *repeatOut = jzc::kHufNone;
+    W->next.ct = W->hufScratch;
+    *hSizeOut = (uint32_t)hSize;
+    return 3;
+}
+
+// The Huffman streams of n literals (HUF_compress1X / 4X_usingCTable):
+// returns their size in bytes (4X: with the 6-byte jump table), or 0 when
+// they would not fit in cap.  out is byte offset `o` of the word-aligned body.
+__device__ uint32_t huf_streams_wave(uint8_t *body, uint32_t o, uint32_t cap, const uint8_t *lit, uint32_t n, bool single,
+                                     const jzc::HufCT &ct, uint32_t lane) {
+    __shared__ uint32_t sz[4];
+    const uint32_t w = single ? 64 : 16;  // lanes per stream
+    const uint32_t s = lane / w, j = lane % w;
+    const uint32_t seg = single ? n : (n + 3) / 4;
+    const uint32_t s0 = s * seg, slen = single ? n : (s < 3 ? seg : n - 3 * seg);
+    const uint32_t per = (slen + w - 1) / w;
+    const uint32_t c0 = min(j * per, slen), c1 = min(c0 + per, slen);
+    uint32_t bits = 0;
+    for (uint32_t i = c0; i < c1; i++) bits += ct.nb[ld8(lit + s0 + i)];
+    const uint32_t before = suffix_excl(bits, lane, w);  // symbols after this run come first
+    const uint32_t total = __shfl(before + bits, (int)(s * w), 64);  // the stream's bits (group lane 0)
+    if (j == 0) sz[s] = (total + 1 + 7) >> 3;  // with the end mark
+    wave_sync();
+    const uint32_t nstreams = single ? 1 : 4;
+    uint32_t start = o + (single ? 0 : 6), end = start;
+    uint32_t my0 = start;
+    for (uint32_t k = 0; k < nstreams; k++) {
+        if (k == s) my0 = end;
+        end += sz[k];
+    }
+    my0 = single ? start : my0;
+    if (end + 16 > cap) return 0;  // the library's bit streams would overflow their buffers
+    zero_range(body, start, end, lane);
+    wave_sync();
+    // this lane's run, last symbol first, from bit `before` of its stream
+    uint64_t q = 8ull * my0 + before;
+    for (int32_t i = (int32_t)c1 - 1; i >= (int32_t)c0; i--) {
+        const uint32_t b = ld8(lit + s0 + i);
+        or_bits((uint32_t *)body, q, ct.val[b], ct.nb[b]);
+        q += ct.nb[b];
+    }
+    if (j == 0) or_bits((uint32_t *)body, 8ull * my0 + total, 1, 1);  // end mark
+    if (!single && lane == 0) {
+        jzc::wr16(body + o, sz[0]);
+        jzc::wr16(body + o + 2, sz[1]);
+        jzc::wr16(body + o + 4, sz[2]);
+    }
+    wave_sync();
+    return end - o;
+}
+
+// literal histogram into W.litCount; returns (maxSym, largest) on every lane
+__device__ void hist_literals(jzc::Work &W, const uint8_t *lit, uint32_t n, uint32_t lane, uint32_t &maxSym,
+                              uint32_t &largest) {
+    for (uint32_t i = lane; i < 256; i += 64) W.litCount[i] = 0;
+    wave_sync();
+    for (uint32_t i = lane; i < n; i += 64) atomicAdd(&W.litCount[ld8(lit + i)], 1u);
+    wave_sync();
+    uint32_t mx = 0, ms = 0;
+    for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t sym = 4 * lane + k, c = W.litCount[sym];
+        if (c > mx) mx = c;
+        if (c) ms = sym;
+    }
+    for (int d = 32; d > 0; d >>= 1) {
+        mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
+        ms = max(ms, (uint32_t)__shfl_xor(ms, d, 64));
+    }
+    maxSym = ms;
+    largest = mx;
+}
+
+__device__ void copy_huf_state(jzc::HufState &d, const jzc::HufState &s, uint32_t lane) {
+    for (uint32_t i = lane; i < 256; i += 64) d.ct.nb[i] = s.ct.nb[i], d.ct.val[i] = s.ct.val[i];
+    if (lane == 0) d.repeat = s.repeat;
+}
+
+// ZSTD_compressLiterals on the wave: the literal section at body[0..),
+// returns its size; W.next as the library leaves nextHuf
+__device__ uint32_t literals_wave(jzc::Work &W, uint8_t *body, const uint8_t *lit, uint32_t n, uint32_t lane) {
+    __shared__ uint32_t bc[3];
+    const uint32_t lhSize = 3 + (n >= 1024) + (n >= 16384);
+    bool single = n < 256;
+    copy_huf_state(W.next, W.prev, lane);
+    const uint32_t fl = 1 + (n > 31) + (n > 4095);
+    uint32_t mode = 0, cLit = 0, hType = jzc::kSetCompressed;
+    wave_sync();
+    if (n > 63) {  // COMPRESS_LITERALS_SIZE_MIN (no table is ever "valid" without a dictionary)
+        uint32_t maxSym, largest;
+        hist_literals(W, lit, n, lane, maxSym, largest);
+        if (lane == 0) {
+            uint32_t hs = 0, rep = 0;
+            bc[0] = huf_plan_lane(&W, body + lhSize, jzc::kBodyCap - lhSize, n, maxSym, largest, n <= 1024, &hs, &rep);
+            bc[1] = hs;
+            bc[2] = rep;
+        }
+        wave_sync();
+        mode = uni(bc[0]);
+        const uint32_t hSize = uni(bc[1]), repeat = uni(bc[2]);
+        if (mode == 1) cLit = 1;
+        if (mode >= 2) {
+            // mode 2: the old table (W.next = prev); mode 3: the new one, now in W.next
+            const uint32_t c = huf_streams_wave(body, lhSize + hSize, jzc::kBodyCap, lit, n, single, W.next.ct, lane);
+            cLit = (c == 0 || hSize + c >= n - 1) ? 0u : hSize + c;
+        }
+        if (repeat != jzc::kHufNone) hType = jzc::kSetRepeat;
+    }
+    if (n <= 63 || cLit == 0 || cLit >= n - jzc::min_gain(n) || cLit == 1) {
+        copy_huf_state(W.next, W.prev, lane);
+        wave_sync();
+        if (n > 63 && cLit == 1) {
+            if (lane == 0) jzc::lit_rle(body, ld8(lit), n);
+            wave_sync();
+            return fl + 1;
+        }
+        if (lane == 0) {
+            if (fl == 1) body[0] = (uint8_t)(jzc::kSetBasic + (n << 3));
+            else if (fl == 2) jzc::wr16(body, jzc::kSetBasic + (1u << 2) + (n << 4));
+            else jzc::wr24(body, jzc::kSetBasic + (3u << 2) + (n << 4));
+        }
+        for (uint32_t i = lane; i < n; i += 64) *(gu8c *)(body + fl + i) = (uint8_t)ld8(lit + i);
+        wave_sync();
+        return fl + n;
+    }
+    if (lane == 0) {
+        if (hType == jzc::kSetCompressed) W.next.repeat = jzc::kHufCheck;
+        const uint32_t c = cLit;
+        if (lhSize == 3) jzc::wr24(body, hType + ((uint32_t)(!single) << 2) + (n << 4) + (c << 14));
+        else if (lhSize == 4) jzc::wr32(body, hType + (2u << 2) + (n << 4) + (c << 18));
+        else {
+            jzc::wr32(body, hType + (3u << 2) + (n << 4) + (c << 22));
+            body[4] = (uint8_t)(c >> 10);
+        }
+    }
+    wave_sync();
+    return lhSize + cLit;
+}
+
+// code histogram of one kind (HIST_countFast): returns (max present, most frequent)
+__device__ void hist_codes_wave(jzc::Work &W, const uint8_t *codes, uint32_t n, uint32_t maxIn, uint32_t lane,
+                                uint32_t &maxSym, uint32_t &mostFreq) {
+    W.sw.count[lane] = 0;
+    wave_sync();
+    for (uint32_t i = lane; i < n; i += 64) atomicAdd(&W.sw.count[ld8(codes + i)], 1u);
+    wave_sync();
+    const uint32_t c = lane <= maxIn ? W.sw.count[lane] : 0u;
+    uint32_t mx = c, ms = c ? lane : 0u;
+    for (int d = 32; d > 0; d >>= 1) {
+        mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
+        ms = max(ms, (uint32_t)__shfl_xor(ms, d, 64));
+    }
+    maxSym = ms;
+    mostFreq = mx;
+}
+
+__device__ __noinline__ uint32_t build_table_lane(jzc::Work *W, uint8_t *op, uint32_t kind, uint32_t type, uint32_t max,
+                                                  const uint8_t *codes, uint32_t nbSeq) {
+    if (kind == 0)
+        return jzc::build_ctable(op, W->sw.ll, jzc::kLLLog, type, W->sw.count, max, codes, nbSeq, jzc::kLLDef, 6,
+                                 jzc::kMaxLL, W->sw);
+    if (kind == 1)
+        return jzc::build_ctable(op, W->sw.of, jzc::kOffLog, type, W->sw.count, max, codes, nbSeq, jzc::kOFDef, 5,
+                                 jzc::kDefaultMaxOff, W->sw);
+    return jzc::build_ctable(op, W->sw.ml, jzc::kMLLog, type, W->sw.count, max, codes, nbSeq, jzc::kMLDef, 6,
+                             jzc::kMaxML, W->sw);
+}
+
+// ZSTD_encodeSequences on the wave.  Lanes 0..2 run the OF / ML / LL state
+// chains (serial by nature) recording each transition's output bits; then
+// every lane emits a run of sequences.  Returns the stream's size, 0 if it
+// would not fit.
+__device__ uint32_t sequences_wave(jzc::Work &W, uint8_t *body, uint32_t o, uint32_t cap, const jzc::SeqDef *seq,
+                                   const uint8_t *llc, const uint8_t *mlc, const uint8_t *ofc, uint16_t *rec,
+                                   uint32_t n, uint32_t lane) {
+    __shared__ uint32_t fin[3];
+    if (lane < 3) {
+        const jzc::FseCT &ct = lane == 0 ? W.sw.of : lane == 1 ? W.sw.ml : W.sw.ll;
+        const uint8_t *cd = lane == 0 ? ofc : lane == 1 ? mlc : llc;
+        gu16c *r = (gu16c *)(rec + (size_t)lane * jzc::kMaxSeq);
+        jzc::FseState st;
+        jzc::fse_init_state2(st, ct, ld8(cd + n - 1));
+        for (int32_t i = (int32_t)n - 2; i >= 0; i--) {
+            const uint32_t c = ld8(cd + i);
+            const uint32_t nb = (st.value + ct.dnb[c]) >> 16;
+            r[i] = (uint16_t)((nb << 12) | (st.value & ((1u << nb) - 1)));
+            st.value = ct.state[(int32_t)(st.value >> nb) + ct.dfs[c]];
+        }
+        fin[lane] = st.value;
+    }
+    wave_sync();
+    // per-sequence bits, runs of sequences per lane (emission: n - 1 first)
+    const uint32_t per = (n + 63) / 64;
+    const uint32_t c0 = min(lane * per, n), c1 = min(c0 + per, n);
+    const gu16c *rOF = (const gu16c *)rec, *rML = rOF + jzc::kMaxSeq, *rLL = rML + jzc::kMaxSeq;
+    uint32_t bits = 0;
+    for (uint32_t i = c0; i < c1; i++) {
+        const uint32_t l = ld8(llc + i), m = ld8(mlc + i), f = ld8(ofc + i);
+        bits += jzc::kLLBits[l] + jzc::kMLBits[m] + f;
+        if (i + 1 < n) bits += (rOF[i] >> 12) + (rML[i] >> 12) + (rLL[i] >> 12);
+    }
+    const uint32_t before = suffix_excl(bits, lane, 64);
+    const uint32_t total = __shfl(before + bits, 0, 64);
+    const uint32_t tl = W.sw.ml.tableLog + W.sw.of.tableLog + W.sw.ll.tableLog;
+    const uint32_t bytes = (total + tl + 1 + 7) >> 3;
+    if (o + bytes + 16 > cap) return 0;
+    zero_range(body, o, o + bytes, lane);
+    wave_sync();
+    uint64_t q = 8ull * o + before;
+    uint32_t *base = (uint32_t *)body;
+    for (int32_t i = (int32_t)c1 - 1; i >= (int32_t)c0; i--) {
+        const uint32_t l = ld8(llc + i), m = ld8(mlc + i), f = ld8(ofc + i);
+        const jzc::SeqDef d = seq[i];
+        if ((uint32_t)i + 1 < n) {
+            const uint32_t a = rOF[i], b = rML[i], c = rLL[i];
+            or_bits(base, q, a & 0xfff, a >> 12);
+            q += a >> 12;
+            or_bits(base, q, b & 0xfff, b >> 12);
+            q += b >> 12;
+            or_bits(base, q, c & 0xfff, c >> 12);
+            q += c >> 12;
+        }
+        or_bits(base, q, d.ll, jzc::kLLBits[l]);
+        q += jzc::kLLBits[l];
+        or_bits(base, q, d.ml, jzc::kMLBits[m]);
+        q += jzc::kMLBits[m];
+        or_bits(base, q, d.offset, f);
+        q += f;
+    }
+    if (lane == 0) {
+        uint64_t e = 8ull * o + total;
+        or_bits(base, e, fin[1], W.sw.ml.tableLog);
+        e += W.sw.ml.tableLog;
+        or_bits(base, e, fin[0], W.sw.of.tableLog);
+        e += W.sw.of.tableLog;
+        or_bits(base, e, fin[2], W.sw.ll.tableLog);
+        e += W.sw.ll.tableLog;
+        or_bits(base, e, 1, 1);  // end mark
+    }
+    wave_sync();
+    return bytes;
+}
+
+// ZSTD_entropyCompressSequences on the wave: the block body in body[0..),
+// 0 when the block is stored raw
+__device__ uint64_t block_body_wave(jzc::Work &W, const WSeq &ss, uint8_t *codes, uint16_t *rec, uint8_t *body,
+                                    uint32_t bs, uint32_t lane) {
+    __shared__ uint32_t bc[2];
+    uint32_t op = literals_wave(W, body, ss.lit, ss.nlit, lane);
+    const uint32_t nbSeq = ss.nseq;
+    if (lane == 0) {
+        if (nbSeq < 128) {
+            body[op] = (uint8_t)nbSeq;
+        } else if (nbSeq < jzc::kLongNbSeq) {
+            body[op] = (uint8_t)((nbSeq >> 8) + 0x80);
+            body[op + 1] = (uint8_t)nbSeq;
+        } else {
+            body[op] = 0xFF;
+            jzc::wr16(body + op + 1, nbSeq - jzc::kLongNbSeq);
+        }
+    }
+    op += nbSeq < 128 ? 1 : nbSeq < jzc::kLongNbSeq ? 2 : 3;
+    if (nbSeq != 0) {
+        uint8_t *llc = codes, *mlc = codes + jzc::kMaxSeq, *ofc = codes + 2 * jzc::kMaxSeq;
+        for (uint32_t i = lane; i < nbSeq; i += 64) {
+            const jzc::SeqDef d = ss.seq[i];
+            *(gu8c *)(llc + i) = (uint8_t)jzc::ll_code(d.ll);
+            *(gu8c *)(ofc + i) = (uint8_t)jzc::highbit32(d.offset);
+            *(gu8c *)(mlc + i) = (uint8_t)jzc::ml_code(d.ml);
+        }
+        wave_sync();
+        if (lane == 0) {
+            if (ss.long_id == 1) llc[ss.long_pos] = jzc::kMaxLL;
+            if (ss.long_id == 2) mlc[ss.long_pos] = jzc::kMaxML;
+        }
+        wave_sync();
+        const uint32_t seqHead = op++;
+        int32_t lastNCount = -1;
+        uint32_t types[3];
+        const uint8_t *cds[3] = {llc, ofc, mlc};
+        const uint32_t maxIn[3] = {jzc::kMaxLL, jzc::kMaxOff, jzc::kMaxML};
+        for (uint32_t k = 0; k < 3; k++) {
+            uint32_t max, mf;
+            hist_codes_wave(W, cds[k], nbSeq, maxIn[k], lane, max, mf);
+            const uint32_t type = k == 1 ? jzc::select_type(mf, nbSeq, 5, max <= jzc::kDefaultMaxOff)
+                                         : jzc::select_type(mf, nbSeq, 6, true);
+            if (lane == 0) bc[0] = build_table_lane(&W, body + op, k, type, max, cds[k], nbSeq);
+            wave_sync();
+            const uint32_t t = uni(bc[0]);
+            if (type == jzc::kSetCompressed) lastNCount = (int32_t)op;
+            op += t;
+            types[k] = type;
+        }
+        if (lane == 0) body[seqHead] = (uint8_t)((types[0] << 6) + (types[1] << 4) + (types[2] << 2));
+        if (op + 16 >= jzc::kBodyCap) return 0;
+        const uint32_t b = sequences_wave(W, body, op, jzc::kBodyCap, ss.seq, llc, mlc, ofc, rec, nbSeq, lane);
+        if (b == 0) return 0;
+        op += b;
+        if (lastNCount >= 0 && (int32_t)op - lastNCount < 4) return 0;
+    }
+    if (op >= bs - jzc::min_gain(bs)) return 0;
+    return op;
+}
+
 // ZSTD_compress(level 1) of one object by the wave
 __device__ uint64_t compress_object(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *htab,
-                                    jzc::SeqDef *seqs, uint8_t *lits, uint8_t *codes, uint8_t *body, jzc::Work &W,
-                                    uint32_t lane) {
+                                    jzc::SeqDef *seqs, uint8_t *lits, uint8_t *codes, uint8_t *body, uint16_t *rec,
+                                    jzc::Work &W, uint32_t lane) {
     const jzc::Params P = jzc::level1_params(n);
     __shared__ uint32_t bcast;
     if (lane == 0) bcast = frame_header_lane(dst, n, P);
@@ -364,12 +748,17 @@ __device__ uint64_t compress_object(const uint8_t *src, uint64_t n, uint8_t *dst
             for (uint32_t o = lane; o < lastLL; o += 64)
                 *(gu8c *)(lits + ss.nlit + o) = (uint8_t)ld8(src + pos + bs - lastLL + o);
             ss.nlit += lastLL;
-            __syncthreads();  // sequences and literals visible to lane 0
+            __syncthreads();  // sequences and literals visible to every lane
+#ifdef JFSX_ZC_LANE0_ENTROPY
             if (lane == 0)
                 bcast = (uint32_t)block_body_lane(&W, seqs, lits, codes, ss.nseq, ss.nlit, ss.long_id, ss.long_pos,
                                                   body, bs);
             __syncthreads();
             cSize = uni(bcast);
+#else
+            cSize = block_body_wave(W, ss, codes, rec, body, bs, lane);
+            __syncthreads();
+#endif
             if (!first && cSize < jzc::kRleMaxLength) {
                 const uint32_t b0 = ld8(ip);
                 bool diff = false;
@@ -419,6 +808,7 @@ __global__ __launch_bounds__(64) void zstd_compress_k(const ZDev *__restrict__ b
     uint8_t *const lits = sc + kZcHtab + kZcSeq;
     uint8_t *const codes = lits + kZcLit;
     uint8_t *const body = codes + kZcCodes;
+    uint16_t *const rec = (uint16_t *)(body + kZcBody);
     for (;;) {
         if (lane == 0) next = (int)atomicAdd(queue, 1u);
         __syncthreads();
@@ -432,7 +822,7 @@ __global__ __launch_bounds__(64) void zstd_compress_k(const ZDev *__restrict__ b
             outs[obj].status = JFSX_OK;
         }
 #else
-        const uint64_t r = compress_object(b.src, b.len, b.dst, htab, seqs, lits, codes, body, W, lane);
+        const uint64_t r = compress_object(b.src, b.len, b.dst, htab, seqs, lits, codes, body, rec, W, lane);
         if (lane == 0) {
             outs[obj].out_len = r;
             outs[obj].status = JFSX_OK;

@@ -12,9 +12,13 @@
  *                               CRCs; and jfsx_cache_verify for the level logic
  *   §5 LZ4.Compress/Decompress (cachedStore.upload / load) -> jfsx_agg_lz4_*
  *                               from many threads, zblk descriptors in C memory
+ *      jfsxLZ4 / jfsxZstd run() with its empty-slice guards and stock
+ *                               fallbacks, through the reference's own
+ *                               testCompress (compress_test.go:25-76)
  *
  * Built in-tree by tests/harness/Makefile (from __graft_entry__.build());
  * run by tests/test_shim_sequence.py on the GPU box.  Exit 0 = all equal. */
+#include <dlfcn.h>
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -254,6 +258,103 @@ static void lz4_stage(jfsx_ctx *ctx) {
     CHECK(jfsx_agg_free(agg) == 0);
 }
 
+/* §5 jfsxEngine.run, as the Go shim makes it: descriptor and both buffers in
+ * C memory (malloc(len + 1): never malloc(0)), the source copied in only when
+ * non-empty, the output copied out only when status is OK and out_len > 0.
+ * Returns 1 and sets *n / *st, or 0 when the engine failed as a whole. */
+enum { OP_LZ4C, OP_LZ4D, OP_ZSTDC, OP_ZSTDD };
+static int shim_run(jfsx_agg *agg, int op, uint8_t *dst, size_t dlen, const uint8_t *src, size_t slen, int *n,
+                    int *st) {
+    jfsx_zblk *z = (jfsx_zblk *)calloc(1, sizeof(jfsx_zblk));
+    void *in = malloc(slen + 1), *out = malloc(dlen + 1);
+    if (slen > 0) memcpy(in, src, slen);
+    z->src = in, z->src_len = slen, z->dst = out, z->dst_cap = dlen;
+    int rc = op == OP_LZ4C ? jfsx_agg_lz4_compress(agg, z, JFSX_MEM_HOST)
+             : op == OP_LZ4D ? jfsx_agg_lz4_decompress(agg, z, JFSX_MEM_HOST)
+             : op == OP_ZSTDC ? jfsx_agg_zstd_compress(agg, z, JFSX_MEM_HOST)
+                              : jfsx_agg_zstd_decompress(agg, z, JFSX_MEM_HOST);
+    int ok = rc == 0;
+    if (ok) {
+        *n = (int)z->out_len;
+        *st = z->status;
+        if (z->status == JFSX_OK && z->out_len > 0) memcpy(dst, out, z->out_len);
+    }
+    free(in), free(out), free(z);
+    return ok;
+}
+
+/* the stock cgo codecs the shim falls back to: go-lz4 (the oracle's LZ4
+ * restatement, pinned to liblz4) and DataDog/zstd (the system libzstd) */
+static size_t (*zs_compress)(void *, size_t, const void *, size_t, int);
+static size_t (*zs_decompress)(void *, size_t, const void *, size_t);
+static size_t (*zs_bound)(size_t);
+static unsigned (*zs_iserr)(size_t);
+static void load_zstd(void) {
+    void *h = dlopen("libzstd.so.1", RTLD_NOW);
+    CHECK(h);
+    zs_compress = (size_t(*)(void *, size_t, const void *, size_t, int))dlsym(h, "ZSTD_compress");
+    zs_decompress = (size_t(*)(void *, size_t, const void *, size_t))dlsym(h, "ZSTD_decompress");
+    zs_bound = (size_t(*)(size_t))dlsym(h, "ZSTD_compressBound");
+    zs_iserr = (unsigned (*)(size_t))dlsym(h, "ZSTD_isError");
+    CHECK(zs_compress && zs_decompress && zs_bound && zs_iserr);
+}
+/* Compressor results: 0 ok (n set), -1 error */
+static int stock(int op, uint8_t *dst, size_t dlen, const uint8_t *src, size_t slen, int *n) {
+    if (op == OP_LZ4C) {
+        int r = orc_lz4_compress(src, (int)slen, dst, (int)dlen);
+        return r > 0 ? (*n = r, 0) : -1;
+    }
+    if (op == OP_LZ4D) {
+        int r = orc_lz4_decompress(src, (int)slen, dst, (int)dlen);
+        return r >= 0 ? (*n = r, 0) : -1;
+    }
+    if (op == OP_ZSTDC) {  /* CompressLevel: a new buffer below the bound -> "buffer too short" */
+        if (dlen < zs_bound(slen)) return -1;
+        size_t r = zs_compress(dst, dlen, src, slen, 1);
+        return zs_iserr(r) ? -1 : (*n = (int)r, 0);
+    }
+    if (slen == 0) return -1; /* ErrEmptySlice */
+    size_t r = zs_decompress(dst, dlen, src, slen); /* too small: a larger buffer, "buffer too short" */
+    return zs_iserr(r) ? -1 : (*n = (int)r, 0);
+}
+/* jfsxLZ4 / jfsxZstd Compress and Decompress */
+static int shim_codec(jfsx_agg *agg, int op, uint8_t *dst, size_t dlen, const uint8_t *src, size_t slen, int *n) {
+    int st = 0;
+    if (op == OP_LZ4C && dlen < jfsx_lz4_bound(slen)) return stock(op, dst, dlen, src, slen, n);
+    if (op == OP_ZSTDC && dlen < jfsx_zstd_bound(slen)) return stock(op, dst, dlen, src, slen, n);
+    if (op == OP_LZ4D && slen == 0) return -1; /* "decompress an empty input" */
+    if (op == OP_ZSTDD && slen == 0) return stock(op, dst, dlen, src, slen, n);
+    if (shim_run(agg, op, dst, dlen, src, slen, n, &st) && st == JFSX_OK) return 0;
+    return stock(op, dst, dlen, src, slen, n);
+}
+
+/* compress_test.go:25-76, testCompress(t, c), for c = lz4 and zstd */
+static void compress_contract(jfsx_agg *agg, int comp, int decomp, const char *name) {
+    for (int pass = 0; pass < 2; pass++) {
+        const uint8_t *src = pass == 0 ? (const uint8_t *)name : NULL;
+        const size_t slen = pass == 0 ? strlen(name) : 0; /* testIt(src), testIt(nil) */
+        uint8_t one[1];
+        int n = 0, m = 0;
+        if (slen > 1) CHECK(shim_codec(agg, comp, one, 1, src, slen, &n) != 0); /* short buffer error */
+        const size_t bound = comp == OP_LZ4C ? jfsx_lz4_bound(slen) : jfsx_zstd_bound(slen);
+        uint8_t *dst = (uint8_t *)malloc(bound + 1);
+        CHECK(shim_codec(agg, comp, dst, bound, src, slen, &n) == 0);
+        /* the engine's bytes are the stock codec's */
+        uint8_t *ref = (uint8_t *)malloc(bound + 1);
+        int rn = 0;
+        CHECK(stock(comp, ref, bound, src, slen, &rn) == 0 && rn == n && memcmp(ref, dst, (size_t)n) == 0);
+        if (slen > 1) CHECK(shim_codec(agg, decomp, one, 1, dst, (size_t)n, &m) != 0);
+        uint8_t *src2 = (uint8_t *)malloc(slen + 1);
+        CHECK(shim_codec(agg, decomp, src2, slen, dst, (size_t)n, &m) == 0);
+        CHECK((size_t)m == slen && (slen == 0 || memcmp(src2, src, slen) == 0));
+        free(dst), free(ref), free(src2);
+    }
+    /* CompressBound(0) > 0 for both: an empty input does not decompress */
+    uint8_t buf[100];
+    int m = 0;
+    CHECK(shim_codec(agg, decomp, buf, sizeof(buf), (const uint8_t *)"", 0, &m) != 0);
+}
+
 int main(void) {
     CHECK(jfsx_abi_version() == JFSX_ABI_VERSION);
     int nd = 0;
@@ -269,6 +370,14 @@ int main(void) {
     }
     cache_checksums(ctx);
     lz4_stage(ctx);
+    {
+        jfsx_agg *agg = NULL;
+        load_zstd();
+        CHECK(jfsx_agg_new_mctx(m, 0, 0, 200, &agg) == 0);
+        compress_contract(agg, OP_LZ4C, OP_LZ4D, "LZ4");
+        compress_contract(agg, OP_ZSTDC, OP_ZSTDD, "Zstd");
+        CHECK(jfsx_agg_free(agg) == 0);
+    }
     CHECK(jfsx_mctx_close(m) == 0);
     CHECK(jfsx_ctx_close(ctx) == 0);
     printf("shim sequence ok (%d device%s)\n", nd, nd == 1 ? "" : "s");
