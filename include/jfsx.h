@@ -378,7 +378,7 @@ void jfsx_gen_key(uint64_t seed, uint64_t block, uint8_t key[32], uint8_t nonce[
 
 /* diagnostics: the lookup tables the kernels stage into LDS, built on the host
  * without a device (AES T0|T2 x32 replicated: 16384 dwords; CRC32C slice-by-16
- * and 1008/4032/1024-byte shift tables: 7168 dwords; CRC lane/power constants: 192) */
+ * and 1008/4032/1024/4096-byte shift tables: 8192 dwords; CRC lane/power constants: 192) */
 int jfsx_debug_tables(uint32_t *aes, uint32_t *crc, uint32_t *crcx);
 
 #ifdef __cplusplus

@@ -130,20 +130,22 @@ void make_crc_tables(std::vector<uint32_t> &crc, std::vector<uint32_t> &crcx) {
             if (n & 1) r = crc_mulmod_h(x8[k], r);
         return r;
     };
-    crc.assign(28 * 256, 0);
+    crc.assign(32 * 256, 0);
     for (int j = 0; j < 16; j++) {
         const uint32_t xp = xpow8(15 - j);
         for (int b = 0; b < 256; b++) crc[j * 256 + b] = crc_mulmod_h(xp, T[b]);
     }
     // S tables: shift a lane CRC across the gap to its next piece -- 1008 B for
     // 16-B pieces at 1 KiB row stride (GCM), 4032 B for 64-B chunks at 4 KiB (ChaCha)
-    // (and 1024 B: a whole row, for the CRC-only kernel's A' = S(A) ^ U(piece))
-    const uint32_t x1008 = xpow8(1008), x4032 = xpow8(4032), x1024 = xpow8(1024);
+    // (and 1024 B / 4096 B: a whole row / a whole 4 KiB span of 64-B lane chunks,
+    // for the CRC-only kernel's A' = S(A) ^ crc_raw(0, chunk))
+    const uint32_t x1008 = xpow8(1008), x4032 = xpow8(4032), x1024 = xpow8(1024), x4096 = xpow8(4096);
     for (int k = 0; k < 4; k++)
         for (uint32_t v = 0; v < 256; v++) {
             crc[(16 + k) * 256 + v] = crc_mulmod_h(x1008, v << (8 * k));
             crc[(20 + k) * 256 + v] = crc_mulmod_h(x4032, v << (8 * k));
             crc[(24 + k) * 256 + v] = crc_mulmod_h(x1024, v << (8 * k));
+            crc[(28 + k) * 256 + v] = crc_mulmod_h(x4096, v << (8 * k));
         }
     crcx.assign(192, 0);
     for (int l = 0; l < 64; l++) crcx[l] = xpow8(16 * (63 - l));
@@ -174,7 +176,10 @@ struct Workspace {
     const void *dout = nullptr;  // device BlkOut[n] of the batch in flight
 };
 
-constexpr int kRing = 3;  // host-ingest pipeline depth (H2D | transform | D2H)
+#ifndef JFSX_RING
+#define JFSX_RING 3
+#endif
+constexpr int kRing = JFSX_RING;  // host-ingest pipeline depth (H2D | transform | D2H)
 
 }  // namespace
 
@@ -552,7 +557,8 @@ int run_aead_host_ring(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, 
         groups.push_back({b0, n});
     }
     std::vector<jfsx_blk> dv(blks, blks + n);
-    int busy[kRing] = {-1, -1, -1};  // group in flight per slot
+    int busy[kRing];  // group in flight per slot
+    for (int k = 0; k < kRing; k++) busy[k] = -1;
     auto drain = [&](int k) -> int {
         if (busy[k] < 0) return 0;
         HIP_OK(hipEventSynchronize(c->ev_out[k]));
@@ -794,7 +800,7 @@ int run_codec(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, CodecOp op) {
     size_t extra = 0;
     if (op == kLz4Comp) extra = kLz4TabBytes * (size_t)n;
     else if (op == kZstdDecomp) extra = kZstdScratch * (size_t)n;
-    else if (op == kZstdComp) extra = 256 + kZstdcScratch * (size_t)zc_waves;  // queue, then per-wave scratch
+    else if (op == kZstdComp) extra = 256 + kZstdcScratch * (size_t)zc_waves;  // per-wave scratch
     if ((rc = ensure_dev(c, &w.d, &w.dcap, o_tab + extra))) return rc;
     if ((rc = ensure_host(&w.h, &w.hcap, o_tab))) return rc;  // descriptors and results only
     hipStream_t s = c->stream;
@@ -833,7 +839,7 @@ int run_codec(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, CodecOp op) {
         launch_zstd_decompress(s, n, dz, dout, (uint8_t *)(w.d + o_tab));
         break;
     case kZstdComp:
-        launch_zstd_compress(s, n, zc_waves, dz, dout, (uint8_t *)(w.d + o_tab + 256), (uint32_t *)(w.d + o_tab));
+        launch_zstd_compress(s, n, zc_waves, dz, dout, (uint8_t *)(w.d + o_tab + 256));
         break;
     }
     if (c->timing) HIP_OK(hipEventRecord(c->ev_k1[0], s));
@@ -1435,7 +1441,7 @@ void jfsx_gen_key(uint64_t seed, uint64_t b, uint8_t key[32], uint8_t nonce[12])
 
 int jfsx_debug_tables(uint32_t *aes, uint32_t *crc, uint32_t *crcx) {
     std::vector<uint32_t> a, c, x;
-    make_aes_table(a);  // 16384 / 7168 / 192 dwords
+    make_aes_table(a);  // 16384 / 8192 / 192 dwords
     make_crc_tables(c, x);
     if (aes) memcpy(aes, a.data(), 4 * a.size());
     if (crc) memcpy(crc, c.data(), 4 * c.size());

@@ -28,6 +28,17 @@ namespace jfsx {
 // one 1 KiB row, so A' = S1024(A) ^ U(piece) and the 32 data lookups of a row
 // do not wait for A.  Each workgroup stages the tables once per task (0.5 to
 // 4 MiB) and every wave loops over segments.
+// JFSX_CRC_SPAN = 64 (default): in whole segments a lane owns 64 contiguous
+// bytes of every 4 KiB span (lane l: bytes 64l..64l+63), four 16-B pieces
+// chained through the slice-by-16 state (crc ^ first word, no lookups between
+// them), and the lane CRC moves from span to span by one 4096-B shift:
+// A' = S4096(A) ^ crc_raw(0, chunk) -- 34 nibble lookups per 16 B instead of
+// the 40 of the 16-B-per-lane rows (A' = S1024(A) ^ U(piece)).  Tables
+// t = 16..19 in LDS are then the 4096-B shift; the guarded path (ragged
+// segment ends) keeps 1 KiB rows and takes its 1024-B shift from global memory.
+#ifndef JFSX_CRC_SPAN
+#define JFSX_CRC_SPAN 64
+#endif
 constexpr uint32_t kCrcWaves = 16;
 #ifndef JFSX_CRC_PF
 #define JFSX_CRC_PF 4
@@ -57,6 +68,23 @@ __device__ __forceinline__ uint32_t crc_row_nib(const char *lds, uint32_t lb, ui
 }
 #undef X3
 
+// crc_raw(0, 16-byte piece p) through the LDS nibble tables U0..U15
+__device__ __forceinline__ uint32_t crc_u16_nib(const char *lds, uint32_t lb, uint32_t x, uint32_t y, uint32_t z,
+                                                uint32_t w) {
+#define X3(a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), 0x96)
+    return X3(crc_word_nib(lds, lb, 0, x), crc_word_nib(lds, lb, 4, y), crc_word_nib(lds, lb, 8, z)) ^
+           crc_word_nib(lds, lb, 12, w);
+#undef X3
+}
+
+// the guarded path's row step with the 1024-B shift from global byte tables
+__device__ __forceinline__ uint32_t crc_row_g(const char *lds, const uint32_t *__restrict__ T, uint32_t lb, uint32_t A,
+                                              uint4 p) {
+    const uint32_t s = T[24 * 256 + (A & 0xffu)] ^ T[25 * 256 + ((A >> 8) & 0xffu)] ^
+                       T[26 * 256 + ((A >> 16) & 0xffu)] ^ T[27 * 256 + (A >> 24)];
+    return crc_u16_nib(lds, lb, p.x, p.y, p.z, p.w) ^ s;
+}
+
 // ragged tails (segment length not a multiple of 16 B: the last segment of an
 // odd-sized block only) read the byte tables from global memory:
 // crc_raw(shift(A, 1008 B), first n bytes of p)
@@ -79,7 +107,7 @@ __global__ __launch_bounds__(kCrcWaves * 64) __attribute__((amdgpu_waves_per_eu(
     // stage: i = (table t, hi, nibble, replica quad rq)
     for (uint32_t i = tid; i < 640 * 8; i += kCrcWaves * 64) {
         const uint32_t rq = i & 7, nib = (i >> 3) & 15, hi = (i >> 7) & 1, t = i >> 8;
-        const uint32_t v = tab.crc[(t < 16 ? t : t + 8) * 256 + (hi ? nib << 4 : nib)];
+        const uint32_t v = tab.crc[(t < 16 ? t : t + (JFSX_CRC_SPAN == 64 ? 12 : 8)) * 256 + (hi ? nib << 4 : nib)];
         *reinterpret_cast<uint4 *>(lds + t * 4096 + nib * 256 + hi * 128 + 16 * rq) = make_uint4(v, v, v, v);
     }
     __syncthreads();
@@ -90,7 +118,28 @@ __global__ __launch_bounds__(kCrcWaves * 64) __attribute__((amdgpu_waves_per_eu(
         const uint64_t seg1 = seg0 + kSeg < task.c1 ? seg0 + kSeg : task.c1;
         uint32_t A = 0, lend = 0;
         const uint64_t nrows = (seg1 - seg0 + 1023) / 1024;
-        if (seg1 - seg0 == (uint64_t)kSeg) {
+        if (JFSX_CRC_SPAN == 64 && seg1 - seg0 == (uint64_t)kSeg) {
+            // full segment: 8 spans of 4 KiB, lane chunk 64 B; the next span's
+            // four loads are in flight while this one is folded
+            const uint8_t *q = src + seg0 + 64 * lane;
+            uint4 buf[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) buf[j] = gld16(q + 16 * j);
+#pragma unroll
+            for (int r = 0; r < 8; r++) {
+                const uint4 p0 = buf[0], p1 = buf[1], p2 = buf[2], p3 = buf[3];
+                if (r + 1 < 8) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) buf[j] = gld16(q + 4096 * (r + 1) + 16 * j);
+                }
+                uint32_t c = crc_u16_nib(lds, lb, p0.x, p0.y, p0.z, p0.w);
+                c = crc_u16_nib(lds, lb, p1.x ^ c, p1.y, p1.z, p1.w);
+                c = crc_u16_nib(lds, lb, p2.x ^ c, p2.y, p2.z, p2.w);
+                c = crc_u16_nib(lds, lb, p3.x ^ c, p3.y, p3.z, p3.w);
+                A = crc_word_nib(lds, lb, 16, A) ^ c;
+            }
+            lend = kSeg;  // marker: lane chunk ends at 28672 + 64 * lane + 64
+        } else if (JFSX_CRC_SPAN != 64 && seg1 - seg0 == (uint64_t)kSeg) {
             // full segment: 32 rows, kCrcPf loads in flight per wave (HBM
             // latency x 8 TB/s needs ~64 KiB in flight per CU)
             const uint8_t *q = src + seg0 + 16 * lane;
@@ -109,7 +158,7 @@ __global__ __launch_bounds__(kCrcWaves * 64) __attribute__((amdgpu_waves_per_eu(
                 const uint64_t o = seg0 + 1024 * r + 16 * lane;
                 const uint4 p = load_piece(src, o, seg1);
                 if (o + 16 <= seg1) {
-                    A = crc_row_nib(lds, lb, A, p);
+                    A = JFSX_CRC_SPAN == 64 ? crc_row_g(lds, tab.crc, lb, A, p) : crc_row_nib(lds, lb, A, p);
                     lend = (uint32_t)(o + 16 - seg0);
                 } else if (o < seg1) {
                     const uint32_t pw[4] = {p.x, p.y, p.z, p.w};
@@ -121,7 +170,7 @@ __global__ __launch_bounds__(kCrcWaves * 64) __attribute__((amdgpu_waves_per_eu(
         const uint32_t Lseg = (uint32_t)(seg1 - seg0);
         uint32_t v, K;
         if (Lseg == (uint32_t)kSeg) {
-            v = crc_mulmod(tab.crcx[lane], A);
+            v = crc_mulmod(tab.crcx[JFSX_CRC_SPAN == 64 ? 128 + lane : lane], A);
             K = tab.crcx[96];
         } else {
             v = crc_mulmod(crc_xpow8(Lseg - lend, tab.crcx + 64), A);

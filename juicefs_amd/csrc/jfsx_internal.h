@@ -267,7 +267,7 @@ struct JfsxTables;
 namespace jfsx {
 struct DevTables {
     const uint32_t *aes;    // 16384 dwords: T0|T2 replicated x32 per index
-    const uint32_t *crc;    // 28 x 256 dwords: U0..U15 (slice-by-16), shift 1008 B, 4032 B, 1024 B
+    const uint32_t *crc;    // 32 x 256 dwords: U0..U15 (slice-by-16), shift 1008 B, 4032 B, 1024 B, 4096 B
     const uint32_t *crcx;   // 64 lane shift constants, 32 x8pow, K_full
 };
 void launch_gcm_keysetup(hipStream_t s, int n, const KeyIn *keys, const BlkDev *blks, GcmSched *sched,
@@ -298,13 +298,12 @@ constexpr size_t kZstdHufOff = 128 * 1024 + 320;
 constexpr size_t kZstdScratch = kZstdHufOff + 8192;
 void launch_zstd_decompress(hipStream_t s, int n, const ZDev *blks, ZOut *outs, uint8_t *scratch);
 // Zstandard level-1 compression (jfsx_zstdc.hip): `waves` persistent
-// one-wave workgroups take objects from *queue (4 device bytes, zeroed on s);
+// one-wave workgroups take objects w, w + waves, ... (a uniform strided loop);
 // each owns kZstdcScratch bytes of scratch (hash table, sequences, literals)
 constexpr size_t kZstdcScratch = 960 * 1024;
 constexpr size_t kZcScratchStride = kZstdcScratch;
 constexpr int kZcWavesPerCu = 8;
-void launch_zstd_compress(hipStream_t s, int n, int waves, const ZDev *blks, ZOut *outs, uint8_t *scratch,
-                          uint32_t *queue);
+void launch_zstd_compress(hipStream_t s, int n, int waves, const ZDev *blks, ZOut *outs, uint8_t *scratch);
 // batched RSA-OAEP unwrap (jfsx_rsa.hip): key = device jfsx_rsa::Key
 void async_detach(jfsx_ctx *c);  // jfsx_agg.cpp
 void launch_rsa_unwrap(hipStream_t s, const void *key, int n, const uint8_t *ct, uint32_t *mh, uint8_t *em,

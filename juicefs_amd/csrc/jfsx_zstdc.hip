@@ -378,6 +378,19 @@ __device__ __forceinline__ void zero_range(uint8_t *body, uint32_t a, uint32_t b
 }
 
 __device__ __forceinline__ void wave_sync() { __syncthreads(); }
+// diagnostic build (-DJFSX_ZC_TRACE): lane 0 prints each stage of the entropy
+// stage as it is reached (device printf is a hostcall: lines appear while the
+// kernel runs, so a hang shows its last stage)
+#ifdef JFSX_ZC_TRACE
+#define ZT(...)                                    \
+    do {                                           \
+        if (threadIdx.x == 0) printf(__VA_ARGS__); \
+    } while (0)
+#else
+#define ZT(...) \
+    do {        \
+    } while (0)
+#endif
 
 // HUF_compress_internal without the encoding: 0 not compressible, 1 RLE,
 // 2 encode with the old table (W->next.ct), 3 encode with the new table
@@ -587,6 +600,7 @@ __device__ uint32_t sequences_wave(jzc::Work &W, uint8_t *body, uint32_t o, uint
                                    const uint8_t *llc, const uint8_t *mlc, const uint8_t *ofc, uint16_t *rec,
                                    uint32_t n, uint32_t lane) {
     __shared__ uint32_t fin[3];
+    ZT("zc: seq chains n %u\n", n);
     if (lane < 3) {
         const jzc::FseCT &ct = lane == 0 ? W.sw.of : lane == 1 ? W.sw.ml : W.sw.ll;
         const uint8_t *cd = lane == 0 ? ofc : lane == 1 ? mlc : llc;
@@ -612,8 +626,10 @@ __device__ uint32_t sequences_wave(jzc::Work &W, uint8_t *body, uint32_t o, uint
         bits += jzc::kLLBits[l] + jzc::kMLBits[m] + f;
         if (i + 1 < n) bits += (rOF[i] >> 12) + (rML[i] >> 12) + (rLL[i] >> 12);
     }
+    ZT("zc: seq bits\n");
     const uint32_t before = suffix_excl(bits, lane, 64);
     const uint32_t total = __shfl(before + bits, 0, 64);
+    ZT("zc: seq total %u\n", total);
     const uint32_t tl = W.sw.ml.tableLog + W.sw.of.tableLog + W.sw.ll.tableLog;
     const uint32_t bytes = (total + tl + 1 + 7) >> 3;
     if (o + bytes + 16 > cap) return 0;
@@ -659,7 +675,9 @@ __device__ uint32_t sequences_wave(jzc::Work &W, uint8_t *body, uint32_t o, uint
 __device__ uint64_t block_body_wave(jzc::Work &W, const WSeq &ss, uint8_t *codes, uint16_t *rec, uint8_t *body,
                                     uint32_t bs, uint32_t lane) {
     __shared__ uint32_t bc[2];
+    ZT("zc: block body nlit %u nseq %u bs %u\n", ss.nlit, ss.nseq, bs);
     uint32_t op = literals_wave(W, body, ss.lit, ss.nlit, lane);
+    ZT("zc: literals -> %u\n", op);
     const uint32_t nbSeq = ss.nseq;
     if (lane == 0) {
         if (nbSeq < 128) {
@@ -695,18 +713,22 @@ __device__ uint64_t block_body_wave(jzc::Work &W, const WSeq &ss, uint8_t *codes
         for (uint32_t k = 0; k < 3; k++) {
             uint32_t max, mf;
             hist_codes_wave(W, cds[k], nbSeq, maxIn[k], lane, max, mf);
+            ZT("zc: hist %u max %u mf %u\n", k, max, mf);
             const uint32_t type = k == 1 ? jzc::select_type(mf, nbSeq, 5, max <= jzc::kDefaultMaxOff)
                                          : jzc::select_type(mf, nbSeq, 6, true);
             if (lane == 0) bc[0] = build_table_lane(&W, body + op, k, type, max, cds[k], nbSeq);
             wave_sync();
             const uint32_t t = uni(bc[0]);
+            ZT("zc: table %u type %u size %u\n", k, type, t);
             if (type == jzc::kSetCompressed) lastNCount = (int32_t)op;
             op += t;
             types[k] = type;
         }
         if (lane == 0) body[seqHead] = (uint8_t)((types[0] << 6) + (types[1] << 4) + (types[2] << 2));
         if (op + 16 >= jzc::kBodyCap) return 0;
+        ZT("zc: sequences at %u\n", op);
         const uint32_t b = sequences_wave(W, body, op, jzc::kBodyCap, ss.seq, llc, mlc, ofc, rec, nbSeq, lane);
+        ZT("zc: sequences -> %u\n", b);
         if (b == 0) return 0;
         op += b;
         if (lastNCount >= 0 && (int32_t)op - lastNCount < 4) return 0;
@@ -720,10 +742,13 @@ __device__ uint64_t compress_object(const uint8_t *src, uint64_t n, uint8_t *dst
                                     jzc::SeqDef *seqs, uint8_t *lits, uint8_t *codes, uint8_t *body, uint16_t *rec,
                                     jzc::Work &W, uint32_t lane) {
     const jzc::Params P = jzc::level1_params(n);
+    ZT("zc: params %u %u %u\n", P.wlog, P.hlog, P.mls);
     __shared__ uint32_t bcast;
     if (lane == 0) bcast = frame_header_lane(dst, n, P);
+    ZT("zc: header %u\n", bcast);
     __syncthreads();
     uint64_t op = uni(bcast);
+    ZT("zc: op %lu\n", (unsigned long)op);
     if (n == 0) {
         if (lane == 0) jzc::wr24(dst + op, 1);
         return op + 3;
@@ -744,7 +769,9 @@ __device__ uint64_t compress_object(const uint8_t *src, uint64_t n, uint8_t *dst
             WSeq ss{seqs, lits, 0, 0, 0, 0};
             uint32_t nrep[2] = {rep[0], rep[1]};
             __syncthreads();  // the table clear / last block's work has landed
+            ZT("zc: parse block at %lu bs %u\n", (unsigned long)pos, bs);
             const uint32_t lastLL = parse_fast_wave(src, (int32_t)pos, (int32_t)(pos + bs), htab, P, nrep, ss, lane);
+            ZT("zc: parsed nseq %u lastLL %u\n", ss.nseq, lastLL);
             for (uint32_t o = lane; o < lastLL; o += 64)
                 *(gu8c *)(lits + ss.nlit + o) = (uint8_t)ld8(src + pos + bs - lastLL + o);
             ss.nlit += lastLL;
@@ -795,12 +822,16 @@ __device__ uint64_t compress_object(const uint8_t *src, uint64_t n, uint8_t *dst
 }
 }  // namespace
 
-// Persistent: wave w takes objects from *queue until none is left, so every
-// wave reaches the exit.  ZDev.len = input bytes, ZDev.cap >= ZSTD_compressBound.
+// Wave w compresses objects w, w + W, w + 2W, ... (W = gridDim.x): a loop
+// whose trip count lives in SGPRs, so every lane runs it in lock-step.  (The
+// first version took objects from an atomic queue through an LDS word; the
+// compiler nested that loop so that lanes 1..63 re-ran the object loop
+// waiting for lane 0's next queue read while lane 0 was masked off -- a hang on
+// the first object, GPU-traced in round 3.)  ZDev.len = input bytes,
+// ZDev.cap >= ZSTD_compressBound.
 __global__ __launch_bounds__(64) void zstd_compress_k(const ZDev *__restrict__ blks, ZOut *__restrict__ outs,
-                                                      uint8_t *__restrict__ scratch, uint32_t *queue, int n) {
+                                                      uint8_t *__restrict__ scratch, int n) {
     __shared__ jzc::Work W;
-    __shared__ int next;
     const uint32_t lane = threadIdx.x;
     uint8_t *const sc = scratch + (size_t)blockIdx.x * kZcScratchStride;
     uint32_t *const htab = (uint32_t *)sc;
@@ -809,33 +840,27 @@ __global__ __launch_bounds__(64) void zstd_compress_k(const ZDev *__restrict__ b
     uint8_t *const codes = lits + kZcLit;
     uint8_t *const body = codes + kZcCodes;
     uint16_t *const rec = (uint16_t *)(body + kZcBody);
-    for (;;) {
-        if (lane == 0) next = (int)atomicAdd(queue, 1u);
-        __syncthreads();
-        const int obj = unis(next);
-        __syncthreads();
-        if (obj >= n) break;
+    for (int obj = (int)blockIdx.x; obj < n; obj += (int)gridDim.x) {
         const ZDev b = blks[obj];
+        ZT("zc: object %d len %lu\n", obj, (unsigned long)b.len);
 #ifdef JFSX_ZC_SCALAR
-        if (lane == 0) {
-            outs[obj].out_len = jzc::compress_frame(b.src, b.len, b.dst, htab, seqs, lits, codes, body, W);
-            outs[obj].status = JFSX_OK;
-        }
+        uint64_t r = 0;
+        if (lane == 0) r = jzc::compress_frame(b.src, b.len, b.dst, htab, seqs, lits, codes, body, W);
 #else
         const uint64_t r = compress_object(b.src, b.len, b.dst, htab, seqs, lits, codes, body, rec, W, lane);
+#endif
+        ZT("zc: object %d -> %lu\n", obj, (unsigned long)r);
         if (lane == 0) {
             outs[obj].out_len = r;
             outs[obj].status = JFSX_OK;
         }
-#endif
+        __syncthreads();  // W and the scratch are reused by the next object
     }
 }
 
-void launch_zstd_compress(hipStream_t s, int n, int waves, const ZDev *blks, ZOut *outs, uint8_t *scratch,
-                          uint32_t *queue) {
+void launch_zstd_compress(hipStream_t s, int n, int waves, const ZDev *blks, ZOut *outs, uint8_t *scratch) {
     if (n <= 0) return;
-    (void)hipMemsetAsync(queue, 0, 4, s);
-    hipLaunchKernelGGL(zstd_compress_k, dim3(waves), dim3(64), 0, s, blks, outs, scratch, queue, n);
+    hipLaunchKernelGGL(zstd_compress_k, dim3(waves), dim3(64), 0, s, blks, outs, scratch, n);
 }
 
 }  // namespace jfsx

@@ -214,7 +214,7 @@ def debug_tables():
     """Host-built lookup tables (no device needed)."""
     L = load_library()
     aes = np.empty(16384, np.uint32)
-    crc = np.empty(7168, np.uint32)
+    crc = np.empty(8192, np.uint32)
     crcx = np.empty(192, np.uint32)
     L.jfsx_debug_tables(aes.ctypes.data, crc.ctypes.data, crcx.ctypes.data)
     return aes, crc, crcx

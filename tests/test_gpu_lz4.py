@@ -129,3 +129,34 @@ def test_edge_statuses(eng):
     with pytest.raises(E.EngineError) as ei:
         eng.lz4_compress_batch(arr, n, E.MEM_HOST)
     assert ei.value.code == E.EINVAL
+
+
+def test_match_in_the_first_bytes(eng):
+    """Periodic inputs whose first match starts at byte 1..8 of the block.  The
+    compressor's combined 4-byte test and match count reads the match side at
+    a lane-0 position below byte 0 here; before that read was clamped the
+    position wrapped to 2^32 - k and the load faulted (the round-2 EIO of
+    gpurun_out/lz4cab_c2).  Every block equals the oracle's, in
+    blocks placed at every alignment of a 4-byte word."""
+    srcs = []
+    for period in range(1, 9):
+        for n in (13, 14, 17, 31, 64, 100, 300, 4096):
+            pat = bytes((0x61 + 7 * k) & 0xff for k in range(period))
+            srcs.append((pat * (n // period + 1))[:n])
+    outs = eng.lz4_compress(srcs)
+    for s, o in zip(srcs, outs):
+        assert o == orc.lz4_compress(s), (len(s), s[:8])
+    inb = eng.alloc(sum(len(s) + 3 for s in srcs) + 64)
+    caps = [int(E.lz4_bound(len(s))) for s in srcs]
+    outb = eng.alloc(sum(caps) + 64)
+    specs, io, oo = [], 1, 0
+    for s, c in zip(srcs, caps):
+        inb.upload(np.frombuffer(s, np.uint8), io)
+        specs.append((inb.ptr + io, len(s), outb.ptr + oo, c))
+        io += len(s) + 3
+        oo += c
+    arr, k = eng.make_zblocks(specs)
+    eng.lz4_compress_batch(arr, k, E.MEM_DEVICE)
+    for i, (s, (_, _, dp, _)) in enumerate(zip(srcs, specs)):
+        assert arr[i].status == E.OK
+        assert outb.download(arr[i].out_len, dp - outb.ptr).tobytes() == orc.lz4_compress(s), i
