@@ -139,7 +139,12 @@ void make_crc_tables(std::vector<uint32_t> &crc, std::vector<uint32_t> &crcx) {
     // 16-B pieces at 1 KiB row stride (GCM), 4032 B for 64-B chunks at 4 KiB (ChaCha)
     // (and 1024 B / 4096 B: a whole row / a whole 4 KiB span of 64-B lane chunks,
     // for the CRC-only kernel's A' = S(A) ^ crc_raw(0, chunk))
-    const uint32_t x1008 = xpow8(1008), x4032 = xpow8(4032), x1024 = xpow8(1024), x4096 = xpow8(4096);
+#ifndef JFSX_CRC_SPAN
+#define JFSX_CRC_SPAN 64
+#endif
+    // (the CRC-only kernel's span: 64 lanes x JFSX_CRC_SPAN bytes, jfsx_crc.hip)
+    const uint32_t x1008 = xpow8(1008), x4032 = xpow8(4032), x1024 = xpow8(1024),
+                   x4096 = xpow8(64 * (JFSX_CRC_SPAN >= 64 ? JFSX_CRC_SPAN : 64));
     for (int k = 0; k < 4; k++)
         for (uint32_t v = 0; v < 256; v++) {
             crc[(16 + k) * 256 + v] = crc_mulmod_h(x1008, v << (8 * k));

@@ -98,7 +98,10 @@ __device__ __noinline__ uint32_t crc_partial_g(const uint32_t *__restrict__ T, u
     return c;
 }
 
-__global__ __launch_bounds__(kCrcWaves * 64) __attribute__((amdgpu_waves_per_eu(8))) void crc_segments_k(const Task *__restrict__ tasks,
+#ifndef JFSX_CRC_WPE
+#define JFSX_CRC_WPE 8
+#endif
+__global__ __launch_bounds__(kCrcWaves * 64) __attribute__((amdgpu_waves_per_eu(JFSX_CRC_WPE))) void crc_segments_k(const Task *__restrict__ tasks,
                                                                 const BlkDev *__restrict__ blks, DevTables tab) {
     __shared__ __attribute__((aligned(16))) char lds[kCrcLds];
     const Task task = tasks[blockIdx.x];
@@ -107,7 +110,7 @@ __global__ __launch_bounds__(kCrcWaves * 64) __attribute__((amdgpu_waves_per_eu(
     // stage: i = (table t, hi, nibble, replica quad rq)
     for (uint32_t i = tid; i < 640 * 8; i += kCrcWaves * 64) {
         const uint32_t rq = i & 7, nib = (i >> 3) & 15, hi = (i >> 7) & 1, t = i >> 8;
-        const uint32_t v = tab.crc[(t < 16 ? t : t + (JFSX_CRC_SPAN == 64 ? 12 : 8)) * 256 + (hi ? nib << 4 : nib)];
+        const uint32_t v = tab.crc[(t < 16 ? t : t + (JFSX_CRC_SPAN >= 64 ? 12 : 8)) * 256 + (hi ? nib << 4 : nib)];
         *reinterpret_cast<uint4 *>(lds + t * 4096 + nib * 256 + hi * 128 + 16 * rq) = make_uint4(v, v, v, v);
     }
     __syncthreads();
@@ -118,28 +121,28 @@ __global__ __launch_bounds__(kCrcWaves * 64) __attribute__((amdgpu_waves_per_eu(
         const uint64_t seg1 = seg0 + kSeg < task.c1 ? seg0 + kSeg : task.c1;
         uint32_t A = 0, lend = 0;
         const uint64_t nrows = (seg1 - seg0 + 1023) / 1024;
-        if (JFSX_CRC_SPAN == 64 && seg1 - seg0 == (uint64_t)kSeg) {
-            // full segment: 8 spans of 4 KiB, lane chunk 64 B; the next span's
-            // four loads are in flight while this one is folded
-            const uint8_t *q = src + seg0 + 64 * lane;
-            uint4 buf[4];
+        if (JFSX_CRC_SPAN >= 64 && seg1 - seg0 == (uint64_t)kSeg) {
+            // full segment: spans of 64 x SPAN bytes, lane chunk SPAN bytes
+            // (P pieces); each piece's load for the next span is issued as
+            // soon as the piece is consumed
+            constexpr int P = JFSX_CRC_SPAN / 16, NSP = 32768 / (64 * JFSX_CRC_SPAN);
+            const uint8_t *q = src + seg0 + JFSX_CRC_SPAN * lane;
+            uint4 buf[P];
 #pragma unroll
-            for (int j = 0; j < 4; j++) buf[j] = gld16(q + 16 * j);
+            for (int j = 0; j < P; j++) buf[j] = gld16(q + 16 * j);
 #pragma unroll
-            for (int r = 0; r < 8; r++) {
-                const uint4 p0 = buf[0], p1 = buf[1], p2 = buf[2], p3 = buf[3];
-                if (r + 1 < 8) {
+            for (int r = 0; r < NSP; r++) {
+                uint32_t c = 0;
 #pragma unroll
-                    for (int j = 0; j < 4; j++) buf[j] = gld16(q + 4096 * (r + 1) + 16 * j);
+                for (int j = 0; j < P; j++) {
+                    const uint4 p = buf[j];
+                    if (r + 1 < NSP) buf[j] = gld16(q + 64 * JFSX_CRC_SPAN * (r + 1) + 16 * j);
+                    c = crc_u16_nib(lds, lb, p.x ^ c, p.y, p.z, p.w);
                 }
-                uint32_t c = crc_u16_nib(lds, lb, p0.x, p0.y, p0.z, p0.w);
-                c = crc_u16_nib(lds, lb, p1.x ^ c, p1.y, p1.z, p1.w);
-                c = crc_u16_nib(lds, lb, p2.x ^ c, p2.y, p2.z, p2.w);
-                c = crc_u16_nib(lds, lb, p3.x ^ c, p3.y, p3.z, p3.w);
                 A = crc_word_nib(lds, lb, 16, A) ^ c;
             }
-            lend = kSeg;  // marker: lane chunk ends at 28672 + 64 * lane + 64
-        } else if (JFSX_CRC_SPAN != 64 && seg1 - seg0 == (uint64_t)kSeg) {
+            lend = kSeg;  // marker: lane chunk ends at 32768 - SPAN * (63 - lane)
+        } else if (JFSX_CRC_SPAN < 64 && seg1 - seg0 == (uint64_t)kSeg) {
             // full segment: 32 rows, kCrcPf loads in flight per wave (HBM
             // latency x 8 TB/s needs ~64 KiB in flight per CU)
             const uint8_t *q = src + seg0 + 16 * lane;
@@ -158,7 +161,7 @@ __global__ __launch_bounds__(kCrcWaves * 64) __attribute__((amdgpu_waves_per_eu(
                 const uint64_t o = seg0 + 1024 * r + 16 * lane;
                 const uint4 p = load_piece(src, o, seg1);
                 if (o + 16 <= seg1) {
-                    A = JFSX_CRC_SPAN == 64 ? crc_row_g(lds, tab.crc, lb, A, p) : crc_row_nib(lds, lb, A, p);
+                    A = JFSX_CRC_SPAN >= 64 ? crc_row_g(lds, tab.crc, lb, A, p) : crc_row_nib(lds, lb, A, p);
                     lend = (uint32_t)(o + 16 - seg0);
                 } else if (o < seg1) {
                     const uint32_t pw[4] = {p.x, p.y, p.z, p.w};
@@ -170,7 +173,15 @@ __global__ __launch_bounds__(kCrcWaves * 64) __attribute__((amdgpu_waves_per_eu(
         const uint32_t Lseg = (uint32_t)(seg1 - seg0);
         uint32_t v, K;
         if (Lseg == (uint32_t)kSeg) {
-            v = crc_mulmod(tab.crcx[JFSX_CRC_SPAN == 64 ? 128 + lane : lane], A);
+            if (JFSX_CRC_SPAN >= 64) {
+                // lane chunk end to segment end: SPAN * (63 - lane) bytes =
+                // crcx[128 + lane] (64 * (63 - lane) bytes) squared SPAN / 64 - 1 times
+                uint32_t x = tab.crcx[128 + lane];
+                for (int k = 64; k < JFSX_CRC_SPAN; k <<= 1) x = crc_mulmod(x, x);
+                v = crc_mulmod(x, A);
+            } else {
+                v = crc_mulmod(tab.crcx[lane], A);
+            }
             K = tab.crcx[96];
         } else {
             v = crc_mulmod(crc_xpow8(Lseg - lend, tab.crcx + 64), A);

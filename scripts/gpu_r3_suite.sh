@@ -2,7 +2,7 @@
 # with its same-run CPU baseline; rocprofv3 kernel stats at the bench lines'
 # own configs; PMC passes named pmc_<variant>__<set> for scripts/pmc_r3.py
 # (FETCH/WRITE at the bench size, SQ busy counters on a 4 GiB batch).
-# usage: bash scripts/gpu_r3_suite.sh <tag> [lines|prof|pmc|all]
+# usage: bash scripts/gpu_r3_suite.sh <tag> [lines1|lines2|prof|pmc1|pmc2|all]
 set -u
 cd "$GRAFT_REPO_ROOT"
 out=gpurun_out/suite_$1
@@ -14,7 +14,7 @@ prof() { name=$1; shift; timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $
 pmc() { name=$1; ctr=$2; shift 2; timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $ctr -d $out/pmc_$name -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu --verify 0 "$@" > $out/pmc_$name.log 2>&1 || { echo "pmc $name failed"; grep -v "^ *@" $out/pmc_$name.log | tail -3; return 1; }; echo "pmc $name ok"; }
 SQ="SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU GRBM_GUI_ACTIVE"
 Z="--blocks 4096"   # codec lines: 16 GiB
-if [ $what = lines ] || [ $what = all ]; then
+if [ $what = lines1 ] || [ $what = all ]; then
 run seal_gcm && \
 run seal_gcm_bitslice --aes bitslice && \
 run seal_chacha --algo chacha20poly1305 && \
@@ -24,7 +24,9 @@ run crc_verify --mode crc && \
 run seal_gcm_ragged --ragged && run open_gcm_ragged --ragged --mode open && \
 run seal_chacha_ragged --ragged --algo chacha20poly1305 && run open_chacha_ragged --ragged --mode open --algo chacha20poly1305 && \
 run decrypt_gcm --mode decrypt && \
-run ingest_gcm --mem host --blocks 2048 --steps 8 --warmup 1 && \
+run ingest_gcm --mem host --blocks 2048 --steps 8 --warmup 1 || exit 1
+fi
+if [ $what = lines2 ] || [ $what = all ]; then
 run lz4_text --mode lz4 $Z && run unlz4_text --mode unlz4 $Z && \
 run zstd_text --mode zstd $Z --steps 3 --warmup 1 && run unzstd_text --mode unzstd $Z && \
 run agg_gcm_t20 --mode agg --threads 20 --steps 5 --warmup 1 && run agg_gcm_t32 --mode agg --threads 32 --steps 5 --warmup 1 && \
@@ -40,7 +42,7 @@ prof cp --algo chacha20poly1305 --steps 10 --warmup 2 && prof crc --mode crc --s
 prof zstd_text --mode zstd $Z --steps 3 --warmup 1 && prof unzstd_text --mode unzstd $Z --steps 10 --warmup 2 && \
 prof lz4_text --mode lz4 $Z --steps 10 --warmup 2 && prof unlz4_text --mode unlz4 $Z --steps 10 --warmup 2 || exit 1
 fi
-if [ $what = pmc ] || [ $what = all ]; then
+if [ $what = pmc1 ] || [ $what = all ]; then
 for v in "seal_gcm:" "open_gcm:--mode open" "seal_chacha:--algo chacha20poly1305" \
          "open_chacha:--mode open --algo chacha20poly1305" "crc_verify:--mode crc" \
          "seal_gcm_ragged:--ragged" "open_gcm_ragged:--ragged --mode open" \
@@ -51,10 +53,12 @@ for v in "seal_gcm:" "open_gcm:--mode open" "seal_chacha:--algo chacha20poly1305
   name=${v%%:*}; a=${v#*:}
   pmc ${name}__fetch FETCH_SIZE $a && pmc ${name}__write WRITE_SIZE $a || exit 1
 done
+fi
+if [ $what = pmc2 ] || [ $what = all ]; then
 for v in "seal_gcm:" "open_gcm:--mode open" "seal_chacha:--algo chacha20poly1305" "crc_verify:--mode crc" \
          "seal_gcm_bitslice:--aes bitslice"; do
   name=${v%%:*}; a=${v#*:}
   pmc ${name}__sq "$SQ" --blocks 1024 $a || exit 1
 done
-python3 scripts/pmc_r3.py $out > $out/pmc_r3.json && echo "pmc summary done"
+echo "pmc2 done (summary: python3 scripts/pmc_r3.py gpurun_out/suite_<tag> on the merged passes)"
 fi
