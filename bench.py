@@ -981,6 +981,7 @@ def zstd_bench(args, world, rank, local, dist, eng):
     for _ in range(args.warmup):
         step()
     eng.sync()
+    eng.metrics(reset=True)
     eng.kernel_time(reset=True)
     eng.set_timing(True)
     barrier(dist)
@@ -993,6 +994,7 @@ def zstd_bench(args, world, rank, local, dist, eng):
     eng.set_timing(False)
     k_ms, k_n = eng.kernel_time(reset=True)
     k_avg = k_ms / max(k_n, 1)
+    serial = eng.metrics()["zstd_serial"]
     verified = 0
     if args.verify:
         for b in range(0, nb, max(1, nb // args.verify))[:args.verify]:
@@ -1020,7 +1022,9 @@ def zstd_bench(args, world, rank, local, dist, eng):
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(algo_bytes / (k_avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if k_n else None,
                          "traffic": pmc_traffic(args, nb * L)[0], "traffic_source": pmc_traffic(args, nb * L)[1],
-                         "kernel": "zstd_decompress_k", "kernel_avg_ms": round(k_avg, 3),
+                         "kernel": "zstd_decompress_k" if os.environ.get("JFSX_ZSTD_SERIAL") == "1"
+                         else "zstd_decompress_par_k", "kernel_avg_ms": round(k_avg, 3),
+                         "objects_to_serial_decoder": serial,
                          "algorithmic_bytes_per_launch": algo_bytes, "plain_bytes_per_launch": nb * L},
             "cpu_baseline": cpu, "verified_blocks": verified}), flush=True)
     eng.close()

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define JFSX_ABI_VERSION 6
+#define JFSX_ABI_VERSION 7
 
 /* algorithms (encrypt.go:142-145) */
 #define JFSX_AES256GCM 0     /* "aes256gcm-rsa" (also the "" default)   */
@@ -155,6 +155,30 @@ int jfsx_ctx_set_timing(jfsx_ctx *ctx, int enable);
  * overlapped on three streams */
 int jfsx_ctx_set_slot_bytes(jfsx_ctx *ctx, uint64_t bytes);
 int jfsx_ctx_kernel_time(jfsx_ctx *ctx, double *ms_total, uint64_t *launches, int reset);
+
+/* Engine counters for the shim's metrics hooks -- the byte / op counters the
+ * reference keeps around the block path (cachedStore's Prometheus collectors,
+ * pkg/chunk/cached_store.go:847-932: object request bytes and durations,
+ * cache hits / misses / read bytes).  Per context, cumulative since open or the
+ * last reset; a batch is counted when it returns 0.  bytes = plaintext
+ * (AEAD), range (CRC) and input / output (codecs); *_fail = blocks whose
+ * status was not JFSX_OK (tag, checksum, malformed, too small).  zstd_serial =
+ * zstd objects the block-parallel decoder handed to the serial decoder (frame
+ * shapes outside its fast path, or frames it rejects).  kernel_ms /
+ * kernel_launches: the main-kernel time, counted only while
+ * jfsx_ctx_set_timing is enabled. */
+typedef struct jfsx_metrics {
+    uint64_t seal_batches, seal_blocks, seal_bytes;
+    uint64_t open_batches, open_blocks, open_bytes, open_fail;
+    uint64_t crc_batches, crc_ranges, crc_bytes, crc_fail;
+    uint64_t lz4c_blocks, lz4c_in, lz4c_out;
+    uint64_t lz4d_blocks, lz4d_in, lz4d_out, lz4d_fail;
+    uint64_t zstdc_blocks, zstdc_in, zstdc_out;
+    uint64_t zstdd_blocks, zstdd_in, zstdd_out, zstdd_fail, zstd_serial;
+    double kernel_ms;
+    uint64_t kernel_launches;
+} jfsx_metrics;
+int jfsx_ctx_metrics(jfsx_ctx *ctx, jfsx_metrics *out, int reset);
 
 /* memory helpers (engine-owned pinned staging, device buffers); pinned memory
  * is portable: any context of the process (any GPU) may stream from it */

@@ -5,6 +5,7 @@
 // main transform kernel (one workgroup per task) -> finalize kernel -> D2H of
 // per-block results (tags, status, first failing CRC) -> stream sync.
 #include <errno.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -214,9 +215,46 @@ struct jfsx_ctx {
     size_t arena_cap = 0;
     std::mutex err_mu;       // last HIP failure on this context (jfsx_last_error)
     ErrRec err;
+    jfsx_metrics met{};      // jfsx_ctx_metrics (updated under mu)
 };
 
 namespace {
+// jfsx_ctx_metrics tallies, under c->mu, after a batch returned 0
+void tally_aead(jfsx_ctx *c, bool open, int n, const jfsx_blk *b) {
+    jfsx_metrics &m = c->met;
+    uint64_t bytes = 0, fail = 0;
+    for (int i = 0; i < n; i++) {
+        bytes += b[i].len;
+        fail += b[i].status != JFSX_OK;
+    }
+    if (open) {
+        m.open_batches++;
+        m.open_blocks += n;
+        m.open_bytes += bytes;
+        m.open_fail += fail;
+    } else {
+        m.seal_batches++;
+        m.seal_blocks += n;
+        m.seal_bytes += bytes;
+    }
+}
+void tally_crc(jfsx_ctx *c, int n, const jfsx_range *r) {
+    jfsx_metrics &m = c->met;
+    m.crc_batches++;
+    m.crc_ranges += n;
+    for (int i = 0; i < n; i++) {
+        m.crc_bytes += r[i].len;
+        m.crc_fail += r[i].status != JFSX_OK;
+    }
+}
+void tally_codec(uint64_t &blocks, uint64_t &in, uint64_t &out, uint64_t *fail, int n, const jfsx_zblk *z) {
+    blocks += n;
+    for (int i = 0; i < n; i++) {
+        in += z[i].src_len;
+        out += z[i].out_len;
+        if (fail) *fail += z[i].status != JFSX_OK;
+    }
+}
 void note_ctx_error(jfsx_ctx *c, const ErrRec &e) {
     std::lock_guard<std::mutex> g(c->err_mu);
     c->err = e;
@@ -801,10 +839,14 @@ int run_codec(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, CodecOp op) {
     int rc;
     Workspace &w = c->ws[0];
     const int zc_waves = std::min(n, c->ncu * kZcWavesPerCu);
+    // zstd decompression: block-parallel persistent waves unless
+    // JFSX_ZSTD_SERIAL=1 selects the one-wave-per-object serial kernel (A/B)
+    static const bool zd_serial = getenv("JFSX_ZSTD_SERIAL") && atoi(getenv("JFSX_ZSTD_SERIAL")) == 1;
+    const int zd_waves = op == kZstdDecomp && !zd_serial ? zstd_par_waves(n, c->ncu) : 0;
     const size_t o_out = align256(sizeof(ZDev) * n), o_tab = o_out + align256(sizeof(ZOut) * n);
     size_t extra = 0;
     if (op == kLz4Comp) extra = kLz4TabBytes * (size_t)n;
-    else if (op == kZstdDecomp) extra = kZstdScratch * (size_t)n;
+    else if (op == kZstdDecomp) extra = zd_waves ? kZstdArena * (size_t)zd_waves : kZstdScratch * (size_t)n;
     else if (op == kZstdComp) extra = 256 + kZstdcScratch * (size_t)zc_waves;  // per-wave scratch
     if ((rc = ensure_dev(c, &w.d, &w.dcap, o_tab + extra))) return rc;
     if ((rc = ensure_host(&w.h, &w.hcap, o_tab))) return rc;  // descriptors and results only
@@ -841,7 +883,7 @@ int run_codec(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, CodecOp op) {
         launch_lz4_decompress(s, n, dz, dout);
         break;
     case kZstdDecomp:
-        launch_zstd_decompress(s, n, dz, dout, (uint8_t *)(w.d + o_tab));
+        launch_zstd_decompress(s, n, dz, dout, (uint8_t *)(w.d + o_tab), zd_waves);
         break;
     case kZstdComp:
         launch_zstd_compress(s, n, zc_waves, dz, dout, (uint8_t *)(w.d + o_tab + 256));
@@ -861,6 +903,7 @@ int run_codec(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, CodecOp op) {
     for (int i = 0; i < n; i++) {
         z[i].out_len = ho[i].out_len;
         z[i].status = ho[i].status;
+        if (op == kZstdDecomp && zd_waves) c->met.zstd_serial += ho[i].fallback != 0;
         if (mem == JFSX_MEM_HOST && ho[i].out_len)
             HIP_OK(hipMemcpyAsync(z[i].dst, sdst[i], ho[i].out_len, hipMemcpyDeviceToHost, s));
     }
@@ -1018,6 +1061,20 @@ int jfsx_ctx_kernel_time(jfsx_ctx *c, double *ms_total, uint64_t *launches, int 
     return 0;
 }
 
+int jfsx_ctx_metrics(jfsx_ctx *c, jfsx_metrics *out, int reset) {
+    if (!c || !out) return JFSX_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    *out = c->met;
+    out->kernel_ms = c->ms_total;
+    out->kernel_launches = c->launches;
+    if (reset) {
+        c->met = jfsx_metrics{};
+        c->ms_total = 0;
+        c->launches = 0;
+    }
+    return 0;
+}
+
 int jfsx_alloc_pinned(jfsx_ctx *c, size_t bytes, void **p) {
     if (!c || !p) return JFSX_EINVAL;
     CtxScope es_(c);
@@ -1069,8 +1126,10 @@ int jfsx_seal_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *blks, int crc_mode, 
     std::lock_guard<std::mutex> g(c->mu);
     CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
-    return mem == JFSX_MEM_HOST ? run_aead_host(c, algo, false, n, blks, crc_mode)
-                                : run_aead(c, algo, false, n, blks, crc_mode);
+    const int rc = mem == JFSX_MEM_HOST ? run_aead_host(c, algo, false, n, blks, crc_mode)
+                                        : run_aead(c, algo, false, n, blks, crc_mode);
+    if (rc == 0) tally_aead(c, false, n, blks);
+    return rc;
 }
 
 int jfsx_open_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *blks, int crc_mode, int mem) {
@@ -1078,8 +1137,10 @@ int jfsx_open_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *blks, int crc_mode, 
     std::lock_guard<std::mutex> g(c->mu);
     CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
-    return mem == JFSX_MEM_HOST ? run_aead_host(c, algo, true, n, blks, crc_mode)
-                                : run_aead(c, algo, true, n, blks, crc_mode);
+    const int rc = mem == JFSX_MEM_HOST ? run_aead_host(c, algo, true, n, blks, crc_mode)
+                                        : run_aead(c, algo, true, n, blks, crc_mode);
+    if (rc == 0) tally_aead(c, true, n, blks);
+    return rc;
 }
 
 int jfsx_crc32c_segments(jfsx_ctx *c, int n, jfsx_range *ranges, int mode, int mem) {
@@ -1087,7 +1148,9 @@ int jfsx_crc32c_segments(jfsx_ctx *c, int n, jfsx_range *ranges, int mode, int m
     std::lock_guard<std::mutex> g(c->mu);
     CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
-    return mem == JFSX_MEM_HOST ? run_crc_host(c, n, ranges, mode) : run_crc(c, n, ranges, mode);
+    const int rc = mem == JFSX_MEM_HOST ? run_crc_host(c, n, ranges, mode) : run_crc(c, n, ranges, mode);
+    if (rc == 0) tally_crc(c, n, ranges);
+    return rc;
 }
 
 uint64_t jfsx_lz4_bound(uint64_t n) { return lz4_bound(n); }
@@ -1097,7 +1160,9 @@ int jfsx_lz4_compress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
     std::lock_guard<std::mutex> g(c->mu);
     CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
-    return run_codec(c, n, blks, mem, kLz4Comp);
+    const int rc = run_codec(c, n, blks, mem, kLz4Comp);
+    if (rc == 0) tally_codec(c->met.lz4c_blocks, c->met.lz4c_in, c->met.lz4c_out, nullptr, n, blks);
+    return rc;
 }
 
 int jfsx_lz4_decompress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
@@ -1105,7 +1170,9 @@ int jfsx_lz4_decompress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
     std::lock_guard<std::mutex> g(c->mu);
     CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
-    return run_codec(c, n, blks, mem, kLz4Decomp);
+    const int rc = run_codec(c, n, blks, mem, kLz4Decomp);
+    if (rc == 0) tally_codec(c->met.lz4d_blocks, c->met.lz4d_in, c->met.lz4d_out, &c->met.lz4d_fail, n, blks);
+    return rc;
 }
 
 int jfsx_zstd_decompress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
@@ -1113,7 +1180,9 @@ int jfsx_zstd_decompress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
     std::lock_guard<std::mutex> g(c->mu);
     CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
-    return run_codec(c, n, blks, mem, kZstdDecomp);
+    const int rc = run_codec(c, n, blks, mem, kZstdDecomp);
+    if (rc == 0) tally_codec(c->met.zstdd_blocks, c->met.zstdd_in, c->met.zstdd_out, &c->met.zstdd_fail, n, blks);
+    return rc;
 }
 
 uint64_t jfsx_zstd_bound(uint64_t n) { return zstd_bound(n); }
@@ -1123,7 +1192,9 @@ int jfsx_zstd_compress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
     std::lock_guard<std::mutex> g(c->mu);
     CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
-    return run_codec(c, n, blks, mem, kZstdComp);
+    const int rc = run_codec(c, n, blks, mem, kZstdComp);
+    if (rc == 0) tally_codec(c->met.zstdc_blocks, c->met.zstdc_in, c->met.zstdc_out, nullptr, n, blks);
+    return rc;
 }
 
 int jfsx_checksum(jfsx_ctx *c, const void *data, uint64_t len, uint8_t *out) {

@@ -94,7 +94,7 @@ struct ZDev {
 struct ZOut {
     uint64_t out_len;
     int32_t status;
-    int32_t pad;
+    int32_t fallback;  // zstd decompression: 1 when the serial decoder took the object
 };
 
 struct BlkOut {        // written by finalize, copied back to the host
@@ -296,7 +296,13 @@ void launch_lz4_decompress(hipStream_t s, int n, const ZDev *blks, ZOut *outs);
 // buffer + the literal window's read-ahead, then a log-12 Huffman table)
 constexpr size_t kZstdHufOff = 128 * 1024 + 320;
 constexpr size_t kZstdScratch = kZstdHufOff + 8192;
-void launch_zstd_decompress(hipStream_t s, int n, const ZDev *blks, ZOut *outs, uint8_t *scratch);
+// Block-parallel decoding (jfsx_zstd2.h): zstd_par_waves(n, ncu) persistent
+// waves, each with a kZstdArena-byte arena (tables, literals, sequences);
+// waves = 0 selects the serial one-wave-per-object kernel (n x kZstdScratch).
+constexpr size_t kZstdArena = (size_t)64 * 9216 + ((size_t)4 << 20) + (size_t)12 * (512u << 10);
+constexpr int kZstdWavesPerCu = 8;
+int zstd_par_waves(int n, int ncu);
+void launch_zstd_decompress(hipStream_t s, int n, const ZDev *blks, ZOut *outs, uint8_t *scratch, int waves);
 // Zstandard level-1 compression (jfsx_zstdc.hip): `waves` persistent
 // one-wave workgroups take objects w, w + waves, ... (a uniform strided loop);
 // each owns kZstdcScratch bytes of scratch (hash table, sequences, literals)

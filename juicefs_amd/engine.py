@@ -43,7 +43,7 @@ EXPORTS = [
     "jfsx_agg_lz4_compress", "jfsx_agg_lz4_decompress", "jfsx_mctx_lz4_compress_batch", "jfsx_mctx_lz4_decompress_batch",
     "jfsx_zstd_decompress_batch", "jfsx_agg_zstd_decompress", "jfsx_mctx_zstd_decompress_batch",
     "jfsx_last_error", "jfsx_zstd_bound", "jfsx_zstd_compress_batch", "jfsx_agg_zstd_compress",
-    "jfsx_mctx_zstd_compress_batch",
+    "jfsx_mctx_zstd_compress_batch", "jfsx_ctx_metrics",
 ]
 
 
@@ -99,6 +99,19 @@ class jfsx_zblk(ctypes.Structure):
     ]
 
 
+_METRIC_FIELDS = [
+    "seal_batches", "seal_blocks", "seal_bytes", "open_batches", "open_blocks", "open_bytes", "open_fail",
+    "crc_batches", "crc_ranges", "crc_bytes", "crc_fail", "lz4c_blocks", "lz4c_in", "lz4c_out",
+    "lz4d_blocks", "lz4d_in", "lz4d_out", "lz4d_fail", "zstdc_blocks", "zstdc_in", "zstdc_out",
+    "zstdd_blocks", "zstdd_in", "zstdd_out", "zstdd_fail", "zstd_serial",
+]
+
+
+class jfsx_metrics(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_uint64) for f in _METRIC_FIELDS] + [
+        ("kernel_ms", ctypes.c_double), ("kernel_launches", ctypes.c_uint64)]
+
+
 _lib = None
 _lib_lock = threading.Lock()
 
@@ -125,6 +138,7 @@ def load_library(path=LIB_PATH):
             "jfsx_ctx_set_timing": (I, [P, I]),
             "jfsx_ctx_set_slot_bytes": (I, [P, U64]),
             "jfsx_ctx_kernel_time": (I, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64), I]),
+            "jfsx_ctx_metrics": (I, [P, ctypes.POINTER(jfsx_metrics), I]),
             "jfsx_alloc_pinned": (I, [P, SZ, PP]),
             "jfsx_free_pinned": (I, [P, P]),
             "jfsx_alloc_device": (I, [P, SZ, PP]),
@@ -349,6 +363,12 @@ class Engine:
         n = ctypes.c_uint64()
         self.L.jfsx_ctx_kernel_time(self.ctx, ctypes.byref(ms), ctypes.byref(n), 1 if reset else 0)
         return ms.value, n.value
+
+    def metrics(self, reset=False):
+        """jfsx_ctx_metrics as a dict (counters since open or the last reset)."""
+        m = jfsx_metrics()
+        self._check(self.L.jfsx_ctx_metrics(self.ctx, ctypes.byref(m), 1 if reset else 0), "jfsx_ctx_metrics")
+        return {f: getattr(m, f) for f, _ in jfsx_metrics._fields_}
 
     # -- batches -----------------------------------------------------------
     @staticmethod

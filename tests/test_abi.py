@@ -23,7 +23,7 @@ def test_library_exports_every_symbol():
     L = engine.load_library()
     for name in _declared():
         assert hasattr(L, name), name
-    assert L.jfsx_abi_version() == 6
+    assert L.jfsx_abi_version() == 7
 
 
 def test_struct_layout_matches_header():
@@ -61,3 +61,13 @@ def test_parse_header():
 def test_last_error_is_empty_without_a_failure():
     # jfsx_last_error(NULL, ...): the calling thread's record; nothing failed here
     assert engine.last_error(None) == (0, "")
+
+
+def test_metrics_struct_layout():
+    # jfsx_metrics: 26 uint64 counters, double kernel_ms, uint64 kernel_launches
+    assert ctypes.sizeof(engine.jfsx_metrics) == 28 * 8
+    assert engine.jfsx_metrics.kernel_ms.offset == 26 * 8
+    src = open(os.path.join(ROOT, "include", "jfsx.h")).read()
+    body = src[src.index("typedef struct jfsx_metrics"):src.index("} jfsx_metrics;")]
+    names = re.findall(r"\b([a-z0-9_]+)\b(?=[,;])", body)
+    assert names == [f for f, _ in engine.jfsx_metrics._fields_]

@@ -207,3 +207,54 @@ def test_checksum_tail_reads_inside_output(eng):
         assert outb.download(n).tobytes() == src, n
         inb.free()
         outb.free()
+
+
+def test_block_parallel_decoder_takes_level1_frames(eng):
+    """The block-parallel decoder (jfsx_zstd2.h) takes every one-frame object
+    of up to 64 blocks without handing it to the serial decoder, across data
+    kinds, sizes, levels and content checksums; the bytes equal the input."""
+    srcs, frames = [], []
+    for kind in lz4_data.KINDS:
+        for n in (9, 4096, 131071, 131072, 131073, 1 << 20, (4 << 20) + 17):
+            for level, ck in ((1, False), (1, True), (3, False), (9, False)):
+                src = lz4_data.sample(kind, n, seed=7 * n + level)
+                srcs.append(src)
+                frames.append(zstd_lib.compress(src, level, ck))
+    eng.metrics(reset=True)
+    got = eng.zstd_decompress(frames, [len(s) for s in srcs])
+    m = eng.metrics()
+    for i, (src, (st, d)) in enumerate(zip(srcs, got)):
+        assert st == E.OK and d == src, i
+    assert m["zstdd_blocks"] == len(frames) and m["zstd_serial"] == 0
+    assert m["zstdd_out"] == sum(len(s) for s in srcs)
+
+
+def test_block_parallel_decoder_hands_off_other_shapes(eng):
+    """Concatenated frames, skippable frames and frames of more than 64 blocks
+    go to the serial decoder (counted in zstd_serial) and still decode."""
+    a = lz4_data.sample("text", 300000, seed=3)
+    big = lz4_data.sample("text", 9 << 20, seed=4)
+    fr = [zstd_lib.compress(a) + zstd_lib.compress(a), zstd_lib.skippable(b"x") + zstd_lib.compress(a),
+          zstd_lib.compress(big)]
+    eng.metrics(reset=True)
+    got = eng.zstd_decompress(fr, [2 * len(a), len(a), len(big)])
+    assert got[0] == (E.OK, a + a) and got[1] == (E.OK, a) and got[2] == (E.OK, big)
+    assert eng.metrics()["zstd_serial"] == 3
+
+
+def test_block_parallel_matches_across_blocks(eng):
+    """Matches and repeat offsets that cross 128 KiB block boundaries: a
+    period longer than a block, short periods (overlapping copies), and runs
+    of one byte; level 1 and 19-style long matches (level 9)."""
+    rng = np.random.default_rng(11)
+    base = rng.integers(0, 256, 200000, dtype=np.uint8).tobytes()
+    srcs = [(base * 6)[:1100000], (b"abcdefg" * 300000)[:2000000], bytes(1500000),
+            (rng.integers(0, 4, 3 << 20, dtype=np.uint8) + 65).astype(np.uint8).tobytes(),
+            b"".join(base[i:i + 5000] for i in range(0, 190000, 3700)) * 4]
+    frames = [zstd_lib.compress(s, lvl) for s in srcs for lvl in (1, 9)]
+    exp = [s for s in srcs for _ in (1, 9)]
+    eng.metrics(reset=True)
+    got = eng.zstd_decompress(frames, [len(s) for s in exp])
+    for i, (s, (st, d)) in enumerate(zip(exp, got)):
+        assert st == E.OK and d == s, i
+    assert eng.metrics()["zstd_serial"] == 0
