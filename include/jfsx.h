@@ -339,7 +339,11 @@ typedef struct jfsx_zblk {
     uint64_t dst_cap;
     uint64_t out_len;  /* out: bytes written to dst                      */
     int32_t status;    /* out: JFSX_OK / JFSX_EFORMAT (decompress)       */
-    int32_t reserved;
+    int32_t reserved;  /* zstd decompress, out: 0, or why the block-parallel
+                          decoder handed the object to the serial one: 1 frame
+                          shape / headers, 2 Huffman stream, 3 sequence stream,
+                          4 sequence execution, 5 raw / RLE block, 6 last
+                          literals, 7 content size, 8 content checksum */
 } jfsx_zblk;
 /* LZ4_compressBound: n + n/255 + 16 (0 for n > 0x7E000000) */
 uint64_t jfsx_lz4_bound(uint64_t n);
@@ -399,6 +403,14 @@ int jfsx_gen_synthetic_batch(jfsx_ctx *ctx, void *dst, uint64_t stride, int n, c
 /* fills n keys (32 B) and nonces (12 B) with the same per-block stream as
  * orc_gen_key, host side */
 void jfsx_gen_key(uint64_t seed, uint64_t block, uint8_t key[32], uint8_t nonce[12]);
+
+/* PCIe probe on the streams the host-ingest ring uses (H2D stream, D2H
+ * stream): `bytes` between engine-pinned host memory and device memory in
+ * 8 chunks per direction, best of 3; out[0] H2D alone, out[1] D2H alone,
+ * out[2] / out[3] H2D / D2H rate while both directions run at once (chunks
+ * issued alternately, as the ring issues them), in GB/s.  The ring moves equal
+ * bytes up and down, so min(out[2], out[3]) bounds a host-ingest seal. */
+int jfsx_pcie_probe(jfsx_ctx *ctx, uint64_t bytes, double out[4]);
 
 /* diagnostics: the lookup tables the kernels stage into LDS, built on the host
  * without a device (AES T0|T2 x32 replicated: 16384 dwords; CRC32C slice-by-16

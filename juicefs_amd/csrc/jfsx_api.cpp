@@ -9,6 +9,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <mutex>
 #include <vector>
 
@@ -903,7 +904,10 @@ int run_codec(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, CodecOp op) {
     for (int i = 0; i < n; i++) {
         z[i].out_len = ho[i].out_len;
         z[i].status = ho[i].status;
-        if (op == kZstdDecomp && zd_waves) c->met.zstd_serial += ho[i].fallback != 0;
+        if (op == kZstdDecomp) {
+            z[i].reserved = zd_waves ? ho[i].fallback : 0;
+            if (zd_waves) c->met.zstd_serial += ho[i].fallback != 0;
+        }
         if (mem == JFSX_MEM_HOST && ho[i].out_len)
             HIP_OK(hipMemcpyAsync(z[i].dst, sdst[i], ho[i].out_len, hipMemcpyDeviceToHost, s));
     }
@@ -1059,6 +1063,66 @@ int jfsx_ctx_kernel_time(jfsx_ctx *c, double *ms_total, uint64_t *launches, int 
         c->launches = 0;
     }
     return 0;
+}
+
+int jfsx_pcie_probe(jfsx_ctx *c, uint64_t bytes, double out[4]) {
+    if (!c || !out || bytes < 8 * 4096) return JFSX_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    CtxScope es_(c);
+    HIP_OK(hipSetDevice(c->device));
+    const int chunks = 8;
+    const size_t ch = (bytes / chunks) & ~(size_t)4095, tot = ch * chunks;
+    char *hA = nullptr, *hB = nullptr, *dA = nullptr, *dB = nullptr;
+    int rc = 0;
+    auto fail = [&](hipError_t e, int line, const char *what) {
+        note_hip_error(e, __FILE__, line, what);
+        rc = JFSX_EIO;
+    };
+    hipError_t e;
+    if ((e = hipHostMalloc((void **)&hA, tot, 0)) != hipSuccess || (e = hipHostMalloc((void **)&hB, tot, 0)) != hipSuccess ||
+        (e = hipMalloc((void **)&dA, tot)) != hipSuccess || (e = hipMalloc((void **)&dB, tot)) != hipSuccess) {
+        fail(e, __LINE__, "pcie probe buffers");
+    } else {
+        memset(hA, 1, tot);
+        memset(hB, 2, tot);
+        hipEvent_t ea, eb;
+        (void)hipEventCreate(&ea);
+        (void)hipEventCreate(&eb);
+        for (int mode = 0; mode < 3 && !rc; mode++) {  // 0 H2D, 1 D2H, 2 both
+            float best_a = 1e30f, best_b = 1e30f;
+            for (int it = 0; it < 4 && !rc; it++) {
+                if ((e = hipDeviceSynchronize()) != hipSuccess) { fail(e, __LINE__, "pcie probe sync"); break; }
+                const auto t0 = std::chrono::steady_clock::now();
+                for (int k = 0; k < chunks; k++) {
+                    if (mode != 1) (void)hipMemcpyAsync(dA + k * ch, hA + k * ch, ch, hipMemcpyHostToDevice, c->s_in);
+                    if (mode != 0) (void)hipMemcpyAsync(hB + k * ch, dB + k * ch, ch, hipMemcpyDeviceToHost, c->s_out);
+                }
+                if (mode != 1) (void)hipEventRecord(ea, c->s_in);
+                if (mode != 0) (void)hipEventRecord(eb, c->s_out);
+                if (mode != 1) (void)hipEventSynchronize(ea);
+                const float ta = std::chrono::duration<float>(std::chrono::steady_clock::now() - t0).count();
+                if (mode != 0) (void)hipEventSynchronize(eb);
+                const float tb = std::chrono::duration<float>(std::chrono::steady_clock::now() - t0).count();
+                if ((e = hipGetLastError()) != hipSuccess) { fail(e, __LINE__, "pcie probe copies"); break; }
+                if (it == 0) continue;  // warm-up
+                if (ta < best_a) best_a = ta;
+                if (tb < best_b) best_b = tb;
+            }
+            if (mode == 0) out[0] = tot / (double)best_a / 1e9;
+            if (mode == 1) out[1] = tot / (double)best_b / 1e9;
+            if (mode == 2) {
+                out[2] = tot / (double)best_a / 1e9;
+                out[3] = tot / (double)best_b / 1e9;
+            }
+        }
+        (void)hipEventDestroy(ea);
+        (void)hipEventDestroy(eb);
+    }
+    if (hA) (void)hipHostFree(hA);
+    if (hB) (void)hipHostFree(hB);
+    if (dA) (void)hipFree(dA);
+    if (dB) (void)hipFree(dB);
+    return rc;
 }
 
 int jfsx_ctx_metrics(jfsx_ctx *c, jfsx_metrics *out, int reset) {

@@ -94,7 +94,7 @@ struct ZDev {
 struct ZOut {
     uint64_t out_len;
     int32_t status;
-    int32_t fallback;  // zstd decompression: 1 when the serial decoder took the object
+    int32_t fallback;  // zstd decompression: why the serial decoder took the object (0: it did not)
 };
 
 struct BlkOut {        // written by finalize, copied back to the host
@@ -299,7 +299,7 @@ constexpr size_t kZstdScratch = kZstdHufOff + 8192;
 // Block-parallel decoding (jfsx_zstd2.h): zstd_par_waves(n, ncu) persistent
 // waves, each with a kZstdArena-byte arena (tables, literals, sequences);
 // waves = 0 selects the serial one-wave-per-object kernel (n x kZstdScratch).
-constexpr size_t kZstdArena = (size_t)64 * 9216 + ((size_t)4 << 20) + (size_t)12 * (512u << 10);
+constexpr size_t kZstdArena = (size_t)64 * 9216 + ((size_t)4 << 20) + ((size_t)1 << 18) + (size_t)12 * (768u << 10);
 constexpr int kZstdWavesPerCu = 8;
 int zstd_par_waves(int n, int ncu);
 void launch_zstd_decompress(hipStream_t s, int n, const ZDev *blks, ZOut *outs, uint8_t *scratch, int waves);

@@ -215,9 +215,11 @@ __global__ __launch_bounds__(64) void zstd_decompress_k(const ZDev *__restrict__
 }
 
 // Block-parallel decoding (jfsx_zstd2.h), persistent waves: wave w decodes
-// objects w, w + W, ... in its own arena of kZstdArena bytes; an object the
-// fast path does not take is decoded by jzd::decompress in the same wave
-// (scratch at the start of the arena), which sets the exact status.
+// objects w, w + W, ... in its own arena of kZstdArena bytes.  An object the
+// fast path does not take is marked (ZOut.fallback = why) and decoded by
+// zstd_fallback_k, the serial decoder in a second launch over the same waves
+// and arenas (scratch at the start of the arena), which sets the exact
+// status.  Two kernels keep the serial decoder's registers out of this one.
 __global__ __launch_bounds__(64) void zstd_decompress_par_k(const ZDev *__restrict__ blks, ZOut *__restrict__ outs,
                                                             uint8_t *__restrict__ arenas, int n) {
     __shared__ jzd2::Shared S;
@@ -229,15 +231,29 @@ __global__ __launch_bounds__(64) void zstd_decompress_par_k(const ZDev *__restri
         for (int k = 0; k < 8; k++) e.st[k] = 0;
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(e.last)::"memory");
 #endif
-        int64_t r = jzd2::decompress_par(e, S, arena, b.len, b.cap);
-        if (r == jzd2::kFallback) {
-            jzd2::wave_fence();
-            DevEnv e1{b.src, (int32_t)b.len, b.dst, arena, threadIdx.x, 0, 0xffffffffu, 0};
-            r = jzd::decompress(e1, S.t, b.len, b.cap);
-            if (threadIdx.x == 0) outs[i].fallback = 1;
-        } else if (threadIdx.x == 0) {
-            outs[i].fallback = 0;
+        const int32_t r = jzd2::decompress_par(e, S, arena, b.len, b.cap);
+#ifdef JFSX_ZSTD_STAMP
+        if (threadIdx.x == 0)
+            for (int k = 0; k < 8; k++) atomicAdd(&g_zstd_stamps[k], e.st[k]);
+#endif
+        if (threadIdx.x == 0) {
+            outs[i].out_len = r < 0 ? 0 : (uint64_t)r;
+            outs[i].status = r < 0 ? JFSX_EFORMAT : JFSX_OK;
+            outs[i].fallback = r <= jzd2::kFallback ? -r - 2 : 0;
         }
+        jzd2::wave_fence();
+    }
+}
+
+__global__ __launch_bounds__(64) void zstd_fallback_k(const ZDev *__restrict__ blks, ZOut *__restrict__ outs,
+                                                      uint8_t *__restrict__ arenas, int n) {
+    __shared__ jzd::Tables T;
+    uint8_t *arena = arenas + (size_t)blockIdx.x * jzd2::kArena;
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        if (!jzd2::uni((uint32_t)outs[i].fallback)) continue;
+        const ZDev b = blks[i];
+        DevEnv e{b.src, (int32_t)b.len, b.dst, arena, threadIdx.x, 0, 0xffffffffu, 0};
+        const int64_t r = jzd::decompress(e, T, b.len, b.cap);
         if (threadIdx.x == 0) {
             outs[i].out_len = r < 0 ? 0 : (uint64_t)r;
             outs[i].status = r >= 0 ? JFSX_OK : r == jzd::ZD_EDSTSIZE ? JFSX_EDSTSIZE : JFSX_EFORMAT;
@@ -250,9 +266,10 @@ int zstd_par_waves(int n, int ncu) { return n < ncu * kZstdWavesPerCu ? n : ncu 
 
 void launch_zstd_decompress(hipStream_t s, int n, const ZDev *blks, ZOut *outs, uint8_t *scratch, int waves) {
     if (n <= 0) return;
-    if (waves > 0)
+    if (waves > 0) {
         hipLaunchKernelGGL(zstd_decompress_par_k, dim3(waves), dim3(64), 0, s, blks, outs, scratch, n);
-    else
+        hipLaunchKernelGGL(zstd_fallback_k, dim3(waves), dim3(64), 0, s, blks, outs, scratch, n);
+    } else
         hipLaunchKernelGGL(zstd_decompress_k, dim3(n), dim3(64), 0, s, blks, outs, scratch);
 }
 

@@ -31,15 +31,18 @@
 namespace jzd2 {
 using namespace jzd;
 
-constexpr int32_t kFallback = -3;
+// decompress_par results below 0: the object goes to the serial decoder; the
+// value says why (jfsx_zblk.reserved = -value - 2 after the batch)
+constexpr int32_t kFallback = -3;   // frame shape or header (scan)
+constexpr int32_t kFbHuf = -4, kFbSeq = -5, kFbExec = -6, kFbRaw = -7, kFbLast = -8, kFbFcs = -9, kFbSum = -10;
 constexpr uint32_t kMaxBlk = 64;                    // blocks per frame (8 MiB of full blocks)
 constexpr uint32_t kSlot = 9216;                   // per-block table slot in the arena
 constexpr uint32_t kSlotLL = 4096, kSlotML = 6144, kSlotOF = 8192;  // Huffman at 0 (2048 x u16)
 constexpr size_t kTabBytes = (size_t)kMaxBlk * kSlot;               // 576 KiB
-constexpr size_t kLitCap = (size_t)4 << 20;                         // literal bytes per object
-constexpr uint32_t kSeqCap = 512u << 10;                            // sequences per object
+constexpr size_t kLitCap = ((size_t)4 << 20) + ((size_t)1 << 18);    // literal bytes per object (4 MiB blocks + table rounding)
+constexpr uint32_t kSeqCap = 768u << 10;                            // sequences per object (4 MiB of 5-byte matches)
 constexpr size_t kLitOff = kTabBytes, kLLMLOff = kLitOff + kLitCap, kOffOff = kLLMLOff + 8ull * kSeqCap;
-constexpr size_t kArena = kOffOff + 4ull * kSeqCap;                 // 10.6 MiB per wave
+constexpr size_t kArena = kOffOff + 4ull * kSeqCap;                 // 13.8 MiB per wave
 static_assert(kArena == jfsx::kZstdArena, "arena size");
 constexpr uint32_t kSym = 0x80000000u;  // symbolic offset: kSym | rep index << 29 | d
 
@@ -60,8 +63,15 @@ struct BDesc {
     uint32_t fin[3];    // repeat offsets on exit, symbolic in rep[] (phase 2)
 };
 
+// output ring of the execution phase: output position p at ring slot
+// (p + (dst mod 16)) mod kRing, so flushes are aligned 16-byte stores
+constexpr uint32_t kRing = 8192, kRingMask = kRing - 1, kWinMax = 4096;
+
 struct Shared {
-    Tables t;
+    union {
+        Tables t;                                   // scan: table building
+        __attribute__((aligned(16))) uint8_t ring[kRing];  // execution: recent output
+    };
     BDesc d[kMaxBlk];
     uint8_t smap[4 * kMaxBlk];  // Huffman stream -> block | stream index << 6
     uint8_t qmap[kMaxBlk];      // sequence stream -> block
@@ -190,7 +200,7 @@ __device__ __forceinline__ void put_table(uint8_t *slot, const void *lds, uint32
 // phase 1: frame and block headers, tables into arena slots
 // ---------------------------------------------------------------------------
 template <class Env>
-__device__ int32_t scan_block(Env &e, Shared &S, Mode &m, uint8_t *arena, BDesc &D, uint32_t bi, int32_t p,
+__device__ __forceinline__ int32_t scan_block(Env &e, Shared &S, Mode &m, uint8_t *arena, BDesc &D, uint32_t bi, int32_t p,
                               int32_t n, uint32_t &litTotal, uint32_t &seqTotal, uint16_t (&slots)[4]) {
     Tables &t = S.t;
     if (n >= (int32_t)kBlockMax || n < 3) return kFallback;
@@ -348,7 +358,7 @@ __device__ int32_t scan_block(Env &e, Shared &S, Mode &m, uint8_t *arena, BDesc 
 }
 
 template <class Env>
-__device__ int32_t scan(Env &e, Shared &S, uint8_t *arena, uint32_t insize, Frame &F) {
+__device__ __forceinline__ int32_t scan(Env &e, Shared &S, uint8_t *arena, uint32_t insize, Frame &F) {
     const int32_t n = (int32_t)insize;
     int32_t p = 0;
     if (n < 9) return kFallback;
@@ -581,22 +591,57 @@ __device__ __forceinline__ void lane_match(uint8_t *dst, uint32_t o, uint32_t of
     }
 }
 
+// Execution state: output below F is in dst (and fenced), output in
+// [max(V, W - kRing), W) is in the ring; W = output written so far.
+struct Out {
+    uint8_t *ring;
+    uint8_t *dst;
+    uint32_t a;  // dst mod 16
+    uint32_t F, V, W;
+    __device__ __forceinline__ uint32_t slot(uint32_t p) const { return (p + a) & kRingMask; }
+    // ring -> dst for [F, end): head bytes, 16-byte units, tail bytes when `all`
+    __device__ __forceinline__ void flush(uint32_t lane, bool all) {
+        const uint32_t end = all ? W : ((W + a) & ~15u) - a;
+        if (!all && (W + a) < 16u) return;
+        if (end <= F) return;
+        uint32_t h = ((F + a + 15u) & ~15u) - a;
+        if (h > end) h = end;
+        if (lane < h - F) *(gu8 *)(dst + F + lane) = ring[slot(F + lane)];
+        const uint32_t e16 = ((end + a) & ~15u) - a;
+        if (e16 > h) {
+            for (uint32_t j = 16 * lane; j < e16 - h; j += 1024) {
+                const uint4 v = *(const uint4 *)(ring + slot(h + j));
+                jfsx::gst16(dst + h + j, v);
+            }
+            h = e16;
+        }
+        if (lane < end - h) *(gu8 *)(dst + h + lane) = ring[slot(h + lane)];
+        F = end;
+        wave_fence();
+    }
+    // a byte of earlier output (q < W): ring or dst
+    __device__ __forceinline__ uint32_t rd(uint32_t q, uint32_t lim) const {
+        return q >= lim ? (uint32_t)ring[slot(q)] : (uint32_t) * (gcu8 *)(dst + q);
+    }
+};
+
 // ---------------------------------------------------------------------------
 // the fast path: decoded size, or kFallback
 // ---------------------------------------------------------------------------
 template <class Env>
-__device__ int32_t decompress_par(Env &e, Shared &S, uint8_t *arena, uint32_t insize, uint32_t cap) {
+__device__ __forceinline__ int32_t decompress_par(Env &e, Shared &S, uint8_t *arena, uint32_t insize, uint32_t cap) {
     const uint32_t lane = e.lane;
     Frame F;
     if (scan(e, S, arena, insize, F) < 0) return kFallback;
     wave_fence();  // arena tables and LDS descriptors before the lanes read them
+    e.stamp(0);    // (-DJFSX_ZSTD_STAMP builds: cycles per phase)
     const uint8_t *src = e.src;
     const int32_t n = (int32_t)insize;
     uint8_t *lit = arena + kLitOff;
     uint64_t *llml = (uint64_t *)(arena + kLLMLOff);
     uint32_t *offs = (uint32_t *)(arena + kOffOff);
     // ---- Huffman streams, one per lane ----
-    bool bad = false;
+    bool bad = false, badq = false;
     for (uint32_t g0 = 0; g0 < F.nstreams; g0 += 64) {
         const uint32_t g = g0 + lane;
         if (g < F.nstreams) {
@@ -610,6 +655,7 @@ __device__ int32_t decompress_par(Env &e, Shared &S, uint8_t *arena, uint32_t in
                 bad = true;
         }
     }
+    e.stamp(1);
     // ---- sequence streams, one block per lane ----
     for (uint32_t g0 = 0; g0 < F.nseqblk; g0 += 64) {
         const uint32_t g = g0 + lane;
@@ -620,14 +666,16 @@ __device__ int32_t decompress_par(Env &e, Shared &S, uint8_t *arena, uint32_t in
             if (!seq_lane(src, n, arena + (size_t)D.llSlot * kSlot + kSlotLL, arena + (size_t)D.mlSlot * kSlot + kSlotML,
                           arena + (size_t)D.ofSlot * kSlot + kSlotOF, D.llLog, D.mlLog, D.ofLog, D.seqIn, D.seqLen,
                           D.nbSeq, llml + D.seqBase, offs + D.seqBase, fin))
-                bad = true;
+                badq = true;
             D.fin[0] = fin[0];
             D.fin[1] = fin[1];
             D.fin[2] = fin[2];
         }
     }
-    if (__ballot(bad)) return kFallback;
+    if (__ballot(bad)) return kFbHuf;
+    if (__ballot(badq)) return kFbSeq;
     wave_fence();  // literals and sequences before the execution reads them
+    e.stamp(2);
     // ---- repeat offsets chained over the blocks ----
     {
         uint32_t r0 = 1, r1 = 4, r2 = 8;
@@ -647,15 +695,21 @@ __device__ int32_t decompress_par(Env &e, Shared &S, uint8_t *arena, uint32_t in
             }
         }
     }
+    e.stamp(3);
     // ---- execution in frame order ----
+    // Windows of up to kWinMax output bytes go through the LDS ring (a wave's
+    // LDS accesses are ordered, so lanes read what earlier lanes and rounds
+    // wrote without fences; flushed in aligned 16-byte stores); larger windows,
+    // raw and RLE blocks write dst directly after a full flush.
+    Out O{S.ring, e.dst, (uint32_t)((uintptr_t)e.dst & 15), 0, 0, 0};
     uint8_t *dst = e.dst;
-    uint32_t o = 0;
     for (uint32_t bi = 0; bi < F.nblk; bi++) {
         const BDesc &D = S.d[bi];
         const uint32_t type = uni(D.type);
         if (type != 2) {
-            const uint32_t sz = uni(D.size);
-            if (sz > cap - o) return kFallback;
+            const uint32_t sz = uni(D.size), o = O.W;
+            if (sz > cap - o) return kFbRaw;
+            O.flush(lane, true);
             const int32_t in = (int32_t)uni((uint32_t)D.in);
             if (type == 0) {
                 for (uint32_t j = lane; j < sz; j += 64) *(gu8 *)(dst + o + j) = *(gcu8 *)(src + in + (int32_t)j);
@@ -663,8 +717,8 @@ __device__ int32_t decompress_par(Env &e, Shared &S, uint8_t *arena, uint32_t in
                 const uint32_t by = lin8(src, n, in);
                 for (uint32_t j = lane; j < sz; j += 64) *(gu8 *)(dst + o + j) = (uint8_t)by;
             }
-            o += sz;
             wave_fence();
+            O.W = O.F = O.V = o + sz;
             continue;
         }
         const uint32_t litSize = uni(D.litSize), ltype = uni(D.ltype), nbSeq = uni(D.nbSeq), sb = uni(D.seqBase);
@@ -673,7 +727,7 @@ __device__ int32_t decompress_par(Env &e, Shared &S, uint8_t *arena, uint32_t in
         const uint8_t *lsrc = ltype == 0 ? src + (int32_t)litSrc : lit + litOff;
         uint32_t lp = 0;
         for (uint32_t w = 0; w < nbSeq; w += 64) {
-            const uint32_t k = w + lane;
+            const uint32_t k = w + lane, o = O.W;
             const bool valid = k < nbSeq;
             uint32_t ll = 0, ml = 0, off = 0;
             if (valid) {
@@ -688,42 +742,88 @@ __device__ int32_t decompress_par(Env &e, Shared &S, uint8_t *arena, uint32_t in
             const uint64_t oj = (uint64_t)o + xo, lj = (uint64_t)lp + xl;
             const bool err = valid && ((uint64_t)ll + ml > (uint64_t)cap - oj || (uint64_t)ll > (uint64_t)litSize - lj ||
                                        (uint64_t)off > oj + ll);
-            if (__ballot(err)) return kFallback;
-            // literal runs
-            if (valid && ll) {
-                if (ltype == 1) lane_fill(dst + oj, litSrc, ll);
-                else lane_copy(dst + oj, lsrc + lj, ll);
-            }
-            wave_fence();
-            // matches in rounds
+            if (__ballot(err)) return kFbExec;
             bool done = !valid || ml == 0;
             const uint32_t mo = (uint32_t)oj + ll, ms = mo - off, need = ms + (off < ml ? off : ml);
-            for (;;) {
-                const uint64_t pend = __ballot(!done);
-                if (!pend) break;
-                const int f = __builtin_ctzll(pend);
-                const uint32_t D0 = __shfl(mo, f, 64);
-                if (!done && need <= D0) {
-                    lane_match(dst, mo, off, ml);
-                    done = true;
+            if (tall <= kWinMax) {
+                // ring path: the window's slots must not hold unflushed output
+                if (o - O.F >= kWinMax) O.flush(lane, false);
+                const uint32_t lim = O.V > o + tall - kRing ? O.V : o + tall - kRing;
+                if (valid) {
+                    uint32_t t = 0;
+                    if (ltype == 1) {
+                        for (; t < ll; t++) O.ring[O.slot((uint32_t)oj + t)] = (uint8_t)litSrc;
+                    } else {
+                        const uint8_t *ls = lsrc + lj;
+                        for (; t + 4 <= ll; t += 4) {
+                            const uint32_t b0 = *(gcu8 *)(ls + t), b1 = *(gcu8 *)(ls + t + 1),
+                                           b2 = *(gcu8 *)(ls + t + 2), b3 = *(gcu8 *)(ls + t + 3);
+                            O.ring[O.slot((uint32_t)oj + t)] = (uint8_t)b0;
+                            O.ring[O.slot((uint32_t)oj + t + 1)] = (uint8_t)b1;
+                            O.ring[O.slot((uint32_t)oj + t + 2)] = (uint8_t)b2;
+                            O.ring[O.slot((uint32_t)oj + t + 3)] = (uint8_t)b3;
+                        }
+                        for (; t < ll; t++) O.ring[O.slot((uint32_t)oj + t)] = *(gcu8 *)(ls + t);
+                    }
+                }
+                for (;;) {
+                    const uint64_t pend = __ballot(!done);
+                    if (!pend) break;
+                    const uint32_t D0 = __shfl(mo, __builtin_ctzll(pend), 64);
+                    if (!done && need <= D0) {
+                        // ms + t reaches this lane's own bytes when off < ml:
+                        // written before they are read (LDS order)
+                        for (uint32_t t = 0; t < ml; t++) O.ring[O.slot(mo + t)] = (uint8_t)O.rd(ms + t, lim);
+                        done = true;
+                    }
+                }
+            } else {
+                // a window larger than half the ring: straight to dst
+                O.flush(lane, true);
+                if (valid && ll) {
+                    if (ltype == 1) lane_fill(dst + oj, litSrc, ll);
+                    else lane_copy(dst + oj, lsrc + lj, ll);
                 }
                 wave_fence();
+                for (;;) {
+                    const uint64_t pend = __ballot(!done);
+                    if (!pend) break;
+                    const uint32_t D0 = __shfl(mo, __builtin_ctzll(pend), 64);
+                    if (!done && need <= D0) {
+                        lane_match(dst, mo, off, ml);
+                        done = true;
+                    }
+                    wave_fence();
+                }
+                O.F = O.V = o + tall;
             }
-            o += tall;
+            O.W = o + tall;
             lp += tll;
         }
-        const uint32_t last = litSize - lp;
-        if (last > cap - o) return kFallback;
-        if (ltype == 1) {
-            for (uint32_t j = lane; j < last; j += 64) *(gu8 *)(dst + o + j) = (uint8_t)litSrc;
+        const uint32_t last = litSize - lp, o = O.W;
+        if (last > cap - o) return kFbLast;
+        if (last <= kWinMax) {
+            if (o - O.F >= kWinMax) O.flush(lane, false);
+            for (uint32_t j = lane; j < last; j += 64)
+                O.ring[O.slot(o + j)] = ltype == 1 ? (uint8_t)litSrc : *(gcu8 *)(lsrc + lp + j);
         } else {
-            for (uint32_t j = lane; j < last; j += 64) *(gu8 *)(dst + o + j) = *(gcu8 *)(lsrc + lp + j);
+            O.flush(lane, true);
+            if (ltype == 1) {
+                for (uint32_t j = lane; j < last; j += 64) *(gu8 *)(dst + o + j) = (uint8_t)litSrc;
+            } else {
+                for (uint32_t j = lane; j < last; j += 64) *(gu8 *)(dst + o + j) = *(gcu8 *)(lsrc + lp + j);
+            }
+            wave_fence();
+            O.F = O.V = o + last;
         }
-        o += last;
-        wave_fence();
+        O.W = o + last;
     }
-    if (F.hasFcs && (uint64_t)o != F.fcs) return kFallback;
-    if (F.checksum && (uint32_t)xxh64(e, 0, o) != F.want) return kFallback;
+    O.flush(lane, true);
+    const uint32_t o = O.W;
+    e.stamp(4);
+    if (F.hasFcs && (uint64_t)o != F.fcs) return kFbFcs;
+    if (F.checksum && (uint32_t)xxh64(e, 0, o) != F.want) return kFbSum;
+    e.stamp(5);
     return (int32_t)o;
 }
 

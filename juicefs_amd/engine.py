@@ -43,7 +43,7 @@ EXPORTS = [
     "jfsx_agg_lz4_compress", "jfsx_agg_lz4_decompress", "jfsx_mctx_lz4_compress_batch", "jfsx_mctx_lz4_decompress_batch",
     "jfsx_zstd_decompress_batch", "jfsx_agg_zstd_decompress", "jfsx_mctx_zstd_decompress_batch",
     "jfsx_last_error", "jfsx_zstd_bound", "jfsx_zstd_compress_batch", "jfsx_agg_zstd_compress",
-    "jfsx_mctx_zstd_compress_batch", "jfsx_ctx_metrics",
+    "jfsx_mctx_zstd_compress_batch", "jfsx_ctx_metrics", "jfsx_pcie_probe",
 ]
 
 
@@ -139,6 +139,7 @@ def load_library(path=LIB_PATH):
             "jfsx_ctx_set_slot_bytes": (I, [P, U64]),
             "jfsx_ctx_kernel_time": (I, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64), I]),
             "jfsx_ctx_metrics": (I, [P, ctypes.POINTER(jfsx_metrics), I]),
+            "jfsx_pcie_probe": (I, [P, U64, ctypes.POINTER(ctypes.c_double)]),
             "jfsx_alloc_pinned": (I, [P, SZ, PP]),
             "jfsx_free_pinned": (I, [P, P]),
             "jfsx_alloc_device": (I, [P, SZ, PP]),
@@ -364,6 +365,13 @@ class Engine:
         self.L.jfsx_ctx_kernel_time(self.ctx, ctypes.byref(ms), ctypes.byref(n), 1 if reset else 0)
         return ms.value, n.value
 
+    def pcie_probe(self, nbytes=1 << 30):
+        """jfsx_pcie_probe: GB/s H2D alone, D2H alone, and each while both run."""
+        out = (ctypes.c_double * 4)()
+        self._check(self.L.jfsx_pcie_probe(self.ctx, nbytes, out), "jfsx_pcie_probe")
+        return {"h2d": round(out[0], 2), "d2h": round(out[1], 2), "duplex_h2d": round(out[2], 2),
+                "duplex_d2h": round(out[3], 2)}
+
     def metrics(self, reset=False):
         """jfsx_ctx_metrics as a dict (counters since open or the last reset)."""
         m = jfsx_metrics()
@@ -454,6 +462,8 @@ class Engine:
         arr, n = self.make_zblocks((s.ctypes.data, s.size, d.ctypes.data, int(c))
                                    for s, d, c in zip(srcs, dsts, caps))
         self.zstd_decompress_batch(arr, n, MEM_HOST)
+        # why each object went to the serial decoder (0: it did not; jfsx.h)
+        self.zstd_serial_reasons = [arr[i].reserved for i in range(len(dsts))]
         return [(arr[i].status, d[:arr[i].out_len].tobytes()) for i, d in enumerate(dsts)]
 
     # -- asynchronous batches (jfsx_*_async + jfsx_wait) ------------------

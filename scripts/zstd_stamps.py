@@ -11,6 +11,8 @@ from juicefs_amd import engine as E  # noqa: E402
 from tests import zstd_lib  # noqa: E402
 
 names = ["literals", "seq headers", "ml/ll/states", "seq execute", "block start/raw", "table reads", "offset", "-"]
+if os.environ.get("JFSX_ZSTD_SERIAL") != "1":  # block-parallel kernel: phases of jfsx_zstd2.h
+    names = ["scan+tables", "huffman lanes", "sequence lanes", "rep chain", "execute", "checksum", "-", "-"]
 nb, L = int(sys.argv[1]) if len(sys.argv) > 1 else 256, 4 << 20
 eng = E.Engine(0)
 lib = E._lib

@@ -213,19 +213,21 @@ def test_block_parallel_decoder_takes_level1_frames(eng):
     """The block-parallel decoder (jfsx_zstd2.h) takes every one-frame object
     of up to 64 blocks without handing it to the serial decoder, across data
     kinds, sizes, levels and content checksums; the bytes equal the input."""
-    srcs, frames = [], []
+    srcs, frames, what = [], [], []
     for kind in lz4_data.KINDS:
         for n in (9, 4096, 131071, 131072, 131073, 1 << 20, (4 << 20) + 17):
             for level, ck in ((1, False), (1, True), (3, False), (9, False)):
                 src = lz4_data.sample(kind, n, seed=7 * n + level)
                 srcs.append(src)
                 frames.append(zstd_lib.compress(src, level, ck))
+                what.append((kind, n, level, ck))
     eng.metrics(reset=True)
     got = eng.zstd_decompress(frames, [len(s) for s in srcs])
     m = eng.metrics()
     for i, (src, (st, d)) in enumerate(zip(srcs, got)):
         assert st == E.OK and d == src, i
-    assert m["zstdd_blocks"] == len(frames) and m["zstd_serial"] == 0
+    serial = [(w, r) for w, r in zip(what, eng.zstd_serial_reasons) if r]
+    assert m["zstdd_blocks"] == len(frames) and m["zstd_serial"] == 0, serial
     assert m["zstdd_out"] == sum(len(s) for s in srcs)
 
 
