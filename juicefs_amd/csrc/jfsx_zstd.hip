@@ -180,10 +180,13 @@ struct DevEnv {
 __device__ unsigned long long g_zstd_stamps[8];  // diagnostic build: cycles per decoder section
 }  // namespace jfsx
 extern "C" int jfsx_debug_zstd_stamps(unsigned long long *out, int reset) {
+    // out[0..7]: cycles per section; out[8..11]: jzd2 counters (ZSTAT)
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(jfsx::g_zstd_stamps), 64) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out + 8, HIP_SYMBOL(jzd2::g_zstd_counts), 32) != hipSuccess) return -1;
     if (reset) {
         unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(jfsx::g_zstd_stamps), z, 64) != hipSuccess) return -1;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(jzd2::g_zstd_counts), z, 32) != hipSuccess) return -1;
     }
     return 0;
 }

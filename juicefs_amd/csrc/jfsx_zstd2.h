@@ -46,6 +46,15 @@ constexpr size_t kArena = kOffOff + 4ull * kSeqCap;                 // 13.8 MiB 
 static_assert(kArena == jfsx::kZstdArena, "arena size");
 constexpr uint32_t kSym = 0x80000000u;  // symbolic offset: kSym | rep index << 29 | d
 
+// diagnostic counters of -DJFSX_ZSTD_STAMP builds: 0 windows, 1 match rounds,
+// 2 far matches fetched before the rounds, 3 sequence output bytes
+#ifdef JFSX_ZSTD_STAMP
+__device__ unsigned long long g_zstd_counts[4];
+#define ZSTAT(k, v) atomicAdd(&g_zstd_counts[k], (unsigned long long)(v))
+#else
+#define ZSTAT(k, v) ((void)0)
+#endif
+
 struct BDesc {
     uint8_t type, ltype, nstreams, hlog;  // type 0 raw, 1 RLE, 2 compressed; ltype as the literal block type
     uint8_t llLog, mlLog, ofLog, pad;
@@ -66,16 +75,24 @@ struct BDesc {
 // output ring of the execution phase: output position p at ring slot
 // (p + (dst mod 16)) mod kRing, so flushes are aligned 16-byte stores
 constexpr uint32_t kRing = 8192, kRingMask = kRing - 1, kWinMax = 4096;
+constexpr uint32_t kWinBytes = 1024;  // byte-parallel windows: 64 lanes x 16 output bytes
+constexpr uint16_t kDone = 0xffff;
 
 struct Shared {
     union {
-        Tables t;                                   // scan: table building
-        __attribute__((aligned(16))) uint8_t ring[kRing];  // execution: recent output
+        Tables t;  // scan: table building
+        struct {   // execution: recent output, and the byte-parallel window
+            __attribute__((aligned(16))) uint8_t ring[kRing];
+            uint16_t ptr[kWinBytes];  // window byte -> earlier window byte it copies, or kDone
+        };
     };
+    uint4 seqtab[65];  // byte-parallel window: per sequence (start, match start, offset, literal index)
     BDesc d[kMaxBlk];
     uint8_t smap[4 * kMaxBlk];  // Huffman stream -> block | stream index << 6
     uint8_t qmap[kMaxBlk];      // sequence stream -> block
 };
+
+static_assert(sizeof(Tables) >= kRing + 2 * kWinBytes, "ring and pointers overlay the tables");
 
 struct Frame {
     uint32_t nblk, nstreams, nseqblk;
@@ -560,6 +577,18 @@ __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t lane, uin
     return x - v;
 }
 
+// number of lanes i with v_i <= x, for v non-decreasing over the 64 lanes
+__device__ __forceinline__ uint32_t wave_count_le(uint32_t v, uint32_t x) {
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t step = 64; step >= 1; step >>= 1) {
+        const uint32_t idx = c + step - 1;
+        const uint32_t y = __shfl(v, (int)(idx & 63u), 64);
+        if (idx < 64 && y <= x) c += step;
+    }
+    return c;
+}
+
 __device__ __forceinline__ void lane_copy(uint8_t *d, const uint8_t *s, uint32_t cnt) {
     uint32_t t = 0;
     for (; t + 4 <= cnt; t += 4) {
@@ -695,7 +724,7 @@ __device__ __forceinline__ int32_t decompress_par(Env &e, Shared &S, uint8_t *ar
             }
         }
     }
-    e.stamp(3);
+    e.stamp(2);
     // ---- execution in frame order ----
     // Windows of up to kWinMax output bytes go through the LDS ring (a wave's
     // LDS accesses are ordered, so lanes read what earlier lanes and rounds
@@ -745,10 +774,92 @@ __device__ __forceinline__ int32_t decompress_par(Env &e, Shared &S, uint8_t *ar
             if (__ballot(err)) return kFbExec;
             bool done = !valid || ml == 0;
             const uint32_t mo = (uint32_t)oj + ll, ms = mo - off, need = ms + (off < ml ? off : ml);
-            if (tall <= kWinMax) {
+            // the lanes this match waits for: those whose match part
+            // [mo_i, oend_i) overlaps its source [ms, need) (sources of
+            // overlapping copies come from the first period, [ms, mo))
+            uint64_t dep = 0;
+            {
+                const uint32_t oend = (uint32_t)oj + ll + ml;  // non-decreasing (invalid lanes: the window end)
+                const uint32_t ks = wave_count_le(oend, ms);     // lanes ending at or before ms
+                const uint32_t ke1 = wave_count_le((uint32_t)oj, need - 1);  // lanes starting before need
+                const uint32_t mks = __shfl(mo, (int)(ks & 63u), 64), mke = __shfl(mo, (int)((ke1 - 1) & 63u), 64);
+                if (!done && need > o && ke1 > 0) {
+                    const uint32_t s0 = need > mks ? ks : ks + 1, e0 = need > mke ? ke1 - 1 : ke1 - 2;
+                    if ((int32_t)s0 <= (int32_t)e0 && e0 < 64)
+                        dep = (e0 - s0 == 63 ? ~0ull : ((1ull << (e0 - s0 + 1)) - 1)) << s0;
+                }
+            }
+            ZSTAT(0, lane == 0 ? 1 : 0);
+            ZSTAT(3, valid ? ll + ml : 0);
+            e.stamp(3);
+            if (tall <= kWinBytes) {
+                // byte-parallel window: lane L owns window bytes [16L, 16L + 16)
+                if (o - O.F >= kWinMax) O.flush(lane, false);
+                const uint32_t old = o + tall > kRing ? o + tall - kRing : 0u;
+                const uint32_t lim = O.V > old ? O.V : old;
+                S.seqtab[lane] = make_uint4((uint32_t)oj - o, mo - o, off, (uint32_t)lj);
+                if (lane == 0) S.seqtab[64] = make_uint4(tall, tall, 0, 0);
+                const uint32_t r0 = 16 * lane;
+                uint32_t j = wave_count_le((uint32_t)oj - o, r0);
+                j = j ? j - 1 : 0;
+                uint4 sq = S.seqtab[j];
+                uint32_t nxt = S.seqtab[j + 1].x;
+                uint32_t pend = 0;  // bytes of this lane still copying a window byte
+                uint32_t val[16];
+#pragma unroll
+                for (uint32_t i = 0; i < 16; i++) {
+                    const uint32_t r = r0 + i;
+                    val[i] = 0;
+                    if (r < tall) {
+                        while (r >= nxt) {
+                            j++;
+                            sq = S.seqtab[j];
+                            nxt = S.seqtab[j + 1].x;
+                        }
+                        if (r < sq.y) {  // literal byte
+                            val[i] = ltype == 1 ? litSrc : (uint32_t) * (gcu8 *)(lsrc + sq.w + (r - sq.x));
+                            S.ptr[r] = kDone;
+                        } else {
+                            const uint32_t q = o + r - sq.z;  // the byte it copies
+                            if (q < o) {
+                                val[i] = O.rd(q, lim);
+                                S.ptr[r] = kDone;
+                            } else {
+                                S.ptr[r] = (uint16_t)(q - o);
+                                pend |= 1u << i;
+                            }
+                        }
+                    }
+                }
+#pragma unroll
+                for (uint32_t i = 0; i < 16; i++)
+                    if (r0 + i < tall && !(pend >> i & 1)) O.ring[O.slot(o + r0 + i)] = (uint8_t)val[i];
+                // pointer jumping: a byte whose source is final takes its
+                // value (ring written before the kDone mark), else follows
+                // the source's pointer; chains halve every pass
+                while (__ballot(pend != 0)) {
+                    ZSTAT(1, lane == 0 ? 1 : 0);
+#pragma unroll
+                    for (uint32_t i = 0; i < 16; i++) {
+                        if (pend >> i & 1) {
+                            const uint32_t r = r0 + i, q = S.ptr[r], pq = S.ptr[q];
+                            if (pq == kDone) {
+                                O.ring[O.slot(o + r)] = O.ring[O.slot(o + q)];
+                                S.ptr[r] = kDone;
+                                pend &= ~(1u << i);
+                            } else {
+                                S.ptr[r] = (uint16_t)pq;
+                            }
+                        }
+                    }
+                }
+                e.stamp(7);
+            } else if (tall <= kWinMax) {
                 // ring path: the window's slots must not hold unflushed output
                 if (o - O.F >= kWinMax) O.flush(lane, false);
-                const uint32_t lim = O.V > o + tall - kRing ? O.V : o + tall - kRing;
+                // sources at or above lim are in the ring, below it in dst
+                const uint32_t old = o + tall > kRing ? o + tall - kRing : 0u;
+                const uint32_t lim = O.V > old ? O.V : old;
                 if (valid) {
                     uint32_t t = 0;
                     if (ltype == 1) {
@@ -766,17 +877,51 @@ __device__ __forceinline__ int32_t decompress_par(Env &e, Shared &S, uint8_t *ar
                         for (; t < ll; t++) O.ring[O.slot((uint32_t)oj + t)] = *(gcu8 *)(ls + t);
                     }
                 }
+                // far matches (source wholly in dst, below lim): no
+                // dependency inside the window, so their bytes are loaded
+                // now, with the literals, as aligned dwords
+                const bool farm = !done && ml <= 32 && off >= ml && ms + ml <= lim;
+                uint32_t fw[8];
+                if (farm) {
+                    const uintptr_t a0 = (uintptr_t)(dst + ms), al = a0 & ~(uintptr_t)3, aend = a0 + ml;
+                    const uint32_t sh = (uint32_t)(a0 & 3);
+                    uint32_t dw[9];
+#pragma unroll
+                    for (uint32_t k = 0; k < 9; k++) dw[k] = al + 4 * k < aend ? *(gcu32 *)(al + 4 * k) : 0u;
+#pragma unroll
+                    for (uint32_t m = 0; m < 8; m++) fw[m] = __builtin_amdgcn_alignbyte(dw[m + 1], dw[m], sh);
+                }
+                e.stamp(6);
                 for (;;) {
                     const uint64_t pend = __ballot(!done);
                     if (!pend) break;
-                    const uint32_t D0 = __shfl(mo, __builtin_ctzll(pend), 64);
-                    if (!done && need <= D0) {
-                        // ms + t reaches this lane's own bytes when off < ml:
-                        // written before they are read (LDS order)
-                        for (uint32_t t = 0; t < ml; t++) O.ring[O.slot(mo + t)] = (uint8_t)O.rd(ms + t, lim);
+                    ZSTAT(1, lane == 0 ? 1 : 0);
+                    if (!done && (dep & pend) == 0) {
+                        ZSTAT(2, farm ? 1 : 0);
+                        if (farm) {
+#pragma unroll
+                            for (uint32_t t = 0; t < 32; t++)
+                                if (t < ml) O.ring[O.slot(mo + t)] = (uint8_t)(fw[t >> 2] >> (8 * (t & 3)));
+                        } else if (off >= 4) {
+                            // 4 source bytes per round trip: ms + t + 3 < mo + t
+                            for (uint32_t t = 0; t < ml; t += 4) {
+                                const uint32_t b0 = O.rd(ms + t, lim), b1 = t + 1 < ml ? O.rd(ms + t + 1, lim) : 0u,
+                                               b2 = t + 2 < ml ? O.rd(ms + t + 2, lim) : 0u,
+                                               b3 = t + 3 < ml ? O.rd(ms + t + 3, lim) : 0u;
+                                O.ring[O.slot(mo + t)] = (uint8_t)b0;
+                                if (t + 1 < ml) O.ring[O.slot(mo + t + 1)] = (uint8_t)b1;
+                                if (t + 2 < ml) O.ring[O.slot(mo + t + 2)] = (uint8_t)b2;
+                                if (t + 3 < ml) O.ring[O.slot(mo + t + 3)] = (uint8_t)b3;
+                            }
+                        } else {
+                            // ms + t reaches this lane's own bytes: written
+                            // before they are read (LDS order)
+                            for (uint32_t t = 0; t < ml; t++) O.ring[O.slot(mo + t)] = (uint8_t)O.rd(ms + t, lim);
+                        }
                         done = true;
                     }
                 }
+                e.stamp(7);
             } else {
                 // a window larger than half the ring: straight to dst
                 O.flush(lane, true);
@@ -788,8 +933,7 @@ __device__ __forceinline__ int32_t decompress_par(Env &e, Shared &S, uint8_t *ar
                 for (;;) {
                     const uint64_t pend = __ballot(!done);
                     if (!pend) break;
-                    const uint32_t D0 = __shfl(mo, __builtin_ctzll(pend), 64);
-                    if (!done && need <= D0) {
+                    if (!done && (dep & pend) == 0) {
                         lane_match(dst, mo, off, ml);
                         done = true;
                     }

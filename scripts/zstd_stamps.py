@@ -12,7 +12,8 @@ from tests import zstd_lib  # noqa: E402
 
 names = ["literals", "seq headers", "ml/ll/states", "seq execute", "block start/raw", "table reads", "offset", "-"]
 if os.environ.get("JFSX_ZSTD_SERIAL") != "1":  # block-parallel kernel: phases of jfsx_zstd2.h
-    names = ["scan+tables", "huffman lanes", "sequence lanes", "rep chain", "execute", "checksum", "-", "-"]
+    names = ["scan+tables", "huffman lanes", "sequence lanes+chain", "exec: seq loads/scans",
+             "exec: flush/tails/raw", "checksum", "exec: literals", "exec: match rounds"]
 nb, L = int(sys.argv[1]) if len(sys.argv) > 1 else 256, 4 << 20
 eng = E.Engine(0)
 lib = E._lib
@@ -22,12 +23,15 @@ blocks = [pool[(b * 2654435761) % (pool.size - L):][:L].tobytes() for b in range
 frames = [zstd_lib.compress(b, 1) for b in blocks]
 got = eng.zstd_decompress([frames[i % 16] for i in range(nb)], [L] * nb)
 assert all(st == E.OK for st, _ in got)
-out = (ctypes.c_ulonglong * 8)()
+out = (ctypes.c_ulonglong * 12)()
 lib.jfsx_debug_zstd_stamps(out, 1)
 eng.zstd_decompress([frames[i % 16] for i in range(nb)], [L] * nb)
 lib.jfsx_debug_zstd_stamps(out, 1)
 tot = sum(out[k] for k in range(8))
 print("cycles per frame (per wave) %.3e" % (tot / nb))
-for k in range(7):
-    print("%-16s %5.1f %%" % (names[k], 100.0 * out[k] / tot))
+for k in range(8):
+    print("%-22s %5.1f %%" % (names[k], 100.0 * out[k] / tot))
+if os.environ.get("JFSX_ZSTD_SERIAL") != "1":
+    print("per frame: windows %.0f, match rounds %.0f (%.2f per window), far-match lanes %.0f, sequence bytes %.0f"
+          % (out[8] / nb, out[9] / nb, out[9] / max(out[8], 1), out[10] / nb, out[11] / nb))
 eng.close()
