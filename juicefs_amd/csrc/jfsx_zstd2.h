@@ -77,6 +77,7 @@ struct BDesc {
 constexpr uint32_t kRing = 8192, kRingMask = kRing - 1, kWinMax = 4096;
 constexpr uint32_t kWinBytes = 1024;  // byte-parallel windows: 64 lanes x 16 output bytes
 constexpr uint16_t kDone = 0xffff;
+constexpr uint32_t kLitStage = 512;  // literal bytes a byte-parallel window stages in LDS
 
 struct Shared {
     union {
@@ -87,6 +88,7 @@ struct Shared {
         };
     };
     uint4 seqtab[65];  // byte-parallel window: per sequence (start, match start, offset, literal index)
+    uint32_t litst[kLitStage / 4 + 1];  // byte-parallel window: its literal bytes (from an aligned dword)
     BDesc d[kMaxBlk];
     uint8_t smap[4 * kMaxBlk];  // Huffman stream -> block | stream index << 6
     uint8_t qmap[kMaxBlk];      // sequence stream -> block
@@ -566,14 +568,19 @@ __device__ __forceinline__ bool seq_lane(const uint8_t *src, int32_t insize, con
 // ---------------------------------------------------------------------------
 // phase 4 helpers: per-lane byte copies
 // ---------------------------------------------------------------------------
+// wave64 prefix sum with DPP (VALU latency, no LDS round trips): row_shr
+// 1 / 2 / 4 / 8 scan each row of 16 lanes, row_bcast:15 and row_bcast:31 carry
+// the row totals (GFX9 DPP)
 __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t lane, uint32_t &total) {
     uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= (uint32_t)d) x += y;
-    }
-    total = __shfl(x, 63, 64);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+    (void)lane;
     return x - v;
 }
 
@@ -755,15 +762,25 @@ __device__ __forceinline__ int32_t decompress_par(Env &e, Shared &S, uint8_t *ar
         const uint32_t r0 = uni(D.rep[0]), r1 = uni(D.rep[1]), r2 = uni(D.rep[2]);
         const uint8_t *lsrc = ltype == 0 ? src + (int32_t)litSrc : lit + litOff;
         uint32_t lp = 0;
+        // the next step's sequences are loaded while this one executes
+        uint64_t nv = 0;
+        uint32_t noff = 0;
+        if (lane < nbSeq) {
+            nv = *(__attribute__((address_space(1))) const uint64_t *)(llml + sb + lane);
+            noff = *(__attribute__((address_space(1))) const uint32_t *)(offs + sb + lane);
+        }
         for (uint32_t w = 0; w < nbSeq; w += 64) {
             const uint32_t k = w + lane, o = O.W;
             const bool valid = k < nbSeq;
             uint32_t ll = 0, ml = 0, off = 0;
             if (valid) {
-                const uint64_t v = *(__attribute__((address_space(1))) const uint64_t *)(llml + sb + k);
-                ll = (uint32_t)v;
-                ml = (uint32_t)(v >> 32);
-                off = resolve(*(__attribute__((address_space(1))) const uint32_t *)(offs + sb + k), r0, r1, r2);
+                ll = (uint32_t)nv;
+                ml = (uint32_t)(nv >> 32);
+                off = resolve(noff, r0, r1, r2);
+            }
+            if (k + 64 < nbSeq) {
+                nv = *(__attribute__((address_space(1))) const uint64_t *)(llml + sb + k + 64);
+                noff = *(__attribute__((address_space(1))) const uint32_t *)(offs + sb + k + 64);
             }
             uint32_t tll, tall;
             const uint32_t xl = wave_excl_sum(ll, lane, tll);
@@ -778,7 +795,7 @@ __device__ __forceinline__ int32_t decompress_par(Env &e, Shared &S, uint8_t *ar
             // [mo_i, oend_i) overlaps its source [ms, need) (sources of
             // overlapping copies come from the first period, [ms, mo))
             uint64_t dep = 0;
-            {
+            if (tall > kWinBytes) {
                 const uint32_t oend = (uint32_t)oj + ll + ml;  // non-decreasing (invalid lanes: the window end)
                 const uint32_t ks = wave_count_le(oend, ms);     // lanes ending at or before ms
                 const uint32_t ke1 = wave_count_le((uint32_t)oj, need - 1);  // lanes starting before need
@@ -797,8 +814,17 @@ __device__ __forceinline__ int32_t decompress_par(Env &e, Shared &S, uint8_t *ar
                 if (o - O.F >= kWinMax) O.flush(lane, false);
                 const uint32_t old = o + tall > kRing ? o + tall - kRing : 0u;
                 const uint32_t lim = O.V > old ? O.V : old;
-                S.seqtab[lane] = make_uint4((uint32_t)oj - o, mo - o, off, (uint32_t)lj);
+                S.seqtab[lane] = make_uint4((uint32_t)oj - o, mo - o, off, (uint32_t)lj - lp);
                 if (lane == 0) S.seqtab[64] = make_uint4(tall, tall, 0, 0);
+                // the step's literal bytes [lp, lp + tll): aligned dwords into LDS
+                const bool stage = ltype != 1 && tll + 3 <= kLitStage;
+                const uint32_t lsh = (uint32_t)((uintptr_t)(lsrc + lp) & 3);
+                if (stage) {
+                    const uintptr_t la = (uintptr_t)(lsrc + lp) - lsh;
+                    const uint32_t nd = (lsh + tll + 3) >> 2;
+                    for (uint32_t d = lane; d < nd; d += 64) S.litst[d] = *(gcu32 *)(la + 4 * d);
+                }
+                const uint8_t *lstage = (const uint8_t *)S.litst + lsh;
                 const uint32_t r0 = 16 * lane;
                 uint32_t j = wave_count_le((uint32_t)oj - o, r0);
                 j = j ? j - 1 : 0;
@@ -817,7 +843,9 @@ __device__ __forceinline__ int32_t decompress_par(Env &e, Shared &S, uint8_t *ar
                             nxt = S.seqtab[j + 1].x;
                         }
                         if (r < sq.y) {  // literal byte
-                            val[i] = ltype == 1 ? litSrc : (uint32_t) * (gcu8 *)(lsrc + sq.w + (r - sq.x));
+                            val[i] = ltype == 1 ? litSrc
+                                     : stage    ? (uint32_t)lstage[sq.w + (r - sq.x)]
+                                                : (uint32_t) * (gcu8 *)(lsrc + lp + sq.w + (r - sq.x));
                             S.ptr[r] = kDone;
                         } else {
                             const uint32_t q = o + r - sq.z;  // the byte it copies

@@ -33,7 +33,8 @@ run agg_gcm_t20 --mode agg --threads 20 --steps 5 --warmup 1 && run agg_gcm_t32 
 run aggcodec_lz4 --mode aggcodec --codec lz4 --threads 20 --steps 2 --warmup 1 && \
 run aggcodec_unlz4 --mode aggcodec --codec unlz4 --threads 20 --steps 2 --warmup 1 && \
 run aggcodec_zstd --mode aggcodec --codec zstd --threads 20 --steps 2 --warmup 1 && \
-run aggcodec_unzstd --mode aggcodec --codec unzstd --threads 20 --steps 2 --warmup 1 || exit 1
+run aggcodec_unzstd --mode aggcodec --codec unzstd --threads 20 --steps 2 --warmup 1 && \
+run unzstd_text_64g --mode unzstd --steps 5 --warmup 1 || exit 1
 fi
 if [ $what = prof ] || [ $what = all ]; then
 prof gcm --steps 10 --warmup 2 && prof gcm_ragged --ragged --steps 10 --warmup 2 && \
