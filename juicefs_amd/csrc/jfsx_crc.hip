@@ -36,6 +36,16 @@ namespace jfsx {
 // the 40 of the 16-B-per-lane rows (A' = S1024(A) ^ U(piece)).  Tables
 // t = 16..19 in LDS are then the 4096-B shift; the guarded path (ragged
 // segment ends) keeps 1 KiB rows and takes its 1024-B shift from global memory.
+// JFSX_CRC_BYTE = 1: slice-by-4 byte tables U12..U15 replicated once per bank
+// (table entry stride 256 B, two tables interleaved per 64 KiB: address =
+// byte << 8 | 4 * (lane mod 32) | region << 16, one v_perm each) -- 16
+// conflict-free lookups and about 28 VALU per 16 B instead of 34 and ~60,
+// at 144 KiB of LDS (one 16-wave workgroup per CU).  A lane's 64-B chunk is a
+// chain of 16 slice-by-4 steps; two spans' chains run interleaved, and the
+// 4096-B span shift keeps its nibble tables (region 2).
+#ifndef JFSX_CRC_BYTE
+#define JFSX_CRC_BYTE 0
+#endif
 #ifndef JFSX_CRC_SPAN
 #define JFSX_CRC_SPAN 64
 #endif
@@ -44,7 +54,11 @@ constexpr uint32_t kCrcWaves = 16;
 #define JFSX_CRC_PF 4
 #endif
 constexpr int kCrcPf = JFSX_CRC_PF;  // rows of 16 B per lane in flight
+#if JFSX_CRC_BYTE
+constexpr uint32_t kCrcLds = 0x24000;  // 147456 B: byte tables 128 KiB + shift nibble tables 16 KiB
+#else
 constexpr uint32_t kCrcLds = 20 * 4096;  // 81920 B
+#endif
 
 #define NIB(t, h, xm, k)                                                                                          \
     lds_u32(lds, __builtin_amdgcn_perm((xm), lb, ((t) >= 16 ? 0x0c020000u : 0x0c0c0000u) | ((4u + (k)) << 8)) + \
@@ -77,12 +91,47 @@ __device__ __forceinline__ uint32_t crc_u16_nib(const char *lds, uint32_t lb, ui
 #undef X3
 }
 
+#if JFSX_CRC_BYTE
+// byte k of x through U(12 + k): region k >> 1 (lb byte 2 = 1), half k & 1
+#define BYT(x, k)                                                                                              \
+    lds_u32(lds, __builtin_amdgcn_perm((x), lb, 0x0c000000u | ((k) >= 2 ? 0x00020000u : 0x000c0000u) |        \
+                                                    ((4u + (k)) << 8)) +                                       \
+                     ((k)&1) * 128u)
+// 4096-B shift nibble tables in region 2 (lb byte 3 = 2)
+#define NIBS(t, h, xm) lds_u32(lds, __builtin_amdgcn_perm((xm), lb, 0x0c030000u | ((4u + (t)) << 8)) + ((t)*4096u + (h)*128u))
+#define X3(a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), 0x96)
+// one slice-by-4 step: crc_raw of the 4 bytes of x (= state ^ word)
+__device__ __forceinline__ uint32_t crc_step4(const char *lds, uint32_t lb, uint32_t x) {
+    return X3(BYT(x, 0), BYT(x, 1), BYT(x, 2)) ^ BYT(x, 3);
+}
+// crc_raw of the 4 bytes of x, XORed with w
+__device__ __forceinline__ uint32_t crc_step4x(const char *lds, uint32_t lb, uint32_t x, uint32_t w) {
+    return X3(X3(BYT(x, 0), BYT(x, 1), BYT(x, 2)), BYT(x, 3), w);
+}
+__device__ __forceinline__ uint32_t crc_shift4096(const char *lds, uint32_t lb, uint32_t A) {
+    const uint32_t xl = A & 0x0f0f0f0fu, xh = (A >> 4) & 0x0f0f0f0fu;
+    return X3(X3(NIBS(0, 0, xl), NIBS(0, 1, xh), NIBS(1, 0, xl)), X3(NIBS(1, 1, xh), NIBS(2, 0, xl), NIBS(2, 1, xh)),
+              NIBS(3, 0, xl) ^ NIBS(3, 1, xh));
+}
+#undef X3
+__device__ __forceinline__ uint32_t crc_u16_byte(const char *lds, uint32_t lb, uint4 p) {
+    uint32_t c = crc_step4(lds, lb, p.x);
+    c = crc_step4(lds, lb, c ^ p.y);
+    c = crc_step4(lds, lb, c ^ p.z);
+    return crc_step4(lds, lb, c ^ p.w);
+}
+#endif
+
 // the guarded path's row step with the 1024-B shift from global byte tables
 __device__ __forceinline__ uint32_t crc_row_g(const char *lds, const uint32_t *__restrict__ T, uint32_t lb, uint32_t A,
                                               uint4 p) {
     const uint32_t s = T[24 * 256 + (A & 0xffu)] ^ T[25 * 256 + ((A >> 8) & 0xffu)] ^
                        T[26 * 256 + ((A >> 16) & 0xffu)] ^ T[27 * 256 + (A >> 24)];
+#if JFSX_CRC_BYTE
+    return crc_u16_byte(lds, lb, p) ^ s;
+#else
     return crc_u16_nib(lds, lb, p.x, p.y, p.z, p.w) ^ s;
+#endif
 }
 
 // ragged tails (segment length not a multiple of 16 B: the last segment of an
@@ -99,7 +148,7 @@ __device__ __noinline__ uint32_t crc_partial_g(const uint32_t *__restrict__ T, u
 }
 
 #ifndef JFSX_CRC_WPE
-#define JFSX_CRC_WPE 8
+#define JFSX_CRC_WPE (JFSX_CRC_BYTE ? 4 : 8)
 #endif
 __global__ __launch_bounds__(kCrcWaves * 64) __attribute__((amdgpu_waves_per_eu(JFSX_CRC_WPE))) void crc_segments_k(const Task *__restrict__ tasks,
                                                                 const BlkDev *__restrict__ blks, DevTables tab) {
@@ -107,6 +156,25 @@ __global__ __launch_bounds__(kCrcWaves * 64) __attribute__((amdgpu_waves_per_eu(
     const Task task = tasks[blockIdx.x];
     const BlkDev blk = blks[task.blk];
     const uint32_t tid = threadIdx.x;
+#if JFSX_CRC_BYTE
+    // stage: byte tables U12..U15, i = (table t, entry e, replica quad rq)
+    for (uint32_t i = tid; i < 4 * 256 * 8; i += kCrcWaves * 64) {
+        const uint32_t rq = i & 7, e = (i >> 3) & 255, t = i >> 11;
+        const uint32_t v = tab.crc[(12 + t) * 256 + e];
+        *reinterpret_cast<uint4 *>(lds + (t >> 1) * 0x10000u + e * 256 + (t & 1) * 128 + 16 * rq) =
+            make_uint4(v, v, v, v);
+    }
+    // the 4096-B shift as nibble tables in region 2: i = (table t, hi, nibble, rq)
+    for (uint32_t i = tid; i < 4 * 2 * 16 * 8; i += kCrcWaves * 64) {
+        const uint32_t rq = i & 7, nib = (i >> 3) & 15, hi = (i >> 7) & 1, t = i >> 8;
+        const uint32_t v = tab.crc[(28 + t) * 256 + (hi ? nib << 4 : nib)];
+        *reinterpret_cast<uint4 *>(lds + 0x20000u + t * 4096 + nib * 256 + hi * 128 + 16 * rq) =
+            make_uint4(v, v, v, v);
+    }
+    __syncthreads();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const uint32_t lb = ((lane & 31) << 2) | 0x10000u | 0x2000000u;
+#else
     // stage: i = (table t, hi, nibble, replica quad rq)
     for (uint32_t i = tid; i < 640 * 8; i += kCrcWaves * 64) {
         const uint32_t rq = i & 7, nib = (i >> 3) & 15, hi = (i >> 7) & 1, t = i >> 8;
@@ -116,12 +184,50 @@ __global__ __launch_bounds__(kCrcWaves * 64) __attribute__((amdgpu_waves_per_eu(
     __syncthreads();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const uint32_t lb = ((lane & 31) << 2) | 0x10000u;
+#endif
     const uint8_t *src = blk.src;
     for (uint64_t seg0 = task.c0 + (uint64_t)wave * kSeg; seg0 < task.c1; seg0 += (uint64_t)kCrcWaves * kSeg) {
         const uint64_t seg1 = seg0 + kSeg < task.c1 ? seg0 + kSeg : task.c1;
         uint32_t A = 0, lend = 0;
         const uint64_t nrows = (seg1 - seg0 + 1023) / 1024;
-        if (JFSX_CRC_SPAN >= 64 && seg1 - seg0 == (uint64_t)kSeg) {
+        if (JFSX_CRC_BYTE && seg1 - seg0 == (uint64_t)kSeg) {
+#if JFSX_CRC_BYTE
+            // full segment, 64-B lane chunks of the 8 spans of 4 KiB; spans
+            // r and r + 1 are two independent slice-by-4 chains, and the next
+            // pair's 128 B per lane are in flight meanwhile
+            const uint8_t *q = src + seg0 + 64 * lane;
+            uint4 c0b[4], c1b[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) c0b[j] = gld16(q + 16 * j), c1b[j] = gld16(q + 4096 + 16 * j);
+#pragma unroll
+            for (int r = 0; r < 8; r += 2) {
+                uint4 n0[4], n1[4];
+                if (r + 2 < 8) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        n0[j] = gld16(q + 4096 * (r + 2) + 16 * j), n1[j] = gld16(q + 4096 * (r + 3) + 16 * j);
+                }
+                // x = state ^ next word; each step folds the next word into
+                // its 4-way XOR (two v_bitop3)
+                uint32_t x0 = c0b[0].x, x1 = c1b[0].x;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    x0 = crc_step4x(lds, lb, x0, c0b[j].y), x1 = crc_step4x(lds, lb, x1, c1b[j].y);
+                    x0 = crc_step4x(lds, lb, x0, c0b[j].z), x1 = crc_step4x(lds, lb, x1, c1b[j].z);
+                    x0 = crc_step4x(lds, lb, x0, c0b[j].w), x1 = crc_step4x(lds, lb, x1, c1b[j].w);
+                    if (j < 3)
+                        x0 = crc_step4x(lds, lb, x0, c0b[j + 1].x), x1 = crc_step4x(lds, lb, x1, c1b[j + 1].x);
+                }
+                A = crc_step4x(lds, lb, x0, crc_shift4096(lds, lb, A));
+                A = crc_step4x(lds, lb, x1, crc_shift4096(lds, lb, A));
+                if (r + 2 < 8) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) c0b[j] = n0[j], c1b[j] = n1[j];
+                }
+            }
+            lend = kSeg;
+#endif
+        } else if (!JFSX_CRC_BYTE && JFSX_CRC_SPAN >= 64 && seg1 - seg0 == (uint64_t)kSeg) {
             // full segment: spans of 64 x SPAN bytes, lane chunk SPAN bytes
             // (P pieces); each piece's load for the next span is issued as
             // soon as the piece is consumed

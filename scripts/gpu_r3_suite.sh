@@ -2,7 +2,7 @@
 # with its same-run CPU baseline; rocprofv3 kernel stats at the bench lines'
 # own configs; PMC passes named pmc_<variant>__<set> for scripts/pmc_r3.py
 # (FETCH/WRITE at the bench size, SQ busy counters on a 4 GiB batch).
-# usage: bash scripts/gpu_r3_suite.sh <tag> [lines1|lines2|prof|pmc1|pmc2|all]
+# usage: bash scripts/gpu_r3_suite.sh <tag> [lines1|lines2|prof|pmc1|pmc1a|pmc1b|pmc2|all]
 set -u
 cd "$GRAFT_REPO_ROOT"
 out=gpurun_out/suite_$1
@@ -43,18 +43,14 @@ prof cp --algo chacha20poly1305 --steps 10 --warmup 2 && prof crc --mode crc --s
 prof zstd_text --mode zstd $Z --steps 3 --warmup 1 && prof unzstd_text --mode unzstd $Z --steps 10 --warmup 2 && \
 prof lz4_text --mode lz4 $Z --steps 10 --warmup 2 && prof unlz4_text --mode unlz4 $Z --steps 10 --warmup 2 || exit 1
 fi
-if [ $what = pmc1 ] || [ $what = all ]; then
-for v in "seal_gcm:" "open_gcm:--mode open" "seal_chacha:--algo chacha20poly1305" \
-         "open_chacha:--mode open --algo chacha20poly1305" "crc_verify:--mode crc" \
-         "seal_gcm_ragged:--ragged" "open_gcm_ragged:--ragged --mode open" \
-         "seal_chacha_ragged:--ragged --algo chacha20poly1305" \
-         "open_chacha_ragged:--ragged --mode open --algo chacha20poly1305" \
-         "ingest_gcm:--mem host --blocks 2048" "zstd_text:--mode zstd $Z" "unzstd_text:--mode unzstd $Z" \
-         "lz4_text:--mode lz4 $Z" "unlz4_text:--mode unlz4 $Z"; do
+P1A='"seal_gcm:" "open_gcm:--mode open" "seal_chacha:--algo chacha20poly1305" "open_chacha:--mode open --algo chacha20poly1305" "crc_verify:--mode crc" "seal_gcm_ragged:--ragged" "open_gcm_ragged:--ragged --mode open"'
+P1B='"seal_chacha_ragged:--ragged --algo chacha20poly1305" "open_chacha_ragged:--ragged --mode open --algo chacha20poly1305" "ingest_gcm:--mem host --blocks 2048" "zstd_text:--mode zstd $Z" "unzstd_text:--mode unzstd $Z" "lz4_text:--mode lz4 $Z" "unlz4_text:--mode unlz4 $Z"'
+case $what in pmc1) P1="$P1A $P1B";; pmc1a) P1=$P1A;; pmc1b) P1=$P1B;; all) P1="$P1A $P1B";; *) P1="";; esac
+eval "set -- $P1"
+for v in "$@"; do
   name=${v%%:*}; a=${v#*:}
   pmc ${name}__fetch FETCH_SIZE $a && pmc ${name}__write WRITE_SIZE $a || exit 1
 done
-fi
 if [ $what = pmc2 ] || [ $what = all ]; then
 for v in "seal_gcm:" "open_gcm:--mode open" "seal_chacha:--algo chacha20poly1305" "crc_verify:--mode crc" \
          "seal_gcm_bitslice:--aes bitslice"; do
