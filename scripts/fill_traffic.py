@@ -1,0 +1,49 @@
+"""Fill `roofline.traffic` / `binding` of suite bench lines that ran before
+profiles/r3/pmc_r3.json existed, with bench.py's own formula (pmc_traffic):
+traffic = HBM bytes per plaintext byte of the variant's PMC passes x this
+line's plaintext bytes per launch.  The variant is the line's file name
+(bench_<variant>.json, the names scripts/gpu_r3_suite.sh gives both).  A
+filled line says so in roofline.traffic_filled_by.
+
+usage: python3 scripts/fill_traffic.py profiles/r3/pmc_r3.json profiles/r3/bench_*.json
+"""
+import json
+import os
+import sys
+
+
+def main(pmc_path, paths):
+    variants = json.load(open(pmc_path))["variants"]
+    for p in paths:
+        lines = open(p).read().splitlines()
+        idx = max((i for i, l in enumerate(lines) if l.startswith("{")), default=None)
+        if idx is None:
+            continue
+        d = json.loads(lines[idx])
+        key = os.path.basename(p)[len("bench_"):-len(".json")]
+        v = variants.get(key)
+        rf = d.get("roofline") or {}
+        plain = rf.get("plain_bytes_per_launch")
+        if v is None or not plain:
+            continue
+        changed = False
+        if rf.get("traffic") is None and "bytes_per_plain_byte" in v:
+            rf["traffic"] = int(v["bytes_per_plain_byte"] * plain)
+            rf["traffic_source"] = "profiles/r3/pmc_r3.json %s (%s; %s)" % (key, v.get("fetch_pass"),
+                                                                            v.get("write_pass"))
+            changed = True
+        if rf.get("binding") is None and ("lds_busy" in v or "valu_issue" in v):
+            b = {k: v[k] for k in ("lds_busy", "valu_issue", "lds_conflict_share") if k in v}
+            b["source"] = "profiles/r3/pmc_r3.json %s (%s)" % (key, v.get("lds_pass") or v.get("valu_pass"))
+            rf["binding"] = b
+            changed = True
+        if changed:
+            rf["traffic_filled_by"] = "scripts/fill_traffic.py (PMC passes ran after this line)"
+            d["roofline"] = rf
+            lines[idx] = json.dumps(d)
+            open(p, "w").write("\n".join(lines) + "\n")
+            print("filled", p)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2:])
