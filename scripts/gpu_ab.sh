@@ -12,7 +12,7 @@ for spec in "$@"; do
   JFSX_LIB=$lib timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py -x -q -m gpu --timeout 120 --timeout-method thread > $out/$name.pytest.log 2>&1 && grep -q passed $out/$name.pytest.log && ! grep -q skipped $out/$name.pytest.log || { echo "$name parity FAILED"; tail -5 $out/$name.pytest.log; exit 1; }
   echo "$name parity: $(tail -1 $out/$name.pytest.log)"
 done
-for rep in 1 2 3; do
+for rep in ${AB_REPS:-1 2 3}; do
   for spec in "$@"; do
     name=${spec%%=*}; v=${spec#*=}
     lib=juicefs_amd/_build/libjfsx_$v.so; [ "$v" = default ] && lib=juicefs_amd/libjfsx.so
