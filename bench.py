@@ -343,21 +343,23 @@ def main():
                "host_us_per_unwrap_1thread": round(host_s * 1e6, 1),
                "host_sample": "%d libcrypto RSA-OAEP decrypts, 1 thread" % len(sample)}
         eng.rsa_key_free(dkey)
+    full = None
+    if args.verify and args.mode in ("seal", "open", "crc") and (args.crc == "full" or args.mode != "seal"):
+        # every block's tag and CRC array against the oracle (host cores)
+        full = full_check(args, E, blks if args.mode != "crc" else None,
+                          crc.download(nb * 4 * nseg).reshape(nb, 4 * nseg), lens, base)
     if args.verify and args.mode == "seal":
+        # and the ciphertext bytes of a few blocks
         from oracle import oracle as orc
-        cs = None
         for b in range(0, nb, max(1, nb // args.verify))[:args.verify]:
             p = orc.gen_block(SEED, base + b, lens[b])
             key, nonce = orc.gen_key(SEED, base + b)
             c, tag = orc.seal(orc.AES256GCM if algo == E.AES256GCM else orc.CHACHA20P1305, key, nonce, p,
                               fast=algo == E.AES256GCM)
-            ok = bytes(blks[b].tag) == tag and dst.download(lens[b], offset=offs[b]).tobytes() == c
-            if args.crc == "full":
-                cs = orc.checksum(p, hw=True)
-                ok = ok and crc.download(len(cs), offset=4 * nseg * b).tobytes() == cs
-            if not ok:
+            if bytes(blks[b].tag) != tag or dst.download(lens[b], offset=offs[b]).tobytes() != c:
                 raise SystemExit("bench: block %d differs from the oracle" % b)
-            verified += 1
+    if full:
+        verified = nb
 
     total_plain = world * sum(lens) * args.steps
     value = total_plain / el / 1e9
@@ -401,6 +403,7 @@ def main():
                          "plain_bytes_per_launch": sum(lens), "binding": binding},
             "cpu_baseline": cpu,
             "verified_blocks": verified,
+            "full_check": full,
             **({"rsa_unwrap": rsa} if rsa else {}),
         }
         print(json.dumps(line), flush=True)
@@ -409,11 +412,51 @@ def main():
         dist.destroy_process_group()
 
 
-PMC_R3 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r3", "pmc_r3.json")
+def full_check(args, E, blks, got, lens, base):
+    """Every block of the batch against the oracle (checker only, after the
+    timed region): the tags of the sealed image (blks: the seal descriptors,
+    None for a CRC-only batch) and every block's checksum() array as the GPU
+    wrote it, byte for byte, against the oracle's own AEAD and CRC over the
+    same synthetic blocks on the host cores.  Exits non-zero on a difference;
+    returns what was compared, with a SHA-256 of each array."""
+    import hashlib
+    import numpy as np
+    from oracle import oracle as orc
+    threads, _ = host_cores()
+    nb, stride = got.shape
+    algo = orc.AES256GCM if args.algo == "aes256gcm" else orc.CHACHA20P1305
+    etags, ecrcs, secs = orc.expect_batch(algo, threads, lens, SEED, base, stride)
+    cl = np.array([4 * max(1, -(-int(x) // E.SEG)) for x in lens])
+    valid = np.arange(stride)[None, :] < cl[:, None]
+    bad_crc = np.nonzero(((got != ecrcs) & valid).any(axis=1))[0]
+    if bad_crc.size:
+        raise SystemExit("bench: block %d: CRC array differs from the oracle (%d blocks)" % (bad_crc[0], bad_crc.size))
+    out = {"blocks": nb, "crc_arrays_sha256": hashlib.sha256(np.where(valid, got, 0).tobytes()).hexdigest(),
+           "oracle_s": round(secs, 2), "oracle_threads": threads}
+    if blks is not None:
+        gt = np.frombuffer(b"".join(bytes(blks[i].tag) for i in range(nb)), np.uint8).reshape(nb, 16)
+        bad = np.nonzero((gt != etags).any(axis=1))[0]
+        if bad.size:
+            raise SystemExit("bench: block %d: tag differs from the oracle (%d blocks)" % (bad[0], bad.size))
+        out["tags_sha256"] = hashlib.sha256(gt.tobytes()).hexdigest()
+    out["what"] = ("%s of all %d blocks equal to the oracle's" %
+                   ("tags and CRC arrays" if blks is not None else "CRC arrays", nb))
+    return out
+
+
+PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
+# labelled PMC summaries (scripts/pmc_r3.py), newest first; the round-2 file
+# (FETCH / WRITE only, keyed by kernel) is the last resort for traffic
+PMC_FILES = ("r4/pmc_r4.json", "r3/pmc_r3.json")
+PMC_R2 = "r2/pmc_traffic.json"
+R2_KEYS = {"seal_gcm": "gcm_ttable", "open_gcm": "gcm_ttable", "seal_gcm_bitslice": "gcm_bitslice",
+           "seal_chacha": "chacha", "open_chacha": "chacha", "crc_verify": "crc_verify",
+           "seal_gcm_ragged": "gcm_ttable", "open_gcm_ragged": "gcm_ttable", "ingest_gcm": "gcm_ttable",
+           "seal_chacha_ragged": "chacha", "open_chacha_ragged": "chacha"}
 
 
 def pmc_variant(args):
-    """The key of this bench line in profiles/r3/pmc_r3.json."""
+    """The key of this bench line in the PMC summaries."""
     if args.mode == "crc":
         return "crc_verify"
     if args.mode in ("lz4", "unlz4", "zstd", "unzstd"):
@@ -429,28 +472,44 @@ def pmc_variant(args):
     return v + ("_ragged" if args.ragged else "")
 
 
+def _load(rel):
+    try:
+        return json.load(open(os.path.join(PROFILES, rel)))
+    except (OSError, ValueError):
+        return None
+
+
 def pmc_traffic(args, plain_per_launch):
     """(traffic, source, binding) of the dominant kernel from the committed
-    round-3 PMC passes (scripts/pmc_r3.py): traffic = HBM bytes per launch
-    (FETCH_SIZE / WRITE_SIZE of the same variant's 64 GiB pass, or its own
-    batch size where stated, corrected as the MI355X guide prescribes, per
-    plaintext byte x this launch's plaintext bytes); binding = the LDS and
-    VALU busy fractions of the same kernel (SQ counters, 4 GiB pass).  None
-    where no pass covers this variant."""
+    PMC passes: traffic = HBM bytes per launch (FETCH_SIZE / WRITE_SIZE of
+    the same variant, corrected as the MI355X guide prescribes, per plaintext
+    byte x this launch's plaintext bytes); binding = the LDS and VALU busy
+    fractions of the same kernel (SQ counters).  The newest summary holding
+    the variant wins (profiles/r4, then r3, then round 2's FETCH / WRITE
+    file); where none covers it, source names the gap instead of leaving a
+    silent null."""
     key = pmc_variant(args)
-    try:
-        v = json.load(open(PMC_R3))["variants"][key]
-    except (OSError, KeyError, ValueError, TypeError):
-        return None, None, None
-    if args.crc != "full" and args.mode == "seal":
-        return None, None, None
+    if key is None or (args.crc != "full" and args.mode == "seal"):
+        return None, "no PMC pass for this mode (%s)" % (key or args.mode), None
     traffic = src = binding = None
-    if "bytes_per_plain_byte" in v:
-        traffic = int(v["bytes_per_plain_byte"] * plain_per_launch)
-        src = "profiles/r3/pmc_r3.json %s (%s; %s)" % (key, v.get("fetch_pass"), v.get("write_pass"))
-    if "lds_busy" in v or "valu_issue" in v:
-        binding = {k: v[k] for k in ("lds_busy", "valu_issue", "lds_conflict_share") if k in v}
-        binding["source"] = "profiles/r3/pmc_r3.json %s (%s)" % (key, v.get("lds_pass") or v.get("valu_pass"))
+    for rel in PMC_FILES:
+        v = ((_load(rel) or {}).get("variants") or {}).get(key)
+        if not v:
+            continue
+        if traffic is None and "bytes_per_plain_byte" in v:
+            traffic = int(v["bytes_per_plain_byte"] * plain_per_launch)
+            src = "profiles/%s %s (%s; %s)" % (rel, key, v.get("fetch_pass"), v.get("write_pass"))
+        if binding is None and ("lds_busy" in v or "valu_issue" in v):
+            binding = {k: v[k] for k in ("lds_busy", "valu_issue", "lds_conflict_share") if k in v}
+            binding["source"] = "profiles/%s %s (%s)" % (rel, key, v.get("lds_pass") or v.get("valu_pass"))
+    if traffic is None and key in R2_KEYS:
+        k2 = ((_load(PMC_R2) or {}).get("kernels") or {}).get(R2_KEYS[key])
+        if k2:
+            traffic = int(k2["bytes_per_plain_byte"] * plain_per_launch)
+            src = "profiles/%s %s (64 GiB FETCH_SIZE / WRITE_SIZE passes, round 2)" % (PMC_R2, R2_KEYS[key])
+    if traffic is None:
+        src = "MISSING: no committed PMC pass covers variant %s (profiles/%s)" % (key, ", ".join(PMC_FILES))
+        print("bench: warning: " + src, file=sys.stderr)
     return traffic, src, binding
 
 
@@ -515,6 +574,11 @@ def host_ingest(args, world, rank, local, dist, eng):
             if bytes(blks[b].tag) != tag or got != c:
                 raise SystemExit("bench: block %d differs from the oracle" % b)
             verified += 1
+    full = None
+    if args.verify:
+        crcs = np.ctypeslib.as_array((ctypes.c_uint8 * (nb * 4 * nseg)).from_address(hcrc)).reshape(nb, 4 * nseg)
+        full = full_check(args, E, blks, crcs.copy(), [L] * nb, base)
+        verified = nb
     value = world * nb * L * args.steps / el / 1e9
     cpu = cpu_baseline(args, "seal") if rank == 0 and world == 1 and not args.no_cpu else None
     plain_launch = int(nb * L * args.steps / max(k_n, 1))
@@ -539,7 +603,7 @@ def host_ingest(args, world, rank, local, dist, eng):
                          "frac_of_one_way_d2h": round(value / pcie["d2h"], 4),
                          "pcie_measured": pcie, "kernel_avg_ms": round(k_ms / max(k_n, 1), 3),
                          "kernel_launches": k_n, "plain_bytes_per_launch": plain_launch, "binding": binding},
-            "cpu_baseline": cpu, "verified_blocks": verified}), flush=True)
+            "cpu_baseline": cpu, "verified_blocks": verified, "full_check": full}), flush=True)
     eng.free_pinned(hin)
     eng.free_pinned(hout)
     eng.free_pinned(hcrc)

@@ -203,6 +203,7 @@ struct jfsx_ctx {
     hipEvent_t ev_k0[kRing] = {}, ev_k1[kRing] = {};  // main-kernel timing per slot
     size_t slot_bytes = (size_t)256 << 20;
     int ncu = 256;  // compute units: persistent transform kernels launch one workgroup per CU
+    size_t zstd_arena_budget = 0;  // device bytes the block-parallel zstd decoder may hold (see run_codec)
     bool timing = false;
     bool bitslice = false;  // JFSX_CTX_BITSLICE
     char *rsa_d = nullptr;  // batched RSA unwrap: ct | halves | em | len (device, grow-only)
@@ -843,13 +844,24 @@ int run_codec(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, CodecOp op) {
     // zstd decompression: block-parallel persistent waves unless
     // JFSX_ZSTD_SERIAL=1 selects the one-wave-per-object serial kernel (A/B)
     static const bool zd_serial = getenv("JFSX_ZSTD_SERIAL") && atoi(getenv("JFSX_ZSTD_SERIAL")) == 1;
-    const int zd_waves = op == kZstdDecomp && !zd_serial ? zstd_par_waves(n, c->ncu) : 0;
+    // the block-parallel decoder's waves are capped by the context's arena
+    // budget (a 64-object batch needs 64 arenas, not 8 per CU); if the
+    // workspace cannot grow to that many, fewer waves are tried, then the
+    // serial kernel, whose scratch is n x kZstdScratch (128 KiB per object)
+    int zd_waves = op == kZstdDecomp && !zd_serial ? zstd_par_waves(n, c->ncu) : 0;
+    if (zd_waves) zd_waves = (int)std::min<size_t>((size_t)zd_waves, std::max<size_t>(c->zstd_arena_budget / kZstdArena, 1));
     const size_t o_out = align256(sizeof(ZDev) * n), o_tab = o_out + align256(sizeof(ZOut) * n);
-    size_t extra = 0;
-    if (op == kLz4Comp) extra = kLz4TabBytes * (size_t)n;
-    else if (op == kZstdDecomp) extra = zd_waves ? kZstdArena * (size_t)zd_waves : kZstdScratch * (size_t)n;
-    else if (op == kZstdComp) extra = 256 + kZstdcScratch * (size_t)zc_waves;  // per-wave scratch
-    if ((rc = ensure_dev(c, &w.d, &w.dcap, o_tab + extra))) return rc;
+    for (;;) {
+        size_t extra = 0;
+        if (op == kLz4Comp) extra = kLz4TabBytes * (size_t)n;
+        else if (op == kZstdDecomp) extra = zd_waves ? kZstdArena * (size_t)zd_waves : kZstdScratch * (size_t)n;
+        else if (op == kZstdComp) extra = 256 + kZstdcScratch * (size_t)zc_waves;  // per-wave scratch
+        rc = ensure_dev(c, &w.d, &w.dcap, o_tab + extra);
+        if (rc != JFSX_ENOMEM || op != kZstdDecomp || zd_waves == 0) break;
+        zd_waves = zd_waves > c->ncu ? std::max(zd_waves / 2, c->ncu) : 0;  // fewer waves, then serial
+        (void)hipGetLastError();  // the failed hipMalloc is not this batch's error
+    }
+    if (rc) return rc;
     if ((rc = ensure_host(&w.h, &w.hcap, o_tab))) return rc;  // descriptors and results only
     hipStream_t s = c->stream;
     ZDev *hz = (ZDev *)w.h;
@@ -961,6 +973,15 @@ int jfsx_ctx_open(int device, uint32_t flags, jfsx_ctx **out) {
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
         c->ncu = ncu;
+    {
+        // the block-parallel zstd decoder's arenas (kZstdArena per wave) may
+        // take at most an eighth of the device's memory (JFSX_ZSTD_ARENA_MB
+        // overrides): 8 waves per CU on a 256-CU, 288 GB part fit (28 GiB)
+        size_t total = 0;
+        (void)hipDeviceTotalMem(&total, device);
+        c->zstd_arena_budget = total ? total / 8 : (size_t)4 << 30;
+        if (const char *e = getenv("JFSX_ZSTD_ARENA_MB")) c->zstd_arena_budget = (size_t)atoll(e) << 20;
+    }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) != hipSuccess) {
@@ -1091,7 +1112,12 @@ int jfsx_pcie_probe(jfsx_ctx *c, uint64_t bytes, double out[4]) {
         for (int mode = 0; mode < 3 && !rc; mode++) {  // 0 H2D, 1 D2H, 2 both
             float best_a = 1e30f, best_b = 1e30f;
             for (int it = 0; it < 4 && !rc; it++) {
-                if ((e = hipDeviceSynchronize()) != hipSuccess) { fail(e, __LINE__, "pcie probe sync"); break; }
+                // the ring's own two streams only: other contexts' work on the
+                // device is not waited for (a diagnostic for an idle context)
+                if ((e = hipStreamSynchronize(c->s_in)) != hipSuccess || (e = hipStreamSynchronize(c->s_out)) != hipSuccess) {
+                    fail(e, __LINE__, "pcie probe sync");
+                    break;
+                }
                 const auto t0 = std::chrono::steady_clock::now();
                 for (int k = 0; k < chunks; k++) {
                     if (mode != 1) (void)hipMemcpyAsync(dA + k * ch, hA + k * ch, ch, hipMemcpyHostToDevice, c->s_in);

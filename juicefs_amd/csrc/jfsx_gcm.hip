@@ -22,6 +22,9 @@
 //   * gcm_finalize: one wave per block.  Lifts each wave partial by
 //     H^(blocks after that wave), XORs, adds E_K(J0)^len-block -> tag; in Open
 //     compares the tag; in VERIFY compares CRCs (first failing segment).
+#include <cstdio>
+#include <cstdlib>
+
 #include "jfsx_dev.h"
 
 #define JFSX_HD __device__ __forceinline__
@@ -432,11 +435,21 @@ __device__ __noinline__ Stream row_generic(char *lds, uint32_t loff, const GhLan
 // BS = 0: T-table AES in LDS, 16 waves (4/SIMD, <= 128 VGPRs).
 // BS = 1: whole 32 KiB segments use the bitsliced AES on the VALU
 //         (jfsx_aes_bs.h; 128 VGPRs of state), 8 waves (2/SIMD, <= 256 VGPRs).
+// BS = 2: hybrid, 8 waves of the BS = 1 shape: the last nbs waves run the
+//         bitsliced AES on whole segments at the front of the task, the other
+//         8 - nbs waves split the rest by rows with the T-table AES at a
+//         raised priority, so the LDS pipe the T-table waves feed and the VALU
+//         the bitsliced waves fill run at once (hyb below).
 template <int BS>
 struct GcmShape {
     static constexpr uint32_t waves = BS ? 8u : (uint32_t)kWaves;
     static constexpr uint32_t threads = waves * 64u;
 };
+// hybrid split (BS = 2), a kernel argument: bits 0..3 nbs (bitsliced waves),
+// bits 8..15 rho = 16 x (bitsliced wave rate / T-table wave rate), bits 16..17
+// the T-table waves' s_setprio level
+__device__ __forceinline__ uint32_t hyb_nbs(uint32_t h) { return h & 15u; }
+__device__ __forceinline__ uint32_t hyb_rho(uint32_t h) { return (h >> 8) & 255u; }
 
 #ifdef JFSX_ABLATE_TRACE
 // diagnostic build only (make variant V=TRACE): per workgroup start / end
@@ -451,7 +464,8 @@ template <bool OPEN, int CRCMODE, int NS, int BS>
 __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDev *__restrict__ blks,
                                          const GcmSched *__restrict__ sched, uint32_t *__restrict__ partial,
                                          uint32_t *__restrict__ pexp, const DevTables &tab, uint32_t tid,
-                                         uint32_t wave, uint32_t lane, uint32_t loff, const GhLane &gl, uint32_t xl) {
+                                         uint32_t wave, uint32_t lane, uint32_t loff, const GhLane &gl, uint32_t xl,
+                                         uint32_t hyb) {
 #ifdef JFSX_ABLATE_TRACE
     const uint64_t trace_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -501,6 +515,19 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
     // CRC from both waves' raw shares (crc_segment_end, task end below).  The
     // bitsliced kernel keys whole 32 KiB segments and keeps the segment split.
     constexpr bool kRowSplit = !BS && NS == 1;
+    // segments shared by two waves' row ranges (their CRC from raw shares)
+    constexpr bool kShares = kRowSplit || (BS == 2 && NS == 1);
+    // hybrid: waves [nt, 8) are bitsliced and take q whole segments each from
+    // the front of the task; waves [0, nt) row-split the rest
+    const uint32_t nbs = BS == 2 ? hyb_nbs(hyb) : 0u, nt = GcmShape<BS>::waves - nbs;
+    const bool isbs = BS == 1 || (BS == 2 && wave >= nt);
+    uint32_t q = 0;
+    if (BS == 2 && nbs) {
+        const uint32_t rho = hyb_rho(hyb), whole = (uint32_t)((c1 - c0) / kSeg);
+        q = nseg * rho / (nbs * rho + nt * 16u);
+        if (nbs * q > whole) q = whole / nbs;
+    }
+    const uint64_t tt0 = c0 + (uint64_t)nbs * q * kSeg;  // the T-table waves' region [tt0, c1)
     // in pairs of rows: every stream starts on an even row, as the two-row
     // loop's segment-end test assumes (only its second row can end a segment)
     const uint32_t npairs = (uint32_t)((c1 - c0 + 2047) / 2048);
@@ -508,7 +535,15 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
 #pragma unroll
     for (int s = 0; s < NS; s++) {
         const uint32_t v = wave * NS + s;
-        if (kRowSplit) {
+        if (BS == 2 && isbs) {
+            st[s].sub0 = c0 + (uint64_t)(wave - nt) * q * kSeg;
+            st[s].sub1 = st[s].sub0 + (uint64_t)q * kSeg;
+        } else if (BS == 2) {
+            const uint32_t np = (uint32_t)((c1 - tt0 + 2047) / 2048);
+            const uint32_t ra = 2 * (wave * np / nt), rb = 2 * ((wave + 1) * np / nt);
+            st[s].sub0 = tt0 + (uint64_t)ra * 1024;
+            st[s].sub1 = rb > ra ? (tt0 + (uint64_t)rb * 1024 < c1 ? tt0 + (uint64_t)rb * 1024 : c1) : st[s].sub0;
+        } else if (kRowSplit) {
             const uint32_t ra = 2 * (v * npairs / V), rb = 2 * ((v + 1) * npairs / V);
             st[s].sub0 = c0 + (uint64_t)ra * 1024;
             st[s].sub1 = rb > ra ? (c0 + (uint64_t)rb * 1024 < c1 ? c0 + (uint64_t)rb * 1024 : c1) : st[s].sub0;
@@ -547,7 +582,7 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
     // BS: whole 32 KiB segments take their 32 rows of keystream from one
     // bitsliced AES pass (lane slot k = row k), then the rows stream through
     // XOR / store / GHASH / CRC with the keystream in registers.
-    if (BS && NS == 1 && act[0] && rf >= 32) {
+    if (BS && isbs && NS == 1 && act[0] && rf >= 32) {
         const uint64_t nfs = rf / 32;
         const uint32_t nrk[3] = {sch->c012[0], sch->c012[1], sch->c012[2]};
         const uint32_t rk3 = sch->rk[3];
@@ -779,7 +814,7 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
     }
 #endif
     // ---- segments shared by two or more waves: sum the raw shares, finish ----
-    if (CRCMODE && kRowSplit) {
+    if (CRCMODE && kShares) {
         __syncthreads();
         if (wave == 0) {
             const uint32_t *raw = reinterpret_cast<const uint32_t *>(lds + kLdsSegRaw);
@@ -815,7 +850,7 @@ __global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *
                                                        const BlkDev *__restrict__ blks,
                                                        const GcmSched *__restrict__ sched,
                                                        uint32_t *__restrict__ partial, uint32_t *__restrict__ pexp,
-                                                       DevTables tab) {
+                                                       DevTables tab, uint32_t hyb) {
     __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
     __shared__ uint32_t s_task;
     const uint32_t tid = threadIdx.x;
@@ -833,6 +868,15 @@ __global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *
     const uint32_t loff = ((lane & 31) << 2) | 0x00010000u;  // AES replica offset | table base
     const GhLane gl = gh_lane(lane);
     const uint32_t xl = CRCMODE ? tab.crcx[lane] : 0u;
+    if (BS == 2 && wave < GcmShape<BS>::waves - hyb_nbs(hyb)) {
+        // the T-table waves win VALU arbitration against the bitsliced ones
+        switch ((hyb >> 16) & 3u) {
+            case 1: __builtin_amdgcn_s_setprio(1); break;
+            case 2: __builtin_amdgcn_s_setprio(2); break;
+            case 3: __builtin_amdgcn_s_setprio(3); break;
+            default: break;
+        }
+    }
     if (tid == 0) s_task = atomicAdd(queue, 1u);
     for (;;) {
         // also orders this task's table writes after the previous task's readers
@@ -842,7 +886,7 @@ __global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *
         __syncthreads();          // every wave holds ti: s_task may take the next index
         if (tid == 0) s_task = atomicAdd(queue, 1u);  // the next task's index arrives during this one
         gcm_task<OPEN, CRCMODE, NS, BS>(lds, tasks[ti], blks, sched, partial, pexp, tab, tid, wave, lane, loff, gl,
-                                        xl);
+                                        xl, hyb);
     }
 }
 
@@ -1027,14 +1071,25 @@ void launch_gcm_main(hipStream_t s, int ntasks, int ncu, uint32_t *queue, bool o
     if (ntasks <= 0) return;
     const unsigned grid = (unsigned)(ntasks < ncu ? ntasks : ncu);  // persistent: one workgroup per CU
     (void)hipMemsetAsync(queue, 0, 4, s);
+    // JFSX_GCM_HYBRID="nbs,rho,prio" selects the hybrid shape (BS = 2) for the
+    // T-table context (an A/B switch; see GcmShape)
+    static const uint32_t hyb = [] {
+        const char *e = getenv("JFSX_GCM_HYBRID");
+        unsigned nbs = 0, rho = 16, prio = 2;
+        if (!e || sscanf(e, "%u,%u,%u", &nbs, &rho, &prio) < 1) return 0xffffffffu;
+        return (nbs & 7u) | ((rho & 255u) << 8) | ((prio & 3u) << 16);
+    }();
 #define L(O, C)                                                                                              \
     do {                                                                                                     \
         if (bitslice)                                                                                        \
             hipLaunchKernelGGL((gcm_main_k<O, C, 1, 1>), dim3(grid), dim3(GcmShape<1>::threads), 0, s, tasks,    \
-                               (uint32_t)ntasks, queue, blks, sched, partial, pexp, t);                      \
+                               (uint32_t)ntasks, queue, blks, sched, partial, pexp, t, 0u);                  \
+        else if (hyb != 0xffffffffu)                                                                         \
+            hipLaunchKernelGGL((gcm_main_k<O, C, 1, 2>), dim3(grid), dim3(GcmShape<2>::threads), 0, s, tasks,    \
+                               (uint32_t)ntasks, queue, blks, sched, partial, pexp, t, hyb);                 \
         else                                                                                                 \
             hipLaunchKernelGGL((gcm_main_k<O, C, kStreams, 0>), dim3(grid), dim3(GcmShape<0>::threads), 0, s,    \
-                               tasks, (uint32_t)ntasks, queue, blks, sched, partial, pexp, t);               \
+                               tasks, (uint32_t)ntasks, queue, blks, sched, partial, pexp, t, 0u);           \
     } while (0)
     switch ((open ? 8 : 0) | crc_mode) {
         case 8: L(true, 0); break;

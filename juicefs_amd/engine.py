@@ -679,8 +679,21 @@ class MultiEngine:
             pass
 
     def _check(self, rc, what):
-        if rc:
-            _raise(None, rc, what)
+        """A failed mctx call raises with the HIP error of every member
+        context that recorded one (each device's part runs on its own
+        thread and records its failure on its own context), or the calling
+        thread's record when none did."""
+        if not rc:
+            return
+        if rc in (EIO, ENOMEM):
+            recs = []
+            for i in range(self.ndev):
+                he, txt = last_error(self.L.jfsx_mctx_ctx(self.m, i))
+                if he or txt:
+                    recs.append((i, he, txt))
+            if recs:
+                raise EngineError(rc, what, recs[0][1], "; ".join("device %d: %s" % (i, t) for i, _, t in recs))
+        _raise(None, rc, what)
 
     def seal_batch(self, algo, blks, n, crc_mode=CRC_GEN, mem=MEM_HOST):
         self._check(self.L.jfsx_mctx_seal_batch(self.m, algo, n, blks, crc_mode, mem), "jfsx_mctx_seal_batch")

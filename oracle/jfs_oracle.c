@@ -1271,3 +1271,70 @@ ORC_EXPORT double orc_bench_baseline(int algo, int mode, int nthreads, uint64_t 
     if (digest) *digest = dg;
     return bad ? -2.0 : el;
 }
+
+/* ------------------------------------------------------------------ */
+/* Expected results of a whole bench batch (bench.py's full check):    */
+/* for block b = block0 + i, len = lens[i] (or blen), the Seal tag and */
+/* the checksum() array of the synthetic block, by the oracle's own    */
+/* AEAD (AES-NI/PCLMUL GCM port, portable ChaCha20-Poly1305) and the   */
+/* SSE4.2 CRC, nthreads threads.  tags: 16 B per block; crcs: crcstride */
+/* bytes per block (checksum() bytes, BE).  Returns wall seconds.      */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    int algo;
+    uint64_t seed, block0, i0, i1, blen, crcstride;
+    const uint64_t *lens;
+    uint8_t *tags, *crcs;
+} expect_job;
+
+static void *expect_worker(void *arg) {
+    expect_job *j = (expect_job *)arg;
+    uint64_t maxlen = j->blen;
+    uint8_t *p = (uint8_t *)malloc(maxlen + 16), *c = (uint8_t *)malloc(maxlen + 16);
+    for (uint64_t i = j->i0; i < j->i1; i++) {
+        const uint64_t n = j->lens ? j->lens[i] : j->blen, b = j->block0 + i;
+        uint8_t key[32], nonce[12];
+        orc_gen_key(j->seed, b, key, nonce);
+        orc_gen_block(j->seed, b, p, n);
+        orc_checksum(p, (int64_t)n, j->crcs + i * j->crcstride, 1);
+        if (j->algo == ALGO_AES256GCM)
+            orc_aes256gcm_seal_ni(key, nonce, p, n, c, j->tags + 16 * i);
+        else
+            orc_chacha20poly1305_seal(key, nonce, NULL, 0, p, n, c, j->tags + 16 * i);
+    }
+    free(p);
+    free(c);
+    return NULL;
+}
+
+ORC_EXPORT double orc_expect_batch(int algo, int nthreads, uint64_t nblocks, const uint64_t *lens, uint64_t blen,
+                                   uint64_t seed, uint64_t block0, uint8_t *tags, uint8_t *crcs, uint64_t crcstride) {
+    if (nthreads < 1) nthreads = 1;
+    uint64_t maxlen = blen;
+    if (lens)
+        for (uint64_t i = 0; i < nblocks; i++) maxlen = lens[i] > maxlen ? lens[i] : maxlen;
+    if ((uint64_t)orc_checksum_len((int64_t)maxlen) > crcstride) return -3.0;
+    expect_job *jobs = (expect_job *)calloc((size_t)nthreads, sizeof(expect_job));
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    const uint64_t per = (nblocks + nthreads - 1) / nthreads;
+    double t0 = now_s();
+    for (int t = 0; t < nthreads; t++) {
+        expect_job *j = &jobs[t];
+        j->algo = algo;
+        j->seed = seed;
+        j->block0 = block0;
+        j->blen = maxlen;
+        j->lens = lens;
+        j->crcstride = crcstride;
+        j->tags = tags;
+        j->crcs = crcs;
+        j->i0 = (uint64_t)t * per < nblocks ? (uint64_t)t * per : nblocks;
+        j->i1 = j->i0 + per < nblocks ? j->i0 + per : nblocks;
+        pthread_create(&th[t], NULL, expect_worker, j);
+    }
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    double el = now_s() - t0;
+    free(jobs);
+    free(th);
+    return el;
+}

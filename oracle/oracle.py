@@ -61,6 +61,7 @@ def lib():
             "orc_data_decrypt": (I64, [I, P, P, I64, P]),
             "orc_bench_seal_crc": (ctypes.c_double, [I, I, U64, U64, U64, P]),
             "orc_bench_baseline": (ctypes.c_double, [I, I, I, U64, P, U64, U64, P]),
+            "orc_expect_batch": (ctypes.c_double, [I, I, U64, P, U64, U64, U64, P, P, U64]),
             "orc_lz4_bound": (I, [I]),
             "orc_lz4_compress": (I, [P, I, P, I]),
             "orc_lz4_decompress": (I, [P, I, P, I]),
@@ -266,6 +267,21 @@ def bench_baseline(algo, mode, nthreads, nblocks, blen, seed, lens=None):
     secs = lib().orc_bench_baseline(algo, mode, nthreads, nblocks, ln.ctypes.data if ln is not None else None, blen,
                                     seed, ctypes.byref(dg))
     return secs, dg.value
+
+
+def expect_batch(algo, nthreads, lens, seed, block0, crcstride):
+    """The oracle's Seal tags (n x 16 B) and checksum() arrays (n x crcstride
+    B, big-endian CRCs, zero-padded) of the synthetic blocks block0 + i of
+    lens[i] bytes: the full check of a bench batch.  (tags, crcs, seconds)."""
+    ln = np.asarray(lens, np.uint64)
+    n = ln.size
+    tags = np.zeros((n, 16), np.uint8)
+    crcs = np.zeros((n, crcstride), np.uint8)
+    secs = lib().orc_expect_batch(algo, nthreads, n, ln.ctypes.data, int(ln.max()) if n else 0, seed, block0,
+                                  tags.ctypes.data, crcs.ctypes.data, crcstride)
+    if secs < 0:
+        raise ValueError("expect_batch: crcstride %d too small" % crcstride)
+    return tags, crcs, secs
 
 
 # -- LZ4 block codec (oracle/jfs_lz4.c; compress.go:107-125) ------------------
