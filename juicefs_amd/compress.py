@@ -102,9 +102,12 @@ class LZ4:
 
 class ZStandard:
     """The "zstd" compressor (DataDog/zstd v1.5.0, level 1): Compress and
-    Decompress both run on the engine (jfsx_zstd_compress_batch writes the
-    zstd library's level-1 frames byte for byte; jfsx_zstd_decompress_batch
-    decodes as ZSTD_decompress)."""
+    Decompress both run on the engine.  jfsx_zstd_compress_batch is bit-exact
+    to the system libzstd 1.4.8's ZSTD_compress(level 1); byte parity with the
+    v1.5.0 library the reference links is unpinned (its vendored C is not in
+    the reference tree), but every frame is valid zstd and reads back through
+    this Decompress and through libzstd's ZSTD_decompress alike.
+    jfsx_zstd_decompress_batch decodes as ZSTD_decompress."""
 
     def __init__(self, level=1, eng=None):
         if level != 1:

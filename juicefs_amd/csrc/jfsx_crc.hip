@@ -43,8 +43,11 @@ namespace jfsx {
 // at 144 KiB of LDS (one 16-wave workgroup per CU).  A lane's 64-B chunk is a
 // chain of 16 slice-by-4 steps; two spans' chains run interleaved, and the
 // 4096-B span shift keeps its nibble tables (region 2).
+// default since round 4: byte tables (JFSX_CRC_BYTE = 1) with quad-transposed
+// coalesced loads (JFSX_CRC_XPOSE = 1), 6.03-6.05 TB/s at 64 GiB against 5.33
+// for the nibble kernel on the same box (profiles/r4/ab_crc.txt)
 #ifndef JFSX_CRC_BYTE
-#define JFSX_CRC_BYTE 0
+#define JFSX_CRC_BYTE 1
 #endif
 #ifndef JFSX_CRC_SPAN
 #define JFSX_CRC_SPAN 64
@@ -91,6 +94,46 @@ __device__ __forceinline__ uint32_t crc_u16_nib(const char *lds, uint32_t lb, ui
 #undef X3
 }
 
+#ifndef JFSX_CRC_CHAINS
+#define JFSX_CRC_CHAINS 2
+#endif
+#ifndef JFSX_CRC_XPOSE
+#define JFSX_CRC_XPOSE 1
+#endif
+// the lane's 64-byte chunk of span r of a segment: piece j.  XPOSE = 0: lane l
+// owns bytes 64l..64l+63 (each load instruction touches 32 cache lines, 32 B
+// of each).  XPOSE = 1: instruction j loads the span's bytes 1024j + 16l
+// (one fully coalesced 1 KiB row, 8 whole lines); after quad_xpose lane
+// l = 4m + t holds the chunk at 64 (16t + m) of the span.
+__device__ __forceinline__ uint4 crc_chunk_ld(const uint8_t *seg, uint32_t lane, int r, int j) {
+    return JFSX_CRC_XPOSE ? gld16(seg + 4096 * r + 1024 * j + 16 * lane) : gld16(seg + 4096 * r + 64 * lane + 16 * j);
+}
+// lane chunk index within a span (the final shift to the segment end)
+__device__ __forceinline__ uint32_t crc_chunk_idx(uint32_t lane) {
+    return JFSX_CRC_XPOSE ? 16u * (lane & 3u) + (lane >> 2) : lane;
+}
+// 4 x 4 transpose of 16-byte pieces across the 4 lanes of a quad: afterwards
+// v[i] of lane t is what v[t] of lane i held.  Two butterfly stages (lane bit
+// 0, then bit 1), each a DPP quad swap of the piece the partner needs.
+__device__ __forceinline__ uint32_t dpp_swap(uint32_t x, int ctrl) {
+    return ctrl == 0xB1 ? (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true)
+                        : (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, true);
+}
+__device__ __forceinline__ void xpose_stage(uint32_t &a, uint32_t &b, bool odd, int ctrl) {
+    const uint32_t r = dpp_swap(odd ? a : b, ctrl);
+    a = odd ? r : a;
+    b = odd ? b : r;
+}
+__device__ __forceinline__ void quad_xpose(uint4 (&v)[4], uint32_t lane) {
+    const bool o1 = lane & 1u, o2 = lane & 2u;
+#define XS(f)                                 \
+    xpose_stage(v[0].f, v[1].f, o1, 0xB1);    \
+    xpose_stage(v[2].f, v[3].f, o1, 0xB1);    \
+    xpose_stage(v[0].f, v[2].f, o2, 0x4E);    \
+    xpose_stage(v[1].f, v[3].f, o2, 0x4E);
+    XS(x) XS(y) XS(z) XS(w)
+#undef XS
+}
 #if JFSX_CRC_BYTE
 // byte k of x through U(12 + k): region k >> 1 (lb byte 2 = 1), half k & 1
 #define BYT(x, k)                                                                                              \
@@ -192,38 +235,53 @@ __global__ __launch_bounds__(kCrcWaves * 64) __attribute__((amdgpu_waves_per_eu(
         const uint64_t nrows = (seg1 - seg0 + 1023) / 1024;
         if (JFSX_CRC_BYTE && seg1 - seg0 == (uint64_t)kSeg) {
 #if JFSX_CRC_BYTE
-            // full segment, 64-B lane chunks of the 8 spans of 4 KiB; spans
-            // r and r + 1 are two independent slice-by-4 chains, and the next
-            // pair's 128 B per lane are in flight meanwhile
-            const uint8_t *q = src + seg0 + 64 * lane;
-            uint4 c0b[4], c1b[4];
+            // full segment, 64-B lane chunks of the 8 spans of 4 KiB; CH spans
+            // are CH independent slice-by-4 chains, and each piece's load for
+            // the span CH further on is issued as soon as the piece is consumed
+            constexpr int CH = JFSX_CRC_CHAINS;
+            uint4 buf[CH][4];
 #pragma unroll
-            for (int j = 0; j < 4; j++) c0b[j] = gld16(q + 16 * j), c1b[j] = gld16(q + 4096 + 16 * j);
+            for (int k = 0; k < CH; k++)
 #pragma unroll
-            for (int r = 0; r < 8; r += 2) {
-                uint4 n0[4], n1[4];
-                if (r + 2 < 8) {
+                for (int j = 0; j < 4; j++) buf[k][j] = crc_chunk_ld(src + seg0, lane, k, j);
 #pragma unroll
-                    for (int j = 0; j < 4; j++)
-                        n0[j] = gld16(q + 4096 * (r + 2) + 16 * j), n1[j] = gld16(q + 4096 * (r + 3) + 16 * j);
+            for (int r = 0; r < 8; r += CH) {
+                if (JFSX_CRC_XPOSE) {
+#pragma unroll
+                    for (int k = 0; k < CH; k++) quad_xpose(buf[k], lane);
                 }
                 // x = state ^ next word; each step folds the next word into
                 // its 4-way XOR (two v_bitop3)
-                uint32_t x0 = c0b[0].x, x1 = c1b[0].x;
+                uint32_t x[CH];
+#pragma unroll
+                for (int k = 0; k < CH; k++) x[k] = buf[k][0].x;
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    x0 = crc_step4x(lds, lb, x0, c0b[j].y), x1 = crc_step4x(lds, lb, x1, c1b[j].y);
-                    x0 = crc_step4x(lds, lb, x0, c0b[j].z), x1 = crc_step4x(lds, lb, x1, c1b[j].z);
-                    x0 = crc_step4x(lds, lb, x0, c0b[j].w), x1 = crc_step4x(lds, lb, x1, c1b[j].w);
-                    if (j < 3)
-                        x0 = crc_step4x(lds, lb, x0, c0b[j + 1].x), x1 = crc_step4x(lds, lb, x1, c1b[j + 1].x);
-                }
-                A = crc_step4x(lds, lb, x0, crc_shift4096(lds, lb, A));
-                A = crc_step4x(lds, lb, x1, crc_shift4096(lds, lb, A));
-                if (r + 2 < 8) {
 #pragma unroll
-                    for (int j = 0; j < 4; j++) c0b[j] = n0[j], c1b[j] = n1[j];
+                    for (int k = 0; k < CH; k++) x[k] = crc_step4x(lds, lb, x[k], buf[k][j].y);
+#pragma unroll
+                    for (int k = 0; k < CH; k++) x[k] = crc_step4x(lds, lb, x[k], buf[k][j].z);
+                    if (j < 3) {
+#pragma unroll
+                        for (int k = 0; k < CH; k++) x[k] = crc_step4x(lds, lb, x[k], buf[k][j].w);
+#pragma unroll
+                        for (int k = 0; k < CH; k++) x[k] = crc_step4x(lds, lb, x[k], buf[k][j + 1].x);
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < CH; k++) x[k] = crc_step4x(lds, lb, x[k], buf[k][j].w);
+                    }
+                    // piece j of every chain consumed (its .x was read one step ago)
+                    if (r + CH < 8 && j > 0) {
+#pragma unroll
+                        for (int k = 0; k < CH; k++) buf[k][j - 1] = crc_chunk_ld(src + seg0, lane, r + CH + k, j - 1);
+                    }
                 }
+                if (r + CH < 8) {
+#pragma unroll
+                    for (int k = 0; k < CH; k++) buf[k][3] = crc_chunk_ld(src + seg0, lane, r + CH + k, 3);
+                }
+#pragma unroll
+                for (int k = 0; k < CH; k++) A = crc_step4x(lds, lb, x[k], crc_shift4096(lds, lb, A));
             }
             lend = kSeg;
 #endif
@@ -233,16 +291,22 @@ __global__ __launch_bounds__(kCrcWaves * 64) __attribute__((amdgpu_waves_per_eu(
             // soon as the piece is consumed
             constexpr int P = JFSX_CRC_SPAN / 16, NSP = 32768 / (64 * JFSX_CRC_SPAN);
             const uint8_t *q = src + seg0 + JFSX_CRC_SPAN * lane;
+            static_assert(!JFSX_CRC_XPOSE || JFSX_CRC_SPAN == 64, "quad transpose needs 64-B lane chunks");
             uint4 buf[P];
 #pragma unroll
-            for (int j = 0; j < P; j++) buf[j] = gld16(q + 16 * j);
+            for (int j = 0; j < P; j++) buf[j] = JFSX_CRC_XPOSE ? crc_chunk_ld(src + seg0, lane, 0, j) : gld16(q + 16 * j);
 #pragma unroll
             for (int r = 0; r < NSP; r++) {
                 uint32_t c = 0;
+#if JFSX_CRC_XPOSE
+                quad_xpose(buf, lane);
+#endif
 #pragma unroll
                 for (int j = 0; j < P; j++) {
                     const uint4 p = buf[j];
-                    if (r + 1 < NSP) buf[j] = gld16(q + 64 * JFSX_CRC_SPAN * (r + 1) + 16 * j);
+                    if (r + 1 < NSP)
+                        buf[j] = JFSX_CRC_XPOSE ? crc_chunk_ld(src + seg0, lane, r + 1, j)
+                                                : gld16(q + 64 * JFSX_CRC_SPAN * (r + 1) + 16 * j);
                     c = crc_u16_nib(lds, lb, p.x ^ c, p.y, p.z, p.w);
                 }
                 A = crc_word_nib(lds, lb, 16, A) ^ c;
@@ -282,7 +346,7 @@ __global__ __launch_bounds__(kCrcWaves * 64) __attribute__((amdgpu_waves_per_eu(
             if (JFSX_CRC_SPAN >= 64) {
                 // lane chunk end to segment end: SPAN * (63 - lane) bytes =
                 // crcx[128 + lane] (64 * (63 - lane) bytes) squared SPAN / 64 - 1 times
-                uint32_t x = tab.crcx[128 + lane];
+                uint32_t x = tab.crcx[128 + crc_chunk_idx(lane)];
                 for (int k = 64; k < JFSX_CRC_SPAN; k <<= 1) x = crc_mulmod(x, x);
                 v = crc_mulmod(x, A);
             } else {

@@ -15,4 +15,8 @@ ab() {
 }
 ab base1 && ab h0 JFSX_GCM_HYBRID=0,16,0 && ab h1 JFSX_GCM_HYBRID=1,20,2 && \
 ab h2r12 JFSX_GCM_HYBRID=2,12,2 && ab h2r20 JFSX_GCM_HYBRID=2,20,2 && ab h2r28 JFSX_GCM_HYBRID=2,28,2 && \
-ab h2p0 JFSX_GCM_HYBRID=2,20,0 && ab h3 JFSX_GCM_HYBRID=3,20,2 && ab base2
+ab h2p0 JFSX_GCM_HYBRID=2,20,0 && ab h3 JFSX_GCM_HYBRID=3,20,2 && ab base2 || exit 1
+# CRC-verify kernel variants (scripts/build_crc_variant.sh): byte tables with 2 / 4
+# chains, quad-transposed coalesced loads (X) on the byte and nibble kernels
+echo "crc A/B (64 GiB verify)"
+AB_REPS="1 2" bash scripts/gpu_ab.sh r4crc "--mode crc" default=default b2=CRCB2 b4=CRCB4 bx2=CRCBX2 bx4=CRCBX4 nx=CRCNX

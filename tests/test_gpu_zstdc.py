@@ -101,3 +101,7 @@ def test_mirror_compress_and_upload_blocks(eng):
     outs = C.upload_blocks(st, keys, blocks, z)
     assert outs == [zstd_lib.compress_simple(b, 1) for b in blocks]
     assert C.load_blocks(st, keys, [len(b) for b in blocks], z) == blocks
+    # the stored objects also read back through the C library's one-shot
+    # decoder, the call DataDog/zstd's Decompress makes (compress.go:93-102)
+    for k, b in zip(keys, blocks):
+        assert zstd_lib.decompress(st.d[k], len(b)) == (len(b), b)
