@@ -14,7 +14,10 @@ each variant this writes, with the pass each number came from:
                          wave64 VALU instruction per cycle over its 4 SIMDs)
             with cycles = GRBM_GUI_ACTIVE / 8 XCDs, CUs = 256
 
-usage: python3 scripts/pmc_r3.py gpurun_out/<suite> > profiles/r3/pmc_r3.json
+            salu_issue = SQ_INSTS_SALU / (cycles x CUs)  (codec passes)
+
+usage: python3 scripts/pmc_r3.py gpurun_out/<suite> [more suites...] > profiles/r4/pmc_r4.json
+(later suites' passes of the same variant and counter set replace earlier ones)
 """
 import csv
 import glob
@@ -52,9 +55,11 @@ def bench_line(log):
     return None
 
 
-def main(root):
-    out = {"source": root, "method": __doc__.split("\n\n")[1].strip(), "passes": {}, "variants": {}}
-    for d in sorted(glob.glob(os.path.join(root, "pmc_*__*"))):
+def main(roots):
+    out = {"source": roots, "method": __doc__.split("\n\n")[1].strip(), "passes": {}, "variants": {}}
+    dirs = [d for root in roots for d in sorted(glob.glob(os.path.join(root, "pmc_*__*")))]
+    for d in dirs:
+        root = os.path.dirname(d)
         if not os.path.isdir(d):
             continue
         variant, cset = os.path.basename(d)[4:].split("__", 1)
@@ -72,7 +77,7 @@ def main(root):
                 vals[r["Counter_Name"]] = vals.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
         b = bench_line(d + ".log") or {}
         plain = (b.get("roofline") or {}).get("plain_bytes_per_launch")
-        rec = {"pass": os.path.relpath(d, root), "kernel_prefix": pref, "dispatch_id": last,
+        rec = {"pass": os.path.relpath(d), "kernel_prefix": pref, "dispatch_id": last,
                "counters": vals, "plain_bytes_per_launch": plain,
                "bench_config": (b.get("config") or {}).get("workload")}
         out["passes"]["%s__%s" % (variant, cset)] = rec
@@ -92,6 +97,14 @@ def main(root):
             if "SQ_INSTS_VALU" in vals:
                 v["valu_issue"] = round(vals["SQ_INSTS_VALU"] / cyc, 4)
                 v["valu_pass"] = rec["pass"]
+            if "SQ_INSTS_SALU" in vals:
+                v["salu_issue"] = round(vals["SQ_INSTS_SALU"] / cyc, 4)
+                v["salu_pass"] = rec["pass"]
+                if plain:
+                    # wave instructions per plaintext byte (scalar and vector)
+                    v["salu_per_byte"] = round(vals["SQ_INSTS_SALU"] / plain, 4)
+                    if "SQ_INSTS_VALU" in vals:
+                        v["valu_per_byte"] = round(vals["SQ_INSTS_VALU"] / plain, 4)
             if "SQ_LDS_BANK_CONFLICT" in vals and "SQ_LDS_IDX_ACTIVE" in vals and vals["SQ_LDS_IDX_ACTIVE"]:
                 v["lds_conflict_share"] = round(vals["SQ_LDS_BANK_CONFLICT"] / vals["SQ_LDS_IDX_ACTIVE"], 4)
     for v in out["variants"].values():
@@ -103,4 +116,4 @@ def main(root):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1:])
