@@ -423,6 +423,8 @@ def full_check(args, E, blks, got, lens, base):
     import numpy as np
     from oracle import oracle as orc
     threads, _ = host_cores()
+    world = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    threads = max(1, threads // max(world, 1))  # the ranks of one node share its cores
     nb, stride = got.shape
     algo = orc.AES256GCM if args.algo == "aes256gcm" else orc.CHACHA20P1305
     etags, ecrcs, secs = orc.expect_batch(algo, threads, lens, SEED, base, stride)

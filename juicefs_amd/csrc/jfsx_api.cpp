@@ -840,7 +840,11 @@ int run_codec(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, CodecOp op) {
     if (n == 0) return 0;
     int rc;
     Workspace &w = c->ws[0];
-    const int zc_waves = std::min(n, c->ncu * kZcWavesPerCu);
+    // zstd compression: persistent waves per CU (JFSX_ZC_WAVES overrides the
+    // default for A/B; LDS allows 11, VGPRs 12)
+    static const int zc_per_cu = getenv("JFSX_ZC_WAVES") ? std::max(1, std::min(11, atoi(getenv("JFSX_ZC_WAVES"))))
+                                                         : kZcWavesPerCu;
+    const int zc_waves = std::min(n, c->ncu * zc_per_cu);
     // zstd decompression: block-parallel persistent waves unless
     // JFSX_ZSTD_SERIAL=1 selects the one-wave-per-object serial kernel (A/B)
     static const bool zd_serial = getenv("JFSX_ZSTD_SERIAL") && atoi(getenv("JFSX_ZSTD_SERIAL")) == 1;

@@ -629,41 +629,50 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
     for (int s = 0; s < NS; s++)
         nxt[s] = r0 < rf ? gld16(src + ld0[s] + 1024 * r0 + lo) : make_uint4(0, 0, 0, 0);
 #if JFSX_U2
-    // two rows of one stream per iteration: the two AES chains interleave,
-    // GHASH/CRC stay sequential (register peak of one row)
-    if (NS == 1 && act[0] && rf >= r0 + 2) {
-        uint4 n0 = gld16(src + ld0[0] + 1024 * r0 + lo);
-        uint4 n1 = gld16(src + ld0[0] + 1024 * (r0 + 1) + lo);
+    // UR rows of one stream per iteration (2 in the 16-wave shape; the 8-wave
+    // shape has twice the VGPRs and takes JFSX_HYB_UR): the UR AES chains
+    // interleave, GHASH/CRC stay sequential (register peak of one row)
+    constexpr int UR = BS == 2 ? JFSX_HYB_UR : 2;
+    if (NS == 1 && act[0] && rf >= r0 + UR) {
+        uint4 nn[UR];
+#pragma unroll
+        for (int u = 0; u < UR; u++) nn[u] = gld16(src + ld0[0] + 1024 * (r0 + u) + lo);
 #if JFSX_UCTR
         uint32_t uw[4] = {0, 0, 0, 0};
         uint32_t uw0 = 0;
         bool uwok = false;
 #endif
-        // task row index of the stream's first row: even (row pairs, see above)
+        // task row index of the stream's first row: even (streams start on row
+        // pairs), so with even UR a row u of even index never ends a segment
+        // and the compiler drops that test
         const uint32_t rb0 = (uint32_t)((ld0[0] - c0) >> 11) << 1;
-        for (; r0 + 1 < rf; r0 += 2) {
-            const uint4 dd[2] = {n0, n1};
+        for (; r0 + UR - 1 < rf; r0 += UR) {
+            uint4 dd[UR];
+#pragma unroll
+            for (int u = 0; u < UR; u++) dd[u] = nn[u];
             const uint64_t o0 = ld0[0] + 1024 * r0 + lo;
-            if (r0 + 3 < rf) {
-                n0 = gld16(src + o0 + 2048);
-                n1 = gld16(src + o0 + 3072);
+            if (r0 + 2 * UR - 1 < rf) {
+#pragma unroll
+                for (int u = 0; u < UR; u++) nn[u] = gld16(src + o0 + 1024 * (UR + u));
             }
-            const uint32_t ctr2[2] = {(uint32_t)((o0 >> 4) + 2), (uint32_t)((o0 >> 4) + 66)};
-            uint32_t ks2[2][4];
+            uint32_t ctrs[UR];
+#pragma unroll
+            for (int u = 0; u < UR; u++) ctrs[u] = (uint32_t)((o0 >> 4) + 2 + 64 * u);
+            uint32_t ks2[UR][4];
 #if JFSX_UCTR
             {
-                // row counters C and C + 64 (C = the row's lane-0 counter, wave-uniform)
+                // row counters C + 64 u (C = the first row's lane-0 counter, wave-uniform)
                 uint32_t C = (uint32_t)(((ld0[0] + 1024 * r0) >> 4) + 2);
                 OPAQUE(C);
-                // the window must hold U(C) .. U(C + 64 + 63)
-                if (!uwok || (C >> 8) < uw0 || ((C + 127) >> 8) - uw0 > 63u) {
+                // the window must hold U(C) .. U(C + 64 UR - 1 + 1)
+                if (!uwok || (C >> 8) < uw0 || ((C + 64u * UR + 63u) >> 8) - uw0 > 63u) {
                     uw0 = C >> 8;
                     aes_r2_uniform(lds, loff, rk, k1, uw0 + lane, uw);
                     uwok = true;
                 }
-                uint32_t u2[2][4], d2[2][4], cym[2];
+                uint32_t u2[UR][4], d2[UR][4], cym[UR];
 #pragma unroll
-                for (int u = 0; u < 2; u++) {
+                for (int u = 0; u < UR; u++) {
                     const uint32_t Cr = C + 64u * u;
                     const uint32_t i0 = (Cr >> 8) - uw0;
                     // ~0 on the lanes whose counter carried into U + 1, else 0
@@ -674,13 +683,13 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
                         d2[u][k] = u2[u][k] ^ __builtin_amdgcn_readlane(uw[k], i0 + 1);
                     }
                 }
-                aes_ctr_blocks_u<2>(lds, loff, rk, k1, ctr2, u2, d2, cym, ks2);
+                aes_ctr_blocks_u<UR>(lds, loff, rk, k1, ctrs, u2, d2, cym, ks2);
             }
 #else
-            aes_ctr_blocks<2>(lds, loff, rk, k1, ctr2, ks2);
+            aes_ctr_blocks<UR>(lds, loff, rk, k1, ctrs, ks2);
 #endif
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
+            for (int u = 0; u < UR; u++) {
                 const uint64_t o = o0 + 1024 * u;
 #if JFSX_UCTR
                 // data ^ keystream ^ last round key in one v_bitop3

@@ -260,3 +260,20 @@ def test_block_parallel_matches_across_blocks(eng):
     for i, (s, (st, d)) in enumerate(zip(exp, got)):
         assert st == E.OK and d == s, i
     assert eng.metrics()["zstd_serial"] == 0
+
+
+def test_arena_budget_caps_the_decoder_waves(monkeypatch):
+    """The block-parallel decoder's arenas (13.8 MiB per wave) are capped by
+    the context's budget (JFSX_ZSTD_ARENA_MB, read at context open): with room
+    for 2 arenas, or for less than one (one wave then), a 20-frame batch still
+    decodes to the same bytes on the block-parallel kernel."""
+    srcs = [lz4_data.sample(lz4_data.KINDS[i % 6], 200000 + 977 * i, seed=300 + i) for i in range(20)]
+    frames = [zstd_lib.compress(s, 1) for s in srcs]
+    for mb in ("30", "1"):
+        monkeypatch.setenv("JFSX_ZSTD_ARENA_MB", mb)
+        e = E.Engine(0)
+        try:
+            got = e.zstd_decompress(frames, [len(s) for s in srcs])
+            assert all(st == E.OK and d == s for s, (st, d) in zip(srcs, got)), mb
+        finally:
+            e.close()
