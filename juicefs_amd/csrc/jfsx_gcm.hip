@@ -539,8 +539,12 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
             st[s].sub0 = c0 + (uint64_t)(wave - nt) * q * kSeg;
             st[s].sub1 = st[s].sub0 + (uint64_t)q * kSeg;
         } else if (BS == 2) {
-            const uint32_t np = (uint32_t)((c1 - tt0 + 2047) / 2048);
-            const uint32_t ra = 2 * (wave * np / nt), rb = 2 * ((wave + 1) * np / nt);
+            // groups of JFSX_HYB_UR rows (a divisor of 32): every stream starts
+            // on a multiple of UR rows, so only the last row of a UR block can
+            // end a segment
+            constexpr uint32_t G = JFSX_HYB_UR;
+            const uint32_t ng = (uint32_t)((c1 - tt0 + 1024 * G - 1) / (1024 * G));
+            const uint32_t ra = G * (wave * ng / nt), rb = G * ((wave + 1) * ng / nt);
             st[s].sub0 = tt0 + (uint64_t)ra * 1024;
             st[s].sub1 = rb > ra ? (tt0 + (uint64_t)rb * 1024 < c1 ? tt0 + (uint64_t)rb * 1024 : c1) : st[s].sub0;
         } else if (kRowSplit) {
@@ -642,10 +646,20 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
         uint32_t uw0 = 0;
         bool uwok = false;
 #endif
-        // task row index of the stream's first row: even (streams start on row
-        // pairs), so with even UR a row u of even index never ends a segment
-        // and the compiler drops that test
-        const uint32_t rb0 = (uint32_t)((ld0[0] - c0) >> 11) << 1;
+        // task row index of the stream's first row: a multiple of 2 (16-wave
+        // shape, row pairs) or of UR (8-wave shape), so the compiler drops the
+        // segment-end test of rows that cannot end a segment
+        constexpr uint32_t RA = BS == 2 ? (32 % UR == 0 ? (uint32_t)UR : 1u) : 2u;
+        const uint32_t rb0 = (uint32_t)((ld0[0] - c0) >> 10) / RA * RA;
+        // software pipelining (8-wave shape, JFSX_HYB_SWP): the GHASH and CRC
+        // lookups of UR block i - 1 share a basic block with the AES of block
+        // i (independent LDS work to fill the rounds' latency); its segment
+        // end, if any, is handled after block i's stores
+        constexpr bool SWP = BS == 2 && JFSX_HYB_SWP;
+        static_assert(!SWP || 32 % UR == 0, "software pipelining needs UR | 32");
+        uint4 pc[UR], pq[UR];
+        bool pend = false;
+        uint32_t pr0 = 0;
         for (; r0 + UR - 1 < rf; r0 += UR) {
             uint4 dd[UR];
 #pragma unroll
@@ -654,6 +668,15 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
             if (r0 + 2 * UR - 1 < rf) {
 #pragma unroll
                 for (int u = 0; u < UR; u++) nn[u] = gld16(src + o0 + 1024 * (UR + u));
+            }
+            if (SWP && pend) {
+#pragma unroll
+                for (int u = 0; u < UR; u++) {
+#ifndef JFSX_ABLATE_GHASH
+                    ghash_step(lds, st[0].acc, gl, pc[u]);
+#endif
+                    if (CRCMODE) st[0].A = crc_piece<kLdsCrc>(lds, st[0].A, pq[u].x, pq[u].y, pq[u].z, pq[u].w);
+                }
             }
             uint32_t ctrs[UR];
 #pragma unroll
@@ -702,6 +725,11 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
                 const uint4 c = OPEN ? dd[u] : x, p = OPEN ? x : dd[u];
                 gst16(dst + o, OPEN ? p : c);
                 const uint4 cq = crc_src<CRCMODE>(c, p);
+                if (SWP) {
+                    pc[u] = c;
+                    pq[u] = cq;
+                    continue;
+                }
 #ifndef JFSX_ABLATE_GHASH
                 ghash_step(lds, st[0].acc, gl, c);
 #endif
@@ -712,6 +740,31 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
                     st[0].A = 0;
                     st[0].seg0 += kSeg;
                 }
+            }
+            if (SWP) {
+                // the previous block's segment end (its CRC went in above)
+                if (CRCMODE && pend && ((rb0 + pr0 + UR - 1) & 31) == 31) {
+                    crc_segment_done<CRCMODE>(blk, tab, lane, xl, st[0].seg0, st[0].A, st[0].seg0 < st[0].sub0, lds,
+                                              c0);
+                    st[0].A = 0;
+                    st[0].seg0 += kSeg;
+                }
+                pend = true;
+                pr0 = (uint32_t)r0;
+            }
+        }
+        if (SWP && pend) {
+#pragma unroll
+            for (int u = 0; u < UR; u++) {
+#ifndef JFSX_ABLATE_GHASH
+                ghash_step(lds, st[0].acc, gl, pc[u]);
+#endif
+                if (CRCMODE) st[0].A = crc_piece<kLdsCrc>(lds, st[0].A, pq[u].x, pq[u].y, pq[u].z, pq[u].w);
+            }
+            if (CRCMODE && ((rb0 + pr0 + UR - 1) & 31) == 31) {
+                crc_segment_done<CRCMODE>(blk, tab, lane, xl, st[0].seg0, st[0].A, st[0].seg0 < st[0].sub0, lds, c0);
+                st[0].A = 0;
+                st[0].seg0 += kSeg;
             }
         }
         if (r0 < rf) nxt[0] = gld16(src + ld0[0] + 1024 * r0 + lo);

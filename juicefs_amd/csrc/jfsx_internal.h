@@ -38,6 +38,10 @@ constexpr int kThreads = kWaves * 64;
 #ifndef JFSX_HYB_UR
 #define JFSX_HYB_UR 4
 #endif
+// software-pipelined GHASH/CRC in the 8-wave shape's T-table loop
+#ifndef JFSX_HYB_SWP
+#define JFSX_HYB_SWP 0
+#endif
 #ifndef JFSX_U2
 #define JFSX_U2 1
 #endif

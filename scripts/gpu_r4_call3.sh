@@ -10,6 +10,8 @@ export TMPDIR=/tmp
 bash scripts/gpu_r3_tests.sh r4c || exit 1
 JFSX_GCM_HYBRID=0,16,0 timeout -k 10 400 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fused_modes.py -x -q --timeout 120 --timeout-method thread > $out/ur4_pytest.log 2>&1 || { echo "UR4 parity failed"; tail -30 $out/ur4_pytest.log; exit 1; }
 echo "8-wave UR4 parity: $(tail -1 $out/ur4_pytest.log)"
+JFSX_LIB=juicefs_amd/_build/libjfsx_HSWP4.so JFSX_GCM_HYBRID=0,16,0 timeout -k 10 400 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fused_modes.py -x -q --timeout 120 --timeout-method thread > $out/swp_pytest.log 2>&1 || { echo "SWP parity failed"; tail -30 $out/swp_pytest.log; exit 1; }
+echo "8-wave UR4 SWP parity: $(tail -1 $out/swp_pytest.log)"
 ab() {
   name=$1; lib=$2; shift 2
   env JFSX_LIB=$lib "$@" timeout -k 10 200 python3 bench.py --blocks 4096 --steps 5 --warmup 1 --no-cpu --verify 0 > $out/ab_$name.json 2> $out/ab_$name.err || { echo "$name failed"; tail -5 $out/ab_$name.err; return 1; }
@@ -18,5 +20,6 @@ ab() {
 D=juicefs_amd/libjfsx.so
 ab base1 $D && ab ur4 $D JFSX_GCM_HYBRID=0,16,0 && ab ur3 juicefs_amd/_build/libjfsx_HUR3.so JFSX_GCM_HYBRID=0,16,0 && \
 ab ur2 juicefs_amd/_build/libjfsx_HUR2.so JFSX_GCM_HYBRID=0,16,0 && ab ur4h2 $D JFSX_GCM_HYBRID=2,20,2 && \
-ab ur4h1 $D JFSX_GCM_HYBRID=1,16,2 && ab base2 $D && ab ur4b $D JFSX_GCM_HYBRID=0,16,0 || exit 1
+ab ur4h1 $D JFSX_GCM_HYBRID=1,16,2 && ab swp4 juicefs_amd/_build/libjfsx_HSWP4.so JFSX_GCM_HYBRID=0,16,0 && \
+ab base2 $D && ab ur4b $D JFSX_GCM_HYBRID=0,16,0 && ab swp4b juicefs_amd/_build/libjfsx_HSWP4.so JFSX_GCM_HYBRID=0,16,0 || exit 1
 bash scripts/gpu_r4_suite.sh r4c lines1
