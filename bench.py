@@ -474,6 +474,11 @@ def pmc_variant(args):
     return v + ("_ragged" if args.ragged else "")
 
 
+CODEC_TRAFFIC_NOTE = ("memory-side L2 requests (2 x FETCH_SIZE + WRITE_SIZE): they include Infinity-Cache hits "
+                      "on the per-wave hash tables and scratch, and these kernels' access widths are uncalibrated "
+                      "for that formula (MI355X_MICROARCH, HBM): an upper bound on HBM bytes, not a measurement")
+
+
 def _load(rel):
     try:
         return json.load(open(os.path.join(PROFILES, rel)))
@@ -501,8 +506,9 @@ def pmc_traffic(args, plain_per_launch):
         if traffic is None and "bytes_per_plain_byte" in v:
             traffic = int(v["bytes_per_plain_byte"] * plain_per_launch)
             src = "profiles/%s %s (%s; %s)" % (rel, key, v.get("fetch_pass"), v.get("write_pass"))
-        if binding is None and ("lds_busy" in v or "valu_issue" in v):
-            binding = {k: v[k] for k in ("lds_busy", "valu_issue", "lds_conflict_share") if k in v}
+        if binding is None and ("lds_busy" in v or "valu_issue" in v or "salu_issue" in v):
+            binding = {k: v[k] for k in ("lds_busy", "valu_issue", "lds_conflict_share", "salu_issue",
+                                         "salu_per_byte", "valu_per_byte") if k in v}
             binding["source"] = "profiles/%s %s (%s)" % (rel, key, v.get("lds_pass") or v.get("valu_pass"))
     if traffic is None and key in R2_KEYS:
         k2 = ((_load(PMC_R2) or {}).get("kernels") or {}).get(R2_KEYS[key])
@@ -532,7 +538,7 @@ def host_ingest(args, world, rank, local, dist, eng):
     nb, L = args.blocks, args.block_bytes
     nseg = -(-L // E.SEG)
     algo = E.AES256GCM if args.algo == "aes256gcm" else E.CHACHA20P1305
-    pcie = pcie_probe(eng)
+    pcie_before = pcie_probe(eng)
     hin = eng.alloc_pinned(nb * L)
     hout = eng.alloc_pinned(nb * L)
     hcrc = eng.alloc_pinned(nb * 4 * nseg)
@@ -565,6 +571,11 @@ def host_ingest(args, world, rank, local, dist, eng):
     el = max_over_ranks(dist, time.perf_counter() - t0, local)
     eng.set_timing(False)
     k_ms, k_n = eng.kernel_time(reset=True)
+    # the link probed again right after the ring (the probe before it has read
+    # below what the ring itself moved on some boxes); the faster of the two
+    pcie_after = pcie_probe(eng)
+    pcie = {k: max(pcie_before.get(k, 0.0), pcie_after.get(k, 0.0)) for k in set(pcie_before) | set(pcie_after)}
+    pcie_runs = {"before_ring": pcie_before, "after_ring": pcie_after}
     verified = 0
     if args.verify:
         from oracle import oracle as orc
@@ -601,9 +612,11 @@ def host_ingest(args, world, rank, local, dist, eng):
                          "frac": round(value / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
                          "traffic_note": "HBM bytes per launch of gcm_main_k (one launch per ring slot)",
                          "peak_basis": "min over directions of simultaneous H2D + D2H copies of 1 GiB on the "
-                                       "ring's streams (jfsx_pcie_probe); one-way rates in pcie_measured",
+                                       "ring's streams (jfsx_pcie_probe, the better of a probe before and one after "
+                                       "the ring); one-way rates in pcie_measured",
                          "frac_of_one_way_d2h": round(value / pcie["d2h"], 4),
-                         "pcie_measured": pcie, "kernel_avg_ms": round(k_ms / max(k_n, 1), 3),
+                         "pcie_measured": pcie, "pcie_probes": pcie_runs,
+                         "kernel_avg_ms": round(k_ms / max(k_n, 1), 3),
                          "kernel_launches": k_n, "plain_bytes_per_launch": plain_launch, "binding": binding},
             "cpu_baseline": cpu, "verified_blocks": verified, "full_check": full}), flush=True)
     eng.free_pinned(hin)
@@ -970,6 +983,7 @@ def lz4_bench(args, world, rank, local, dist, eng):
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(algo_bytes / (k_avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if k_n else None,
                          "traffic": pmc_traffic(args, nb * L)[0], "traffic_source": pmc_traffic(args, nb * L)[1],
+                         "traffic_note": CODEC_TRAFFIC_NOTE, "binding": pmc_traffic(args, nb * L)[2],
                          "kernel": "lz4_compress_k" if args.mode == "lz4" else "lz4_decompress_k",
                          "kernel_avg_ms": round(k_avg, 3), "algorithmic_bytes_per_launch": algo_bytes,
                          "plain_bytes_per_launch": nb * L},
@@ -1080,6 +1094,7 @@ def zstd_bench(args, world, rank, local, dist, eng):
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(algo_bytes / (k_avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if k_n else None,
                          "traffic": pmc_traffic(args, nb * L)[0], "traffic_source": pmc_traffic(args, nb * L)[1],
+                         "traffic_note": CODEC_TRAFFIC_NOTE, "binding": pmc_traffic(args, nb * L)[2],
                          "kernel": "zstd_decompress_k" if os.environ.get("JFSX_ZSTD_SERIAL") == "1"
                          else "zstd_decompress_par_k", "kernel_avg_ms": round(k_avg, 3),
                          "objects_to_serial_decoder": serial,
@@ -1185,6 +1200,7 @@ def zstdc_bench(args, world, rank, local, dist, eng):
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(algo_bytes / (k_avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if k_n else None,
                          "traffic": pmc_traffic(args, nb * L)[0], "traffic_source": pmc_traffic(args, nb * L)[1],
+                         "traffic_note": CODEC_TRAFFIC_NOTE, "binding": pmc_traffic(args, nb * L)[2],
                          "kernel": "zstd_compress_k", "kernel_avg_ms": round(k_avg, 3),
                          "algorithmic_bytes_per_launch": algo_bytes, "plain_bytes_per_launch": nb * L},
             "cpu_baseline": cpu, "verified_blocks": verified}), flush=True)

@@ -1104,7 +1104,9 @@ int jfsx_pcie_probe(jfsx_ctx *c, uint64_t bytes, double out[4]) {
         rc = JFSX_EIO;
     };
     hipError_t e;
-    if ((e = hipHostMalloc((void **)&hA, tot, 0)) != hipSuccess || (e = hipHostMalloc((void **)&hB, tot, 0)) != hipSuccess ||
+    // host buffers exactly as jfsx_alloc_pinned makes the ring's staging
+    if ((e = hipHostMalloc((void **)&hA, tot, hipHostMallocPortable)) != hipSuccess ||
+        (e = hipHostMalloc((void **)&hB, tot, hipHostMallocPortable)) != hipSuccess ||
         (e = hipMalloc((void **)&dA, tot)) != hipSuccess || (e = hipMalloc((void **)&dB, tot)) != hipSuccess) {
         fail(e, __LINE__, "pcie probe buffers");
     } else {

@@ -1,11 +1,14 @@
 """Fill `roofline.traffic` / `binding` of suite bench lines that ran before
-profiles/r3/pmc_r3.json existed, with bench.py's own formula (pmc_traffic):
+their round's PMC summary existed, with bench.py's own formula (pmc_traffic):
 traffic = HBM bytes per plaintext byte of the variant's PMC passes x this
 line's plaintext bytes per launch.  The variant is the line's file name
 (bench_<variant>.json, the names scripts/gpu_r3_suite.sh gives both).  A
 filled line says so in roofline.traffic_filled_by.
 
-usage: python3 scripts/fill_traffic.py profiles/r3/pmc_r3.json profiles/r3/bench_*.json
+A traffic figure a line took from an older round's file (traffic_source
+under profiles/r2 or r3) is replaced by the newer summary's.
+
+usage: python3 scripts/fill_traffic.py profiles/r4/pmc_r4.json profiles/r4/bench_*.json
 """
 import json
 import os
@@ -27,14 +30,15 @@ def main(pmc_path, paths):
         if v is None or not plain:
             continue
         changed = False
-        if rf.get("traffic") is None and "bytes_per_plain_byte" in v:
+        older = str(rf.get("traffic_source") or "").startswith(("profiles/r2", "profiles/r3"))
+        if (rf.get("traffic") is None or older) and "bytes_per_plain_byte" in v:
             rf["traffic"] = int(v["bytes_per_plain_byte"] * plain)
-            rf["traffic_source"] = "profiles/r3/pmc_r3.json %s (%s; %s)" % (key, v.get("fetch_pass"),
-                                                                            v.get("write_pass"))
+            rf["traffic_source"] = "%s %s (%s; %s)" % (pmc_path, key, v.get("fetch_pass"), v.get("write_pass"))
             changed = True
-        if rf.get("binding") is None and ("lds_busy" in v or "valu_issue" in v):
-            b = {k: v[k] for k in ("lds_busy", "valu_issue", "lds_conflict_share") if k in v}
-            b["source"] = "profiles/r3/pmc_r3.json %s (%s)" % (key, v.get("lds_pass") or v.get("valu_pass"))
+        if rf.get("binding") is None and ("lds_busy" in v or "valu_issue" in v or "salu_issue" in v):
+            b = {k: v[k] for k in ("lds_busy", "valu_issue", "lds_conflict_share", "salu_issue", "salu_per_byte",
+                                   "valu_per_byte") if k in v}
+            b["source"] = "%s %s (%s)" % (pmc_path, key, v.get("lds_pass") or v.get("valu_pass") or v.get("salu_pass"))
             rf["binding"] = b
             changed = True
         if changed:

@@ -77,10 +77,13 @@ def main(roots):
                 vals[r["Counter_Name"]] = vals.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
         b = bench_line(d + ".log") or {}
         plain = (b.get("roofline") or {}).get("plain_bytes_per_launch")
-        rec = {"pass": os.path.relpath(d), "kernel_prefix": pref, "dispatch_id": last,
+        # a pass is named <suite>/pmc_<variant>__<set>; its raw counter values
+        # are kept under that key in "passes"
+        pname = os.path.relpath(d, os.path.dirname(root))
+        rec = {"pass": pname, "kernel_prefix": pref, "dispatch_id": last,
                "counters": vals, "plain_bytes_per_launch": plain,
                "bench_config": (b.get("config") or {}).get("workload")}
-        out["passes"]["%s__%s" % (variant, cset)] = rec
+        out["passes"][pname] = rec
         v = out["variants"].setdefault(variant, {"kernel_prefix": pref})
         if "FETCH_SIZE" in vals and plain:
             v["fetch_bytes"] = 2 * vals["FETCH_SIZE"] * 1024
