@@ -845,6 +845,7 @@ int run_codec(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, CodecOp op) {
     static const int zc_per_cu = getenv("JFSX_ZC_WAVES") ? std::max(1, std::min(11, atoi(getenv("JFSX_ZC_WAVES"))))
                                                          : kZcWavesPerCu;
     const int zc_waves = std::min(n, c->ncu * zc_per_cu);
+    static const bool zc_queue = getenv("JFSX_ZC_QUEUE") && atoi(getenv("JFSX_ZC_QUEUE")) == 1;
     // zstd decompression: block-parallel persistent waves unless
     // JFSX_ZSTD_SERIAL=1 selects the one-wave-per-object serial kernel (A/B)
     static const bool zd_serial = getenv("JFSX_ZSTD_SERIAL") && atoi(getenv("JFSX_ZSTD_SERIAL")) == 1;
@@ -903,7 +904,10 @@ int run_codec(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, CodecOp op) {
         launch_zstd_decompress(s, n, dz, dout, (uint8_t *)(w.d + o_tab), zd_waves);
         break;
     case kZstdComp:
-        launch_zstd_compress(s, n, zc_waves, dz, dout, (uint8_t *)(w.d + o_tab + 256));
+        // JFSX_ZC_QUEUE=1: ticket-queue object assignment (A/B; the word
+        // before the scratch is the ticket counter)
+        launch_zstd_compress(s, n, zc_waves, dz, dout, (uint8_t *)(w.d + o_tab + 256),
+                             zc_queue ? (uint32_t *)(w.d + o_tab) : nullptr);
         break;
     }
     if (c->timing) HIP_OK(hipEventRecord(c->ev_k1[0], s));

@@ -317,7 +317,8 @@ void launch_zstd_decompress(hipStream_t s, int n, const ZDev *blks, ZOut *outs, 
 constexpr size_t kZstdcScratch = 960 * 1024;
 constexpr size_t kZcScratchStride = kZstdcScratch;
 constexpr int kZcWavesPerCu = 8;
-void launch_zstd_compress(hipStream_t s, int n, int waves, const ZDev *blks, ZOut *outs, uint8_t *scratch);
+void launch_zstd_compress(hipStream_t s, int n, int waves, const ZDev *blks, ZOut *outs, uint8_t *scratch,
+                          uint32_t *queue);
 // batched RSA-OAEP unwrap (jfsx_rsa.hip): key = device jfsx_rsa::Key
 void async_detach(jfsx_ctx *c);  // jfsx_agg.cpp
 void launch_rsa_unwrap(hipStream_t s, const void *key, int n, const uint8_t *ct, uint32_t *mh, uint8_t *em,

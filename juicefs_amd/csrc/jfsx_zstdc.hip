@@ -829,8 +829,13 @@ __device__ uint64_t compress_object(const uint8_t *src, uint64_t n, uint8_t *dst
 // waiting for lane 0's next queue read while lane 0 was masked off -- a hang on
 // the first object, GPU-traced in round 3.)  ZDev.len = input bytes,
 // ZDev.cap >= ZSTD_compressBound.
+// queue != nullptr: after its first object (blockIdx.x) a wave takes the next
+// object index from a ticket counter (lane 0's vector atomic, made wave-uniform
+// by readfirstlane before the loop test), so a batch of more objects than
+// waves finishes in about n / W object times instead of ceil(n / W).
 __global__ __launch_bounds__(64) void zstd_compress_k(const ZDev *__restrict__ blks, ZOut *__restrict__ outs,
-                                                      uint8_t *__restrict__ scratch, int n) {
+                                                      uint8_t *__restrict__ scratch, int n,
+                                                      uint32_t *__restrict__ queue) {
     __shared__ jzc::Work W;
     const uint32_t lane = threadIdx.x;
     uint8_t *const sc = scratch + (size_t)blockIdx.x * kZcScratchStride;
@@ -840,7 +845,7 @@ __global__ __launch_bounds__(64) void zstd_compress_k(const ZDev *__restrict__ b
     uint8_t *const codes = lits + kZcLit;
     uint8_t *const body = codes + kZcCodes;
     uint16_t *const rec = (uint16_t *)(body + kZcBody);
-    for (int obj = (int)blockIdx.x; obj < n; obj += (int)gridDim.x) {
+    for (int obj = (int)blockIdx.x; obj < n;) {
         const ZDev b = blks[obj];
         ZT("zc: object %d len %lu\n", obj, (unsigned long)b.len);
 #ifdef JFSX_ZC_SCALAR
@@ -855,12 +860,21 @@ __global__ __launch_bounds__(64) void zstd_compress_k(const ZDev *__restrict__ b
             outs[obj].status = JFSX_OK;
         }
         __syncthreads();  // W and the scratch are reused by the next object
+        if (queue) {
+            uint32_t t = 0;
+            if (lane == 0) t = atomicAdd(queue, 1u);
+            obj = (int)gridDim.x + (int)__builtin_amdgcn_readfirstlane(t);
+        } else {
+            obj += (int)gridDim.x;
+        }
     }
 }
 
-void launch_zstd_compress(hipStream_t s, int n, int waves, const ZDev *blks, ZOut *outs, uint8_t *scratch) {
+void launch_zstd_compress(hipStream_t s, int n, int waves, const ZDev *blks, ZOut *outs, uint8_t *scratch,
+                          uint32_t *queue) {
     if (n <= 0) return;
-    hipLaunchKernelGGL(zstd_compress_k, dim3(waves), dim3(64), 0, s, blks, outs, scratch, n);
+    if (queue) (void)hipMemsetAsync(queue, 0, 4, s);
+    hipLaunchKernelGGL(zstd_compress_k, dim3(waves), dim3(64), 0, s, blks, outs, scratch, n, queue);
 }
 
 }  // namespace jfsx

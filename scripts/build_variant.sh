@@ -8,4 +8,5 @@ objs=$(ls _build/*.o | grep -v "/$SRCF.o" | grep -v "_var_")
 sched=""
 case $SRCF in jfsx_gcm.hip|jfsx_chacha.hip) sched="-mllvm -amdgpu-sched-strategy=iterative-ilp";; esac
 /opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-variable $sched "$@" -I../include -c csrc/$SRCF -o _build/_var_$V.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o _build/libjfsx_$V.so $objs _build/_var_$V.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o _build/libjfsx_$V.so.tmp $objs _build/_var_$V.o
+mv -f _build/libjfsx_$V.so.tmp _build/libjfsx_$V.so

@@ -36,6 +36,10 @@ run aggcodec_zstd --mode aggcodec --codec zstd --threads 20 --steps 2 --warmup 1
 run aggcodec_unzstd --mode aggcodec --codec unzstd --threads 20 --steps 2 --warmup 1 && \
 run unzstd_text_64g --mode unzstd --steps 5 --warmup 1 || exit 1
 fi
+if [ $what = agg_codec_zstd ]; then
+run aggcodec_zstd --mode aggcodec --codec zstd --threads 20 --steps 2 --warmup 1 && \
+run aggcodec_unzstd --mode aggcodec --codec unzstd --threads 20 --steps 2 --warmup 1 || exit 1
+fi
 if [ $what = prof ] || [ $what = all ]; then
 prof gcm --steps 10 --warmup 2 && prof gcm_ragged --ragged --steps 10 --warmup 2 && \
 prof open_gcm --mode open --steps 10 --warmup 2 && \
