@@ -636,7 +636,7 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
     // UR rows of one stream per iteration (2 in the 16-wave shape; the 8-wave
     // shape has twice the VGPRs and takes JFSX_HYB_UR): the UR AES chains
     // interleave, GHASH/CRC stay sequential (register peak of one row)
-    constexpr int UR = BS == 2 ? JFSX_HYB_UR : 2;
+    constexpr int UR = BS == 2 ? JFSX_HYB_UR : JFSX_UR0;
     if (NS == 1 && act[0] && rf >= r0 + UR) {
         uint4 nn[UR];
 #pragma unroll

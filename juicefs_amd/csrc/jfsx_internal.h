@@ -34,6 +34,10 @@ constexpr int kThreads = kWaves * 64;
 #endif
 // Two-row unrolled T-table loop (two AES chains interleaved); with the GHASH
 // quarters it fits the 128-VGPR cap (+2% measured).
+// rows per iteration of the default shape's T-table loop (2 fits 128 VGPRs)
+#ifndef JFSX_UR0
+#define JFSX_UR0 2
+#endif
 // rows per iteration of the 8-wave (BS = 2) shape's T-table loop
 #ifndef JFSX_HYB_UR
 #define JFSX_HYB_UR 4

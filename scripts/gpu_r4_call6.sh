@@ -17,3 +17,15 @@ bash scripts/gpu_r4_suite.sh r4f agg_codec_zstd
 s=gpurun_out/suite_r4f
 timeout -k 10 500 python3 bench.py --mem host --blocks 2048 --steps 8 --warmup 1 > $s/bench_ingest_gcm.json 2> $s/bench_ingest_gcm.err || { echo "ingest failed"; tail -5 $s/bench_ingest_gcm.err; exit 1; }
 echo "ingest: $(tail -1 $s/bench_ingest_gcm.json | cut -c1-160)"
+# GCM: 12 waves (3 per SIMD, 168 VGPRs) with 2 or 3 T-table rows per iteration
+# against the 16-wave default (parity first on the 3-row build)
+JFSX_LIB=juicefs_amd/_build/libjfsx_W12U3.so timeout -k 10 400 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fused_modes.py -x -q --timeout 120 --timeout-method thread > $out/w12u3_pytest.log 2>&1 || { echo "W12U3 parity failed"; tail -20 $out/w12u3_pytest.log; exit 1; }
+echo "W12U3 parity: $(tail -1 $out/w12u3_pytest.log)"
+gab() {
+  name=$1; lib=$2
+  JFSX_LIB=$lib timeout -k 10 200 python3 bench.py --blocks 4096 --steps 5 --warmup 1 --no-cpu --verify 0 > $out/gab_$name.json 2> $out/gab_$name.err || { echo "$name failed"; tail -5 $out/gab_$name.err; return 1; }
+  python3 -c "import json; d=json.loads(open('$out/gab_$name.json').read().splitlines()[-1]); print('%-8s value %8.2f kernel_ms %7.3f' % ('$name', d['value'], d['roofline']['kernel_avg_ms']))"
+}
+B=juicefs_amd/_build
+gab base1 juicefs_amd/libjfsx.so && gab w12u3 $B/libjfsx_W12U3.so && gab w12u2 $B/libjfsx_W12U2.so && \
+gab base2 juicefs_amd/libjfsx.so && gab w12u3b $B/libjfsx_W12U3.so
