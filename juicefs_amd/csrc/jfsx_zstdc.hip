@@ -30,6 +30,10 @@
 #include "jfsx_dev.h"
 #include "jfsx_zstdc.h"
 
+#ifndef JFSX_ZC_K0
+#define JFSX_ZC_K0 64
+#endif
+
 namespace jfsx {
 
 namespace {
@@ -171,8 +175,14 @@ __device__ uint32_t parse_fast_wave(const uint8_t *src, int32_t istart, int32_t 
     }
     const uint8_t *const iendp = src + iend;
     gu32c *const T = (gu32c *)htab;
+    // speculation width: a step evaluates the next K iterations of the serial
+    // loop (a prefix, so the semantics are unchanged).  Each iteration costs a
+    // random hash-table read and a random candidate read; on text the first
+    // success comes within a few iterations, so after every match a step starts
+    // with JFSX_ZC_K0 lanes and doubles K on each step without a success.
+    uint32_t K = JFSX_ZC_K0;
     while (ip0 + 1 < ilimit) {
-        // ---- one search step: iterations j = 0..63 of the serial loop ----
+        // ---- one search step: iterations j = 0..K-1 of the serial loop ----
         const int32_t d0 = ip0 - anchor;
         int32_t d;
         if (d0 < 2) {
@@ -180,13 +190,14 @@ __device__ uint32_t parse_fast_wave(const uint8_t *src, int32_t istart, int32_t 
         } else {
             int32_t x = d0;
             d = d0;
-            for (uint32_t j = 0; j < 64; j++) {
+            for (uint32_t j = 0; j < K; j++) {
                 if (lane == j) d = x;
                 x += (x >> 7) + 2;
             }
         }
         const int32_t p = anchor + d;
-        const bool valid = p + 1 < ilimit;
+        const uint64_t amask = K >= 64 ? ~0ull : ((1ull << K) - 1ull);
+        const bool valid = lane < K && p + 1 < ilimit;
         const uint64_t vmask = ballot(valid);
         const int32_t pc = valid ? p : ip0;
         uint64_t w0, w1;
@@ -248,10 +259,12 @@ __device__ uint32_t parse_fast_wave(const uint8_t *src, int32_t istart, int32_t 
         if (wA) T[A] = (uint32_t)(p + 1);
         if (wB) T[B] = (uint32_t)(p + 2);
         if (!sm) {
-            if (vmask != ~0ull) break;  // the serial loop ends inside this step
-            ip0 = anchor + unis(readlanes(d + (d >> 7) + 2, 63));
+            if (vmask != amask) break;  // the serial loop ends inside this step
+            ip0 = anchor + unis(readlanes(d + (d >> 7) + 2, (int)K - 1));
+            K = K < 64 ? 2 * K : 64;
             continue;
         }
+        K = JFSX_ZC_K0;
         // ---- the match of the first successful iteration f ----
         const int f = __builtin_ctzll(sm);
         const int32_t pf = unis(readlanes(p, f));
