@@ -277,6 +277,9 @@ __device__ unsigned long long g_lz4_stamps[8];
 
 // One wave per block.  ZDev.len = input bytes, ZDev.cap >= LZ4_compressBound
 // (checked on the host); ZOut.out_len = compressed bytes.
+#ifndef JFSX_LZ4_K0
+#define JFSX_LZ4_K0 4
+#endif
 __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ blks, ZOut *__restrict__ outs,
                                                      uint32_t *__restrict__ tabs) {
 #ifdef JFSX_LZ4_LDS_TABLE
@@ -331,12 +334,20 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
             {
                 const uint32_t q0 = ip;
                 if (!iwin_has(W, I, anchor, q0 - anchor + 72)) iwin_load(W, I, anchor, lane);
-                for (uint32_t k0 = 0;; k0 += 64) {
+                // speculation width: a step runs the next K probes (a prefix of
+                // the serial search, so the output is unchanged); a search
+                // starts with JFSX_LZ4_K0 lanes and doubles K on each step
+                // without a match -- on text the first match comes within a few
+                // probes, and every probe costs a random table read and a random
+                // candidate read
+                uint32_t K = JFSX_LZ4_K0;
+                for (uint32_t k0 = 0;; k0 += K, K = K < 64 ? 2 * K : 64) {
                     const uint32_t k = k0 + lane;
                     const uint32_t p = q0 + probe_off(k);
-                    const bool valid = q0 + probe_off(k + 1) <= mflimit1;  // else this probe ends the search
+                    const bool valid = lane < K && q0 + probe_off(k + 1) <= mflimit1;  // else this probe ends the search
+                    const uint64_t amask = K >= 64 ? ~0ull : ((1ull << K) - 1ull);
                     const uint32_t pc = valid ? p : q0;
-                    const uint32_t pf = q0 + probe_off(k0), pl = q0 + probe_off(k0 + 63);
+                    const uint32_t pf = q0 + probe_off(k0), pl = q0 + probe_off(k0 + K - 1);
                     uint32_t cur, b4;
                     if (iwin_has(W, I, pf, pl - pf + 8)) {
                         cur = iwin_u32_lane(W, I, pc, b4);
@@ -390,7 +401,7 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
                         found = true;
                         break;
                     }
-                    if (vmask != ~0ull) break;
+                    if (vmask != amask) break;
                 }
             }
             LZ_SEC(0);  // search

@@ -31,7 +31,7 @@
 #include "jfsx_zstdc.h"
 
 #ifndef JFSX_ZC_K0
-#define JFSX_ZC_K0 64
+#define JFSX_ZC_K0 4
 #endif
 
 namespace jfsx {
@@ -218,15 +218,30 @@ __device__ uint32_t parse_fast_wave(const uint8_t *src, int32_t istart, int32_t 
             wA = lane == 0 && A != B;
             wB = lane == 0;
         } else {
-            // lanes whose writes share this lane's buckets (hashLog x 2 ballots)
+            // lanes whose writes share this lane's buckets: bit i of eqXY is
+            // set when lane i's hash Y equals this lane's hash X
             uint64_t eqAA = ~0ull, eqBA = ~0ull, eqAB = ~0ull, eqBB = ~0ull;
-            for (uint32_t bit = 0; bit < hlog; bit++) {
-                const bool a = (A >> bit) & 1u, b = (B >> bit) & 1u;
-                const uint64_t bA = ballot(a), bB = ballot(b);
-                eqAA &= a ? bA : ~bA;
-                eqBA &= a ? bB : ~bB;
-                eqAB &= b ? bA : ~bA;
-                eqBB &= b ? bB : ~bB;
+            if (K <= 16) {
+                // a narrow step: compare with each active lane's hashes directly
+                eqAA = eqBA = eqAB = eqBB = 0ull;
+                for (uint32_t i = 0; i < K; i++) {
+                    const uint32_t Ai = readlane(A, (int)i), Bi = readlane(B, (int)i);
+                    const uint64_t bit = 1ull << i;
+                    eqAA |= A == Ai ? bit : 0ull;
+                    eqBA |= A == Bi ? bit : 0ull;
+                    eqAB |= B == Ai ? bit : 0ull;
+                    eqBB |= B == Bi ? bit : 0ull;
+                }
+            } else {
+                // hashLog x 2 ballots
+                for (uint32_t bit = 0; bit < hlog; bit++) {
+                    const bool a = (A >> bit) & 1u, b = (B >> bit) & 1u;
+                    const uint64_t bA = ballot(a), bB = ballot(b);
+                    eqAA &= a ? bA : ~bA;
+                    eqBA &= a ? bB : ~bB;
+                    eqAB &= b ? bA : ~bA;
+                    eqBB &= b ? bB : ~bB;
+                }
             }
             eqAA &= vmask;
             eqBA &= vmask;
