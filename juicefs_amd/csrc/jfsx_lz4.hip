@@ -369,13 +369,22 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
                         okm = 1ull;
                         writer = lane == 0;
                     } else {
-                        // lanes of the same bucket (13 ballots over the hash bits)
+                        // lanes of the same bucket: bit i of eq is set when lane
+                        // i's hash equals this lane's
                         uint64_t eq = ~0ull;
+                        if (K <= 16) {
+                            // a narrow step: compare with each active lane's hash
+                            eq = 0ull;
+                            for (uint32_t i = 0; i < K; i++)
+                                eq |= h == __builtin_amdgcn_readlane(h, (int)i) ? 1ull << i : 0ull;
+                        } else {
+                            // 13 ballots over the hash bits
 #pragma unroll
-                        for (int bit = 0; bit < 13; bit++) {
-                            const bool hb = (h >> bit) & 1u;
-                            const uint64_t bl = ballot(hb);
-                            eq &= hb ? bl : ~bl;
+                            for (int bit = 0; bit < 13; bit++) {
+                                const bool hb = (h >> bit) & 1u;
+                                const uint64_t bl = ballot(hb);
+                                eq &= hb ? bl : ~bl;
+                            }
                         }
                         const uint64_t below = lanes_below(lane);
                         const uint64_t prev = eq & below & vmask;
