@@ -30,6 +30,9 @@
 #include "jfsx_dev.h"
 #include "jfsx_zstdc.h"
 
+#ifndef JFSX_ZC_WIN
+#define JFSX_ZC_WIN 0
+#endif
 #ifndef JFSX_ZC_K0
 #define JFSX_ZC_K0 4
 #endif
@@ -153,6 +156,110 @@ __device__ __forceinline__ void store_seq_wave(WSeq &ss, const uint8_t *lits, ui
     }
     ss.nseq++;
     ss.nlit += litLen;
+}
+
+// ---------------------------------------------------------------------------
+// Register windows (JFSX_ZC_WIN): 256 input bytes in the wave's VGPRs, lane L
+// holding the image dword at w0 + 4L (zero past the object's end).  A read
+// inside a window is a ds_bpermute (per-lane position) or v_readlane (uniform
+// position), not a memory round trip; the search steps, the literal copies and
+// the hash inserts after a match read from them, and the catch-up bytes and
+// the match length come from one round of loads (count_back).
+// ---------------------------------------------------------------------------
+struct ZImg {  // the object as an aligned image: byte pos at offset pos + sh of al
+    const uint8_t *al;
+    uint32_t sh, n;
+};
+struct ZWin {
+    uint32_t w0, w;
+};
+__device__ __forceinline__ void zw_load(ZWin &W, const ZImg &I, uint32_t pos, uint32_t lane) {
+    W.w0 = (pos + I.sh) & ~3u;
+    const uint32_t o = W.w0 + 4 * lane;
+    W.w = o < I.n + I.sh ? ld32a(I.al + o) : 0u;
+}
+// [pos, pos + len) inside the window (pos may be any int)
+__device__ __forceinline__ bool zw_has(const ZWin &W, const ZImg &I, int32_t pos, uint32_t len) {
+    const int64_t x = (int64_t)pos + I.sh;
+    return x >= (int64_t)W.w0 && x + len <= (int64_t)W.w0 + 256;
+}
+// 4 bytes at a per-lane position inside the window (zw_has(pos, 8))
+__device__ __forceinline__ uint32_t zw_u32_lane(const ZWin &W, const ZImg &I, int32_t pos) {
+    const uint32_t r = (uint32_t)pos + I.sh - W.w0, i = r >> 2, sh = r & 3;
+    const uint32_t d0 = __shfl(W.w, (int)(i & 63), 64), d1 = __shfl(W.w, (int)((i + 1) & 63), 64);
+    return __builtin_amdgcn_alignbyte(d1, d0, sh);
+}
+// 8 bytes at a uniform position inside the window (zw_has(pos, 12))
+__device__ __forceinline__ uint64_t zw_u64(const ZWin &W, const ZImg &I, int32_t pos) {
+    const uint32_t r = (uint32_t)pos + I.sh - W.w0, i = r >> 2, sh = r & 3;
+    const uint32_t d0 = readlane(W.w, (int)i), d1 = readlane(W.w, (int)i + 1), d2 = readlane(W.w, (int)i + 2);
+    return (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32);
+}
+// load9 from the window: bytes [p, p + 8) and [p + 1, p + 9) (zw_has(p, 12))
+__device__ __forceinline__ void zw_load9(const ZWin &W, const ZImg &I, int32_t p, uint64_t &w0, uint64_t &w1) {
+    const uint32_t r = (uint32_t)p + I.sh - W.w0, i = r >> 2, sh = r & 3;
+    const uint32_t d0 = __shfl(W.w, (int)(i & 63), 64), d1 = __shfl(W.w, (int)((i + 1) & 63), 64),
+                   d2 = __shfl(W.w, (int)((i + 2) & 63), 64);
+    w0 = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32);
+    if (sh == 3) {
+        w1 = (uint64_t)d1 | ((uint64_t)d2 << 32);
+    } else {
+        w1 = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh + 1) |
+             ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh + 1) << 32);
+    }
+}
+// ZSTD_storeSeq with the literals [pos, pos + litLen) taken from the window
+__device__ __forceinline__ void store_seq_win(WSeq &ss, const ZWin &W, const ZImg &I, int32_t pos, uint32_t litLen,
+                                              uint32_t offCode, uint32_t mlBase, uint32_t lane) {
+    const uint32_t r = (uint32_t)pos + I.sh - W.w0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t j = lane + 64 * k, q = r + j;
+        const uint32_t dw = __shfl(W.w, (int)((q >> 2) & 63), 64);
+        if (j < litLen) *(gu8c *)(ss.lit + ss.nlit + j) = (uint8_t)(dw >> (8 * (q & 3)));
+    }
+    if (litLen > 0xFFFF) ss.long_id = 1, ss.long_pos = ss.nseq;
+    if (mlBase > 0xFFFF) ss.long_id = 2, ss.long_pos = ss.nseq;
+    if (lane == 0) {
+        jzc::SeqDef d;
+        d.offset = offCode + 1;
+        d.ll = (uint16_t)litLen;
+        d.ml = (uint16_t)mlBase;
+        ss.seq[ss.nseq] = d;
+    }
+    ss.nseq++;
+    ss.nlit += litLen;
+}
+// ZSTD_count(ipX + 4, mX + 4, limit) and, in the same round of loads, the
+// catch-up: how many of the limc (<= 64) bytes before ipX and mX are equal
+// (back; 64 when all 64 were).  C receives the window at ipX + 4.
+__device__ uint32_t count_back(ZWin &C, const ZImg &I, const uint8_t *src, int32_t ipX, int32_t mX, int32_t limit,
+                               uint32_t limc, uint32_t &back, uint32_t lane) {
+    const int32_t aa = ipX + 4, off = ipX - mX;
+    zw_load(C, I, (uint32_t)aa, lane);
+    const int32_t lp = (int32_t)(C.w0 + 4 * lane) - (int32_t)I.sh;  // input position of this lane's window dword
+    const int32_t mp = lp - off;                                      // >= 1: mX >= 0 and lp >= aa - 3
+    const uint32_t mw = ld32u(src + (mp + 4 <= (int32_t)I.n ? mp : (int32_t)I.n - 4));
+    bool ceq = false;
+    if (lane < limc) ceq = ld8(src + ipX - 1 - (int32_t)lane) == ld8(src + mX - 1 - (int32_t)lane);
+    const uint64_t cst = ballot(!ceq);
+    back = cst ? (uint32_t)__builtin_ctzll(cst) : 64u;
+    // first byte of this lane's 4 that stops the count: at or after aa, and
+    // differing or at or past limit
+    const int32_t k = aa - lp, m = limit - lp;
+    const uint32_t pre = k > 0 ? (0xffffffffu << (8 * (uint32_t)k)) : 0xffffffffu;
+    const uint32_t lim = m >= 4 ? 0u : (m <= 0 ? 0xffffffffu : (0xffffffffu << (8 * (uint32_t)m)));
+    const uint32_t y = ((C.w ^ mw) | lim) & pre;
+    const uint32_t si = y ? (uint32_t)__builtin_ctz(y) >> 3 : 4u;
+    const uint64_t sm = ballot(si < 4);
+    if (sm) {
+        const int L = __builtin_ctzll(sm);
+        return uni((uint32_t)((int32_t)(C.w0 + 4 * L) - (int32_t)I.sh + (int32_t)readlane(si, L) - aa));
+    }
+    // a long match: continue 256 bytes per step from the window's end
+    const uint32_t avail = limit > aa ? (uint32_t)(limit - aa) : 0u;
+    uint32_t mc = (uint32_t)((int32_t)(C.w0 + 256) - (int32_t)I.sh - aa);
+    return uni(mc >= avail ? avail : mc + count_wave(src + aa + mc, src + mX + 4 + mc, src + limit, lane));
 }
 
 // jzc::parse_fast on the wave: same sequences, same table, same repcodes.
@@ -333,6 +440,233 @@ __device__ uint32_t parse_fast_wave(const uint8_t *src, int32_t istart, int32_t 
                 anchor = ip0;
             }
         }
+    }
+    rep[0] = offset_1 ? offset_1 : offsetSaved;
+    rep[1] = offset_2 ? offset_2 : offsetSaved;
+    return (uint32_t)(iend - anchor);
+}
+
+// parse_fast_wave with the input reads served from register windows where
+// they fall inside one (JFSX_ZC_WIN): the same sequences, table and repcodes.
+// W covers the search step's positions; C, loaded by count_back at the
+// match, covers the match's end, the next anchor and often the next step.
+__device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t istart, int32_t iend, uint32_t *htab,
+                                      jzc::Params P, uint32_t rep[2], WSeq &ss, uint32_t lane) {
+    const uint32_t hlog = P.hlog, mls = P.mls;
+    const int32_t endIndex = iend + 1;
+    const int32_t prefixStartIndex = jzc::prefix_start_index(endIndex, P.wlog);
+    const int32_t prefixStart = prefixStartIndex - 1;
+    const int32_t ilimit = iend - 8;
+    int32_t ip0 = istart, anchor = istart;
+    uint32_t offset_1 = rep[0], offset_2 = rep[1], offsetSaved = 0;
+    ip0 += (ip0 == prefixStart);
+    {
+        const int32_t cur = ip0 + 1;
+        const int32_t windowLow = jzc::prefix_start_index(cur, P.wlog);
+        const uint32_t maxRep = (uint32_t)(cur - windowLow);
+        if (offset_2 > maxRep) offsetSaved = offset_2, offset_2 = 0;
+        if (offset_1 > maxRep) offsetSaved = offset_1, offset_1 = 0;
+    }
+    const uint8_t *const iendp = src + iend;
+    gu32c *const T = (gu32c *)htab;
+    // speculation width: a step evaluates the next K iterations of the serial
+    // loop (a prefix, so the semantics are unchanged).  Each iteration costs a
+    // random hash-table read and a random candidate read; on text the first
+    // success comes within a few iterations, so after every match a step starts
+    // with JFSX_ZC_K0 lanes and doubles K on each step without a success.
+    uint32_t K = JFSX_ZC_K0;
+    ZWin W, C;
+    W.w0 = 0xfffff000u;  // empty
+    W.w = 0;
+    while (ip0 + 1 < ilimit) {
+        // ---- one search step: iterations j = 0..K-1 of the serial loop ----
+        const int32_t d0 = ip0 - anchor;
+        int32_t d;
+        if (d0 < 2) {
+            d = d0 + 2 * (int32_t)lane;  // every step is 2 while d < 128
+        } else {
+            int32_t x = d0;
+            d = d0;
+            for (uint32_t j = 0; j < K; j++) {
+                if (lane == j) d = x;
+                x += (x >> 7) + 2;
+            }
+        }
+        const int32_t p = anchor + d;
+        const uint64_t amask = K >= 64 ? ~0ull : ((1ull << K) - 1ull);
+        const bool valid = lane < K && p + 1 < ilimit;
+        const uint64_t vmask = ballot(valid);
+        const int32_t pc = valid ? p : ip0;
+        // the step's positions [ip0, p of lane K-1] (+ 8 bytes each, + the
+        // hash insert at pf + 2) from W, reloaded at ip0 when it does not cover them
+        const int32_t phi = unis(readlanes(p, (int)K - 1));
+        const uint32_t span = (uint32_t)(phi - ip0) + 16u;
+        bool win = zw_has(W, I, ip0, span);
+        if (!win && span <= 240u) {
+            zw_load(W, I, (uint32_t)ip0, lane);
+            win = true;
+        }
+        uint64_t w0, w1;
+        if (win)
+            zw_load9(W, I, pc, w0, w1);
+        else
+            load9(src, pc, w0, w1);
+        const uint32_t A = hash_w(w0, hlog, mls), B = hash_w(w1, hlog, mls);
+        const int32_t tA0 = (int32_t)T[A], tB0 = (int32_t)T[B];
+        const uint32_t v0 = (uint32_t)w0, v1 = (uint32_t)w1, r2 = (uint32_t)(w0 >> 16);
+        // the repcode candidate: from W when every active lane's lies inside it
+        const int32_t q = pc + 2 - (int32_t)offset_1;
+        const bool rq = valid && offset_1 > 0;
+        bool okr;
+        if (win && !ballot(rq && !zw_has(W, I, q, 8)))
+            okr = rq && zw_u32_lane(W, I, q) == r2;
+        else
+            okr = rq && ld32u(src + q) == r2;
+        bool ok0 = valid && tA0 > prefixStartIndex && ld32u(src + tA0 - 1) == v0;
+        bool ok1 = valid && tB0 > prefixStartIndex && ld32u(src + tB0 - 1) == v1;
+        int32_t tA = tA0, tB = tB0;
+        uint64_t sm = ballot(okr || ok0 || ok1);
+        uint64_t commit;
+        bool wA, wB;
+        if (sm & 1ull) {
+            // the first iteration succeeds on its own: it alone ran
+            commit = 1ull;
+            wA = lane == 0 && A != B;
+            wB = lane == 0;
+        } else {
+            // lanes whose writes share this lane's buckets: bit i of eqXY is
+            // set when lane i's hash Y equals this lane's hash X
+            uint64_t eqAA = ~0ull, eqBA = ~0ull, eqAB = ~0ull, eqBB = ~0ull;
+            if (K <= 16) {
+                // a narrow step: compare with each active lane's hashes directly
+                eqAA = eqBA = eqAB = eqBB = 0ull;
+                for (uint32_t i = 0; i < K; i++) {
+                    const uint32_t Ai = readlane(A, (int)i), Bi = readlane(B, (int)i);
+                    const uint64_t bit = 1ull << i;
+                    eqAA |= A == Ai ? bit : 0ull;
+                    eqBA |= A == Bi ? bit : 0ull;
+                    eqAB |= B == Ai ? bit : 0ull;
+                    eqBB |= B == Bi ? bit : 0ull;
+                }
+            } else {
+                // hashLog x 2 ballots
+                for (uint32_t bit = 0; bit < hlog; bit++) {
+                    const bool a = (A >> bit) & 1u, b = (B >> bit) & 1u;
+                    const uint64_t bA = ballot(a), bB = ballot(b);
+                    eqAA &= a ? bA : ~bA;
+                    eqBA &= a ? bB : ~bB;
+                    eqAB &= b ? bA : ~bA;
+                    eqBB &= b ? bB : ~bB;
+                }
+            }
+            eqAA &= vmask;
+            eqBA &= vmask;
+            eqAB &= vmask;
+            eqBB &= vmask;
+            const uint64_t below = lanes_below(lane), above = lanes_above(lane);
+            // reads: the latest earlier write to the bucket (B after A within an iteration)
+            {
+                const uint64_t ea = eqAA & below, eb = eqBA & below;
+                const int ia = ea ? 63 - __builtin_clzll(ea) : -1, ib = eb ? 63 - __builtin_clzll(eb) : -1;
+                const int src_l = ib >= ia ? ib : ia;
+                const int32_t pv = __shfl(p, src_l < 0 ? (int)lane : src_l, 64);
+                if (src_l >= 0) tA = pv + (ib >= ia ? 2 : 1);
+            }
+            {
+                const uint64_t ea = eqAB & below, eb = eqBB & below;
+                const int ia = ea ? 63 - __builtin_clzll(ea) : -1, ib = eb ? 63 - __builtin_clzll(eb) : -1;
+                const int src_l = ib >= ia ? ib : ia;
+                const int32_t pv = __shfl(p, src_l < 0 ? (int)lane : src_l, 64);
+                if (src_l >= 0) tB = pv + (ib >= ia ? 2 : 1);
+            }
+            if (tA != tA0) ok0 = valid && tA > prefixStartIndex && ld32u(src + tA - 1) == v0;
+            if (tB != tB0) ok1 = valid && tB > prefixStartIndex && ld32u(src + tB - 1) == v1;
+            sm = ballot(okr || ok0 || ok1);
+            commit = sm ? ((sm & (0ull - sm)) << 1) - 1ull : vmask;  // iterations that ran
+            const bool in = (commit >> lane) & 1ull;
+            wA = in && A != B && !((eqAA | eqBA) & above & commit);
+            wB = in && !((eqAB | eqBB) & above & commit);
+        }
+        if (wA) T[A] = (uint32_t)(p + 1);
+        if (wB) T[B] = (uint32_t)(p + 2);
+        if (!sm) {
+            if (vmask != amask) break;  // the serial loop ends inside this step
+            ip0 = anchor + unis(readlanes(d + (d >> 7) + 2, (int)K - 1));
+            K = K < 64 ? 2 * K : 64;
+            continue;
+        }
+        K = JFSX_ZC_K0;
+        // ---- the match of the first successful iteration f ----
+        const int f = __builtin_ctzll(sm);
+        const int32_t pf = unis(readlanes(p, f));
+        const bool fr = (readlane((uint32_t)okr, f) & 1u) != 0, f0 = (readlane((uint32_t)ok0, f) & 1u) != 0;
+        const int32_t current0 = pf + 1;
+        int32_t match0;
+        uint32_t mLength, offcode;
+        uint32_t back;
+        if (fr) {
+            // the repcode match extends one byte back when ip2[-1] == repMatch[-1]
+            const int32_t ip2 = pf + 2, repMatch = ip2 - (int32_t)offset_1;
+            const uint32_t mc = count_back(C, I, src, ip2, repMatch, iend, 1u, back, lane);
+            ip0 = ip2 - (int32_t)back;
+            match0 = repMatch - (int32_t)back;
+            mLength = 4 + back + mc;
+            offcode = 0;
+        } else {
+            int32_t ipX;
+            if (f0) {
+                ipX = pf;
+                match0 = unis(readlanes(tA, f)) - 1;
+            } else {
+                ipX = pf + 1;
+                match0 = unis(readlanes(tB, f)) - 1;
+            }
+            offset_2 = offset_1;
+            offset_1 = (uint32_t)(ipX - match0);
+            offcode = offset_1 + 2;
+            const uint32_t lim = (uint32_t)min(ipX - anchor, match0 - prefixStart);
+            const uint32_t mc = count_back(C, I, src, ipX, match0, iend, lim < 64u ? lim : 64u, back, lane);
+            if (back == 64u && lim > 64u) back = 64u + back_wave(src + ipX - 64, src + match0 - 64, lim - 64u, lane);
+            ip0 = ipX - (int32_t)back;
+            match0 -= (int32_t)back;
+            mLength = 4 + back + mc;
+        }
+        mLength = uni(mLength);
+        if (zw_has(W, I, anchor, (uint32_t)(ip0 - anchor)))
+            store_seq_win(ss, W, I, anchor, (uint32_t)(ip0 - anchor), offcode, mLength - 3, lane);
+        else
+            store_seq_wave(ss, src + anchor, (uint32_t)(ip0 - anchor), offcode, mLength - 3, lane);
+        ip0 += (int32_t)mLength;
+        anchor = ip0;
+        if (ip0 <= ilimit) {
+            {
+                const uint64_t h1 = zw_has(W, I, current0 + 1, 12) ? zw_u64(W, I, current0 + 1) : ld64u(src + current0 + 1);
+                const uint64_t h2 = zw_has(C, I, ip0 - 2, 12) ? zw_u64(C, I, ip0 - 2) : ld64u(src + ip0 - 2);
+                if (lane == 0) {
+                    T[hash_w(h1, hlog, mls)] = (uint32_t)(current0 + 2);
+                    T[hash_w(h2, hlog, mls)] = (uint32_t)(ip0 - 1);
+                }
+            }
+            for (;;) {
+                if (!(ip0 <= ilimit && offset_2 > 0)) break;
+                const uint32_t a = zw_has(C, I, ip0, 8) ? (uint32_t)zw_u64(C, I, ip0) : uni(ld32u(src + ip0));
+                const int32_t rp = ip0 - (int32_t)offset_2;
+                const uint32_t bq = zw_has(C, I, rp, 12) ? (uint32_t)zw_u64(C, I, rp) : uni(ld32u(src + rp));
+                if (a != bq) break;
+                const uint64_t h3 = zw_has(C, I, ip0, 12) ? zw_u64(C, I, ip0) : ld64u(src + ip0);
+                uint32_t b0;
+                const uint32_t rLength = count_back(C, I, src, ip0, rp, iend, 0u, b0, lane) + 4;
+                const uint32_t t = offset_2;
+                offset_2 = offset_1;
+                offset_1 = t;
+                if (lane == 0) T[hash_w(h3, hlog, mls)] = (uint32_t)(ip0 + 1);
+                ip0 += (int32_t)rLength;
+                store_seq_wave(ss, src + anchor, 0, 0, rLength - 3, lane);
+                anchor = ip0;
+            }
+        }
+        // the next search starts at anchor: C often covers it already
+        if (zw_has(C, I, anchor, 2 * JFSX_ZC_K0 + 16)) W = C;
     }
     rep[0] = offset_1 ? offset_1 : offsetSaved;
     rep[1] = offset_2 ? offset_2 : offsetSaved;
@@ -766,6 +1100,12 @@ __device__ uint64_t block_body_wave(jzc::Work &W, const WSeq &ss, uint8_t *codes
 }
 
 // ZSTD_compress(level 1) of one object by the wave
+#ifdef JFSX_ZC_STAMP
+// diagnostic build only: the wave's wall-clock ticks (100 MHz) in the parse
+// and the entropy stage, and the sequences found (one wave per workgroup, so
+// LDS words are per wave); waves 0..1 print them per object
+__shared__ uint64_t g_zc_parse, g_zc_entropy, g_zc_nseq;
+#endif
 __device__ uint64_t compress_object(const uint8_t *src, uint64_t n, uint8_t *dst, uint32_t *htab,
                                     jzc::SeqDef *seqs, uint8_t *lits, uint8_t *codes, uint8_t *body, uint16_t *rec,
                                     jzc::Work &W, uint32_t lane) {
@@ -798,7 +1138,20 @@ __device__ uint64_t compress_object(const uint8_t *src, uint64_t n, uint8_t *dst
             uint32_t nrep[2] = {rep[0], rep[1]};
             __syncthreads();  // the table clear / last block's work has landed
             ZT("zc: parse block at %lu bs %u\n", (unsigned long)pos, bs);
+#ifdef JFSX_ZC_STAMP
+            const uint64_t t_p0 = wall_clock64();
+#endif
+#if JFSX_ZC_WIN
+            const ZImg I{(const uint8_t *)((uintptr_t)src & ~(uintptr_t)3), (uint32_t)((uintptr_t)src & 3), (uint32_t)n};
+            const uint32_t lastLL =
+                parse_fast_wave_w(src, I, (int32_t)pos, (int32_t)(pos + bs), htab, P, nrep, ss, lane);
+#else
             const uint32_t lastLL = parse_fast_wave(src, (int32_t)pos, (int32_t)(pos + bs), htab, P, nrep, ss, lane);
+#endif
+#ifdef JFSX_ZC_STAMP
+            const uint64_t t_p1 = wall_clock64();
+            if (lane == 0) g_zc_parse += t_p1 - t_p0, g_zc_nseq += ss.nseq;
+#endif
             ZT("zc: parsed nseq %u lastLL %u\n", ss.nseq, lastLL);
             for (uint32_t o = lane; o < lastLL; o += 64)
                 *(gu8c *)(lits + ss.nlit + o) = (uint8_t)ld8(src + pos + bs - lastLL + o);
@@ -813,6 +1166,9 @@ __device__ uint64_t compress_object(const uint8_t *src, uint64_t n, uint8_t *dst
 #else
             cSize = block_body_wave(W, ss, codes, rec, body, bs, lane);
             __syncthreads();
+#endif
+#ifdef JFSX_ZC_STAMP
+            if (lane == 0) g_zc_entropy += wall_clock64() - t_p1;
 #endif
             if (!first && cSize < jzc::kRleMaxLength) {
                 const uint32_t b0 = ld8(ip);
@@ -880,7 +1236,17 @@ __global__ __launch_bounds__(64) void zstd_compress_k(const ZDev *__restrict__ b
         uint64_t r = 0;
         if (lane == 0) r = jzc::compress_frame(b.src, b.len, b.dst, htab, seqs, lits, codes, body, W);
 #else
+#ifdef JFSX_ZC_STAMP
+        if (lane == 0) g_zc_parse = g_zc_entropy = g_zc_nseq = 0;
+        const uint64_t t_o0 = wall_clock64();
+#endif
         const uint64_t r = compress_object(b.src, b.len, b.dst, htab, seqs, lits, codes, body, rec, W, lane);
+#ifdef JFSX_ZC_STAMP
+        if (lane == 0 && blockIdx.x < 2)
+            printf("zc-stamp wave %u obj %d len %lu out %lu total %lu parse %lu entropy %lu nseq %lu (100 MHz ticks)\n",
+                   blockIdx.x, obj, (unsigned long)b.len, (unsigned long)r, (unsigned long)(wall_clock64() - t_o0),
+                   (unsigned long)g_zc_parse, (unsigned long)g_zc_entropy, (unsigned long)g_zc_nseq);
+#endif
 #endif
         ZT("zc: object %d -> %lu\n", obj, (unsigned long)r);
         if (lane == 0) {
