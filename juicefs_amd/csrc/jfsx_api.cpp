@@ -841,8 +841,8 @@ int run_codec(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, CodecOp op) {
     int rc;
     Workspace &w = c->ws[0];
     // zstd compression: persistent waves per CU (JFSX_ZC_WAVES overrides the
-    // default for A/B; LDS allows 11, VGPRs 12)
-    static const int zc_per_cu = getenv("JFSX_ZC_WAVES") ? std::max(1, std::min(11, atoi(getenv("JFSX_ZC_WAVES"))))
+    // default for A/B; LDS and VGPRs allow 16)
+    static const int zc_per_cu = getenv("JFSX_ZC_WAVES") ? std::max(1, std::min(16, atoi(getenv("JFSX_ZC_WAVES"))))
                                                          : kZcWavesPerCu;
     const int zc_waves = std::min(n, c->ncu * zc_per_cu);
     static const bool zc_queue = getenv("JFSX_ZC_QUEUE") && atoi(getenv("JFSX_ZC_QUEUE")) == 1;

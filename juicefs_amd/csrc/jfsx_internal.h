@@ -320,7 +320,7 @@ void launch_zstd_decompress(hipStream_t s, int n, const ZDev *blks, ZOut *outs, 
 // each owns kZstdcScratch bytes of scratch (hash table, sequences, literals)
 constexpr size_t kZstdcScratch = 960 * 1024;
 constexpr size_t kZcScratchStride = kZstdcScratch;
-constexpr int kZcWavesPerCu = 8;
+constexpr int kZcWavesPerCu = 16;
 void launch_zstd_compress(hipStream_t s, int n, int waves, const ZDev *blks, ZOut *outs, uint8_t *scratch,
                           uint32_t *queue);
 // batched RSA-OAEP unwrap (jfsx_rsa.hip): key = device jfsx_rsa::Key

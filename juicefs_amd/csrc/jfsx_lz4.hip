@@ -341,7 +341,7 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
                 // probes, and every probe costs a random table read and a random
                 // candidate read
                 uint32_t K = JFSX_LZ4_K0;
-                for (uint32_t k0 = 0;; k0 += K, K = K < 64 ? 2 * K : 64) {
+                for (uint32_t k0 = 0;; k0 += K, K = K < 32 ? 2 * K : 64) {
                     const uint32_t k = k0 + lane;
                     const uint32_t p = q0 + probe_off(k);
                     const bool valid = lane < K && q0 + probe_off(k + 1) <= mflimit1;  // else this probe ends the search

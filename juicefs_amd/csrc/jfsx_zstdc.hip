@@ -25,16 +25,28 @@
 //     (up to the first success) stores.
 //   * backward catch-up and the match-length count run 64 / 256 bytes per
 //     step with a ballot for the first difference.
+//   * the input bytes a step, a match's catch-up and length, its literal copy
+//     and its hash inserts need come from 256-byte register windows where
+//     they fall inside one (parse_fast_wave_w, JFSX_ZC_WIN bits), so most
+//     sequences cost two or three memory round trips, not eight.
 // The entropy stage of a block (literal Huffman coding, sequence FSE coding)
-// runs the library's serial code (jfsx_zstdc.h) on one lane.
+// builds its tables on one lane (the library's serial code, jfsx_zstdc.h) and
+// spreads the per-symbol work over the lanes.
+//
+// The parser is bound by memory latency (a chain of dependent random reads
+// per sequence), so occupancy is what buys throughput: 16 waves per CU (LDS
+// 9.3 KiB and <= 128 VGPRs per wave) -- a 4096-object batch in one pass.
 #include "jfsx_dev.h"
 #include "jfsx_zstdc.h"
 
+// 0: parse_fast_wave (every read from memory); else parse_fast_wave_w with
+// the window features named below (31: all; A/B in profiles/r4/ab_zstdc_win.txt)
 #ifndef JFSX_ZC_WIN
-#define JFSX_ZC_WIN 0
+#define JFSX_ZC_WIN 31
 #endif
+// lanes of the first search step after a match (doubling on each miss)
 #ifndef JFSX_ZC_K0
-#define JFSX_ZC_K0 4
+#define JFSX_ZC_K0 2
 #endif
 
 namespace jfsx {
@@ -140,6 +152,22 @@ struct WSeq {  // the wave's view of the block's sequence store
     uint8_t *lit;
     uint32_t nseq, nlit, long_id, long_pos;
 };
+
+// ZSTD_storeSeq's record (the literals already copied), by lane 0
+__device__ __forceinline__ void store_seq_rec(WSeq &ss, uint32_t litLen, uint32_t offCode, uint32_t mlBase,
+                                              uint32_t lane) {
+    if (litLen > 0xFFFF) ss.long_id = 1, ss.long_pos = ss.nseq;
+    if (mlBase > 0xFFFF) ss.long_id = 2, ss.long_pos = ss.nseq;
+    if (lane == 0) {
+        jzc::SeqDef d;
+        d.offset = offCode + 1;
+        d.ll = (uint16_t)litLen;
+        d.ml = (uint16_t)mlBase;
+        ss.seq[ss.nseq] = d;
+    }
+    ss.nseq++;
+    ss.nlit += litLen;
+}
 
 // ZSTD_storeSeq: literals copied by the lanes, the record by lane 0
 __device__ __forceinline__ void store_seq_wave(WSeq &ss, const uint8_t *lits, uint32_t litLen, uint32_t offCode,
@@ -383,7 +411,7 @@ __device__ uint32_t parse_fast_wave(const uint8_t *src, int32_t istart, int32_t 
         if (!sm) {
             if (vmask != amask) break;  // the serial loop ends inside this step
             ip0 = anchor + unis(readlanes(d + (d >> 7) + 2, (int)K - 1));
-            K = K < 64 ? 2 * K : 64;
+            K = K < 32 ? 2 * K : 64;  // any K0: never past 64
             continue;
         }
         K = JFSX_ZC_K0;
@@ -450,6 +478,11 @@ __device__ uint32_t parse_fast_wave(const uint8_t *src, int32_t istart, int32_t 
 // they fall inside one (JFSX_ZC_WIN): the same sequences, table and repcodes.
 // W covers the search step's positions; C, loaded by count_back at the
 // match, covers the match's end, the next anchor and often the next step.
+// ZWF (JFSX_ZC_WIN bits): 1 search positions, 2 count_back, 4 literal copies,
+// 8 hash inserts and repcode loop, 16 the match window as the next search window,
+// 32 everything after a match from one round of loads (supersedes 4, 8, 16),
+// 64 (with 32) the next step's table reads in that round too
+constexpr int ZWF = JFSX_ZC_WIN == 1 ? 31 : JFSX_ZC_WIN;
 __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t istart, int32_t iend, uint32_t *htab,
                                       jzc::Params P, uint32_t rep[2], WSeq &ss, uint32_t lane) {
     const uint32_t hlog = P.hlog, mls = P.mls;
@@ -476,8 +509,12 @@ __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t 
     // with JFSX_ZC_K0 lanes and doubles K on each step without a success.
     uint32_t K = JFSX_ZC_K0;
     ZWin W, C;
-    W.w0 = 0xfffff000u;  // empty
-    W.w = 0;
+    W.w0 = C.w0 = 0xfffff000u;  // empty
+    W.w = C.w = 0;
+    // bit 64: the first step after a match has its table reads issued with
+    // the post-match loads (hashes from C), patched for the match's inserts
+    bool pre = false;
+    int32_t ptA = 0, ptB = 0;
     while (ip0 + 1 < ilimit) {
         // ---- one search step: iterations j = 0..K-1 of the serial loop ----
         const int32_t d0 = ip0 - anchor;
@@ -501,8 +538,8 @@ __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t 
         // hash insert at pf + 2) from W, reloaded at ip0 when it does not cover them
         const int32_t phi = unis(readlanes(p, (int)K - 1));
         const uint32_t span = (uint32_t)(phi - ip0) + 16u;
-        bool win = zw_has(W, I, ip0, span);
-        if (!win && span <= 240u) {
+        bool win = (ZWF & 1) && zw_has(W, I, ip0, span);
+        if ((ZWF & 1) && !win && span <= 240u) {
             zw_load(W, I, (uint32_t)ip0, lane);
             win = true;
         }
@@ -512,15 +549,24 @@ __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t 
         else
             load9(src, pc, w0, w1);
         const uint32_t A = hash_w(w0, hlog, mls), B = hash_w(w1, hlog, mls);
-        const int32_t tA0 = (int32_t)T[A], tB0 = (int32_t)T[B];
+        int32_t tA0 = ptA, tB0 = ptB;
+        if (!pre) {
+            tA0 = (int32_t)T[A];
+            tB0 = (int32_t)T[B];
+        }
+        pre = false;
         const uint32_t v0 = (uint32_t)w0, v1 = (uint32_t)w1, r2 = (uint32_t)(w0 >> 16);
         // the repcode candidate: from W when every active lane's lies inside it
         const int32_t q = pc + 2 - (int32_t)offset_1;
         const bool rq = valid && offset_1 > 0;
         bool okr;
-        if (win && !ballot(rq && !zw_has(W, I, q, 8)))
-            okr = rq && zw_u32_lane(W, I, q) == r2;
-        else
+        if (win && !ballot(rq && !zw_has(W, I, q, 8))) {
+            // every lane takes part in the ds_bpermute (a lane masked off
+            // would hand 0 to the lanes reading its dword); lanes without a
+            // repcode candidate read their own position
+            const uint32_t qv = zw_u32_lane(W, I, rq ? q : pc);
+            okr = rq && qv == r2;
+        } else
             okr = rq && ld32u(src + q) == r2;
         bool ok0 = valid && tA0 > prefixStartIndex && ld32u(src + tA0 - 1) == v0;
         bool ok1 = valid && tB0 > prefixStartIndex && ld32u(src + tB0 - 1) == v1;
@@ -592,7 +638,7 @@ __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t 
         if (!sm) {
             if (vmask != amask) break;  // the serial loop ends inside this step
             ip0 = anchor + unis(readlanes(d + (d >> 7) + 2, (int)K - 1));
-            K = K < 64 ? 2 * K : 64;
+            K = K < 32 ? 2 * K : 64;  // any K0: never past 64
             continue;
         }
         K = JFSX_ZC_K0;
@@ -607,7 +653,14 @@ __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t 
         if (fr) {
             // the repcode match extends one byte back when ip2[-1] == repMatch[-1]
             const int32_t ip2 = pf + 2, repMatch = ip2 - (int32_t)offset_1;
-            const uint32_t mc = count_back(C, I, src, ip2, repMatch, iend, 1u, back, lane);
+            uint32_t mc;
+            if (ZWF & 2) {
+                mc = count_back(C, I, src, ip2, repMatch, iend, 1u, back, lane);
+            } else {
+                back = ld8(src + ip2 - 1) == ld8(src + repMatch - 1) ? 1u : 0u;
+                mc = uni(count_wave(src + ip2 + 4, src + repMatch + 4, src + iend, lane));
+                C.w0 = 0xfffff000u;
+            }
             ip0 = ip2 - (int32_t)back;
             match0 = repMatch - (int32_t)back;
             mLength = 4 + back + mc;
@@ -625,14 +678,88 @@ __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t 
             offset_1 = (uint32_t)(ipX - match0);
             offcode = offset_1 + 2;
             const uint32_t lim = (uint32_t)min(ipX - anchor, match0 - prefixStart);
-            const uint32_t mc = count_back(C, I, src, ipX, match0, iend, lim < 64u ? lim : 64u, back, lane);
-            if (back == 64u && lim > 64u) back = 64u + back_wave(src + ipX - 64, src + match0 - 64, lim - 64u, lane);
+            uint32_t mc;
+            if (ZWF & 2) {
+                mc = count_back(C, I, src, ipX, match0, iend, lim < 64u ? lim : 64u, back, lane);
+                if (back == 64u && lim > 64u) back = 64u + back_wave(src + ipX - 64, src + match0 - 64, lim - 64u, lane);
+            } else {
+                back = lim ? back_wave(src + ipX, src + match0, lim, lane) : 0u;
+                mc = uni(count_wave(src + ipX + 4, src + match0 + 4, src + iend, lane));
+                C.w0 = 0xfffff000u;
+            }
             ip0 = ipX - (int32_t)back;
             match0 -= (int32_t)back;
             mLength = 4 + back + mc;
         }
         mLength = uni(mLength);
-        if (zw_has(W, I, anchor, (uint32_t)(ip0 - anchor)))
+        if (ZWF & 32) {
+            // after the match, one round of loads: the first 64 literal
+            // bytes, the window at nip - 2 (the second hash insert, the
+            // repcode test's bytes at nip and the next search), the first
+            // insert's bytes and the repcode candidate's; then the stores
+            const uint32_t litLen = (uint32_t)(ip0 - anchor);
+            const int32_t nip = ip0 + (int32_t)mLength;
+            const bool more = nip <= ilimit;
+            const uint32_t lb = lane < litLen ? ld8(src + anchor + (int32_t)lane) : 0u;
+            ZWin Wn;
+            zw_load(Wn, I, (uint32_t)(nip - 2), lane);
+            const uint64_t h1 = zw_has(W, I, current0 + 1, 12) ? zw_u64(W, I, current0 + 1) : ld64u(src + current0 + 1);
+            const uint32_t bq0 = more && offset_2 > 0 ? uni(ld32u(src + nip - (int32_t)offset_2)) : 0u;
+            uint32_t pA = 0, pB = 0;
+            if ((ZWF & 64) && more && zw_has(C, I, nip, 2 * JFSX_ZC_K0 + 16)) {
+                // the next step's positions nip + 2j (j < K0; K restarts at K0)
+                const int32_t pp = nip + 2 * (int32_t)lane;
+                const bool pv = lane < JFSX_ZC_K0 && pp + 1 < ilimit;
+                uint64_t x0, x1;
+                zw_load9(C, I, pv ? pp : nip, x0, x1);
+                pA = hash_w(x0, hlog, mls);
+                pB = hash_w(x1, hlog, mls);
+                ptA = (int32_t)T[pA];
+                ptB = (int32_t)T[pB];
+                pre = true;
+            }
+            if (lane < litLen) *(gu8c *)(ss.lit + ss.nlit + lane) = (uint8_t)lb;
+            for (uint32_t o = 64 + lane; o < litLen; o += 64) *(gu8c *)(ss.lit + ss.nlit + o) = (uint8_t)ld8(src + anchor + o);
+            store_seq_rec(ss, litLen, offcode, mLength - 3, lane);
+            ip0 = anchor = nip;
+            if (more) {
+                const uint64_t h2 = zw_u64(Wn, I, nip - 2);
+                const uint32_t b1 = hash_w(h1, hlog, mls), b2 = hash_w(h2, hlog, mls);
+                if (lane == 0) {
+                    T[b1] = (uint32_t)(current0 + 2);
+                    T[b2] = (uint32_t)(nip - 1);
+                }
+                if (pre) {  // the prefetched reads see these two writes
+                    ptA = pA == b2 ? nip - 1 : pA == b1 ? current0 + 2 : ptA;
+                    ptB = pB == b2 ? nip - 1 : pB == b1 ? current0 + 2 : ptB;
+                }
+                for (bool first_rep = true;; first_rep = false) {
+                    if (!(ip0 <= ilimit && offset_2 > 0)) break;
+                    const int32_t rp = ip0 - (int32_t)offset_2;
+                    const bool inw = zw_has(Wn, I, ip0, 12);
+                    const uint64_t h3 = inw ? zw_u64(Wn, I, ip0) : ld64u(src + ip0);
+                    const uint32_t bq = first_rep ? bq0 : uni(ld32u(src + rp));
+                    if ((uint32_t)h3 != bq) break;
+                    uint32_t b0;
+                    const uint32_t rLength =
+                        ((ZWF & 2) ? count_back(C, I, src, ip0, rp, iend, 0u, b0, lane)
+                                   : uni(count_wave(src + ip0 + 4, src + rp + 4, src + iend, lane))) + 4;
+                    const uint32_t t = offset_2;
+                    offset_2 = offset_1;
+                    offset_1 = t;
+                    if (lane == 0) T[hash_w(h3, hlog, mls)] = (uint32_t)(ip0 + 1);
+                    ip0 += (int32_t)rLength;
+                    store_seq_rec(ss, 0, 0, rLength - 3, lane);
+                    anchor = ip0;
+                    pre = false;  // the next step starts elsewhere
+                }
+            } else {
+                pre = false;
+            }
+            W = Wn;  // the next search starts at anchor (reloaded by the step when not covered)
+            continue;
+        }
+        if ((ZWF & 4) && zw_has(W, I, anchor, (uint32_t)(ip0 - anchor)))
             store_seq_win(ss, W, I, anchor, (uint32_t)(ip0 - anchor), offcode, mLength - 3, lane);
         else
             store_seq_wave(ss, src + anchor, (uint32_t)(ip0 - anchor), offcode, mLength - 3, lane);
@@ -640,8 +767,9 @@ __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t 
         anchor = ip0;
         if (ip0 <= ilimit) {
             {
-                const uint64_t h1 = zw_has(W, I, current0 + 1, 12) ? zw_u64(W, I, current0 + 1) : ld64u(src + current0 + 1);
-                const uint64_t h2 = zw_has(C, I, ip0 - 2, 12) ? zw_u64(C, I, ip0 - 2) : ld64u(src + ip0 - 2);
+                const uint64_t h1 = (ZWF & 8) && zw_has(W, I, current0 + 1, 12) ? zw_u64(W, I, current0 + 1)
+                                                                              : ld64u(src + current0 + 1);
+                const uint64_t h2 = (ZWF & 8) && zw_has(C, I, ip0 - 2, 12) ? zw_u64(C, I, ip0 - 2) : ld64u(src + ip0 - 2);
                 if (lane == 0) {
                     T[hash_w(h1, hlog, mls)] = (uint32_t)(current0 + 2);
                     T[hash_w(h2, hlog, mls)] = (uint32_t)(ip0 - 1);
@@ -649,13 +777,15 @@ __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t 
             }
             for (;;) {
                 if (!(ip0 <= ilimit && offset_2 > 0)) break;
-                const uint32_t a = zw_has(C, I, ip0, 8) ? (uint32_t)zw_u64(C, I, ip0) : uni(ld32u(src + ip0));
+                const uint32_t a = (ZWF & 8) && zw_has(C, I, ip0, 8) ? (uint32_t)zw_u64(C, I, ip0) : uni(ld32u(src + ip0));
                 const int32_t rp = ip0 - (int32_t)offset_2;
-                const uint32_t bq = zw_has(C, I, rp, 12) ? (uint32_t)zw_u64(C, I, rp) : uni(ld32u(src + rp));
+                const uint32_t bq = (ZWF & 8) && zw_has(C, I, rp, 12) ? (uint32_t)zw_u64(C, I, rp) : uni(ld32u(src + rp));
                 if (a != bq) break;
-                const uint64_t h3 = zw_has(C, I, ip0, 12) ? zw_u64(C, I, ip0) : ld64u(src + ip0);
+                const uint64_t h3 = (ZWF & 8) && zw_has(C, I, ip0, 12) ? zw_u64(C, I, ip0) : ld64u(src + ip0);
                 uint32_t b0;
-                const uint32_t rLength = count_back(C, I, src, ip0, rp, iend, 0u, b0, lane) + 4;
+                const uint32_t rLength =
+                    ((ZWF & 2) ? count_back(C, I, src, ip0, rp, iend, 0u, b0, lane)
+                               : uni(count_wave(src + ip0 + 4, src + rp + 4, src + iend, lane))) + 4;
                 const uint32_t t = offset_2;
                 offset_2 = offset_1;
                 offset_1 = t;
@@ -666,7 +796,7 @@ __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t 
             }
         }
         // the next search starts at anchor: C often covers it already
-        if (zw_has(C, I, anchor, 2 * JFSX_ZC_K0 + 16)) W = C;
+        if ((ZWF & 16) && zw_has(C, I, anchor, 2 * JFSX_ZC_K0 + 16)) W = C;
     }
     rep[0] = offset_1 ? offset_1 : offsetSaved;
     rep[1] = offset_2 ? offset_2 : offsetSaved;
@@ -1217,7 +1347,12 @@ __device__ uint64_t compress_object(const uint8_t *src, uint64_t n, uint8_t *dst
 // object index from a ticket counter (lane 0's vector atomic, made wave-uniform
 // by readfirstlane before the loop test), so a batch of more objects than
 // waves finishes in about n / W object times instead of ceil(n / W).
-__global__ __launch_bounds__(64) void zstd_compress_k(const ZDev *__restrict__ blks, ZOut *__restrict__ outs,
+// 4 waves per SIMD (<= 128 VGPRs): with the 9.3 KiB Work, 16 objects per CU
+// are in flight, which is what a latency-bound parser needs
+#ifndef JFSX_ZC_WPE
+#define JFSX_ZC_WPE 4
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(JFSX_ZC_WPE))) void zstd_compress_k(const ZDev *__restrict__ blks, ZOut *__restrict__ outs,
                                                       uint8_t *__restrict__ scratch, int n,
                                                       uint32_t *__restrict__ queue) {
     __shared__ jzc::Work W;
