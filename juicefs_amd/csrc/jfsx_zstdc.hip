@@ -40,9 +40,10 @@
 #include "jfsx_zstdc.h"
 
 // 0: parse_fast_wave (every read from memory); else parse_fast_wave_w with
-// the window features named below (31: all; A/B in profiles/r4/ab_zstdc_win.txt)
+// the window features named below (287: windows for everything + candidate
+// extensions; A/B in profiles/r4/ab_zstdc_win.txt)
 #ifndef JFSX_ZC_WIN
-#define JFSX_ZC_WIN 31
+#define JFSX_ZC_WIN 287
 #endif
 // lanes of the first search step after a match (doubling on each miss)
 #ifndef JFSX_ZC_K0
@@ -236,12 +237,72 @@ __device__ __forceinline__ void zw_load9(const ZWin &W, const ZImg &I, int32_t p
              ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh + 1) << 32);
     }
 }
+// Repcode windows (bit 128): lanes 0..31 hold the 128 image bytes from b1,
+// lanes 32..63 the 128 from b2 (zero outside the object).  A step loads them
+// at its positions minus offset_1 and minus offset_2, in the same round as its
+// table reads, so the step's repcode test and the repcode test after its
+// match read registers.
+struct ZRep {
+    int32_t b1, b2;
+    uint32_t w;
+};
+__device__ __forceinline__ void zr_load(ZRep &R, const ZImg &I, int32_t x1, int32_t x2, uint32_t lane) {
+    R.b1 = (x1 + (int32_t)I.sh) & ~3;
+    R.b2 = (x2 + (int32_t)I.sh) & ~3;
+    const int32_t o = lane < 32 ? R.b1 + 4 * (int32_t)lane : R.b2 + 4 * ((int32_t)lane - 32);
+    R.w = o >= 0 && o < (int32_t)(I.n + I.sh) ? ld32a(I.al + o) : 0u;
+}
+// [pos, pos + len) inside half h
+__device__ __forceinline__ bool zr_has(const ZRep &R, const ZImg &I, int h, int32_t pos, uint32_t len) {
+    const int64_t b = h ? R.b2 : R.b1, x = (int64_t)pos + I.sh;
+    return x >= b && x + len <= b + 128;
+}
+// 4 bytes at a per-lane position of half 0 (zr_has(0, pos, 8); other lanes
+// read some dword of the half, ignored)
+__device__ __forceinline__ uint32_t zr_u32_lane(const ZRep &R, const ZImg &I, int32_t pos) {
+    const uint32_t r = (uint32_t)(pos + (int32_t)I.sh - R.b1), i = (r >> 2) & 31, sh = r & 3;
+    const uint32_t d0 = __shfl(R.w, (int)i, 64), d1 = __shfl(R.w, (int)((i + 1) & 31), 64);
+    return __builtin_amdgcn_alignbyte(d1, d0, sh);
+}
+// 4 bytes at a uniform position of half h (zr_has(h, pos, 8))
+__device__ __forceinline__ uint32_t zr_u32_uni(const ZRep &R, const ZImg &I, int h, int32_t pos) {
+    const uint32_t r = (uint32_t)(pos + (int32_t)I.sh - (h ? R.b2 : R.b1)), i = (r >> 2) + 32u * h, sh = r & 3;
+    return __builtin_amdgcn_alignbyte(readlane(R.w, (int)i + 1), readlane(R.w, (int)i), sh);
+}
+// 4 bytes at a uniform position from W, C, R or memory, the first that holds them
+__device__ __forceinline__ uint32_t zwr_u32(const ZWin &W, const ZWin &C, const ZRep &R, const ZImg &I,
+                                            const uint8_t *src, int32_t pos) {
+    if (zw_has(C, I, pos, 12)) return (uint32_t)zw_u64(C, I, pos);
+    if (zw_has(W, I, pos, 12)) return (uint32_t)zw_u64(W, I, pos);
+    if (zr_has(R, I, 0, pos, 8)) return zr_u32_uni(R, I, 0, pos);
+    if (zr_has(R, I, 1, pos, 8)) return zr_u32_uni(R, I, 1, pos);
+    return uni(ld32u(src + pos));
+}
+
+// Candidate extensions (bit 256): with its 4-byte check a lane loads the 24
+// image bytes from the dword at or below m - 4 (m the candidate), so the
+// winner's catch-up (up to 4 bytes) and first 12 match bytes are in registers
+// when the step's ballot names it and a short match needs no count_back.
+typedef unsigned int zv4u __attribute__((ext_vector_type(4), aligned(4)));
+typedef unsigned int zv2u __attribute__((ext_vector_type(2), aligned(4)));
+struct ZExt {
+    uint32_t e[6];
+    bool in;  // the 24 bytes lie inside the object image (else e is not loaded)
+};
+__device__ __forceinline__ void zx_load(ZExt &X, const ZImg &I, int32_t m) {
+    const int32_t o = ((m + (int32_t)I.sh) & ~3) - 4;
+    X.in = o >= 0 && o + 24 <= (int32_t)(I.n + I.sh);
+    const uint8_t *a = I.al + (X.in ? o : 0);
+    const zv4u v = *(__attribute__((address_space(1))) const zv4u *)a;
+    const zv2u w = *(__attribute__((address_space(1))) const zv2u *)(a + 16);
+    X.e[0] = v.x, X.e[1] = v.y, X.e[2] = v.z, X.e[3] = v.w, X.e[4] = w.x, X.e[5] = w.y;
+}
+
 // ZSTD_storeSeq with the literals [pos, pos + litLen) taken from the window
 __device__ __forceinline__ void store_seq_win(WSeq &ss, const ZWin &W, const ZImg &I, int32_t pos, uint32_t litLen,
                                               uint32_t offCode, uint32_t mlBase, uint32_t lane) {
     const uint32_t r = (uint32_t)pos + I.sh - W.w0;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
+    for (uint32_t k = 0; k < 4 && 64 * k < litLen; k++) {  // literal runs are short: one pass, mostly
         const uint32_t j = lane + 64 * k, q = r + j;
         const uint32_t dw = __shfl(W.w, (int)((q >> 2) & 63), 64);
         if (j < litLen) *(gu8c *)(ss.lit + ss.nlit + j) = (uint8_t)(dw >> (8 * (q & 3)));
@@ -481,7 +542,9 @@ __device__ uint32_t parse_fast_wave(const uint8_t *src, int32_t istart, int32_t 
 // ZWF (JFSX_ZC_WIN bits): 1 search positions, 2 count_back, 4 literal copies,
 // 8 hash inserts and repcode loop, 16 the match window as the next search window,
 // 32 everything after a match from one round of loads (supersedes 4, 8, 16),
-// 64 (with 32) the next step's table reads in that round too
+// 64 (with 32) the next step's table reads in that round too, 128 repcode
+// windows (ZRep) for the step's repcode test and the one after its match,
+// 256 candidate extensions (ZExt): a short match needs no count_back
 constexpr int ZWF = JFSX_ZC_WIN == 1 ? 31 : JFSX_ZC_WIN;
 __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t istart, int32_t iend, uint32_t *htab,
                                       jzc::Params P, uint32_t rep[2], WSeq &ss, uint32_t lane) {
@@ -515,6 +578,9 @@ __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t 
     // the post-match loads (hashes from C), patched for the match's inserts
     bool pre = false;
     int32_t ptA = 0, ptB = 0;
+    ZRep R;
+    R.b1 = R.b2 = -0x40000000;  // empty
+    R.w = 0;
     while (ip0 + 1 < ilimit) {
         // ---- one search step: iterations j = 0..K-1 of the serial loop ----
         const int32_t d0 = ip0 - anchor;
@@ -538,6 +604,7 @@ __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t 
         // hash insert at pf + 2) from W, reloaded at ip0 when it does not cover them
         const int32_t phi = unis(readlanes(p, (int)K - 1));
         const uint32_t span = (uint32_t)(phi - ip0) + 16u;
+        if (ZWF & 128) zr_load(R, I, ip0 + 2 - (int32_t)offset_1, ip0 - (int32_t)offset_2, lane);
         bool win = (ZWF & 1) && zw_has(W, I, ip0, span);
         if ((ZWF & 1) && !win && span <= 240u) {
             zw_load(W, I, (uint32_t)ip0, lane);
@@ -566,10 +633,25 @@ __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t 
             // repcode candidate read their own position
             const uint32_t qv = zw_u32_lane(W, I, rq ? q : pc);
             okr = rq && qv == r2;
+        } else if ((ZWF & 128) && !ballot(rq && !zr_has(R, I, 0, q, 8))) {
+            const uint32_t qv = zr_u32_lane(R, I, q);
+            okr = rq && qv == r2;
         } else
             okr = rq && ld32u(src + q) == r2;
-        bool ok0 = valid && tA0 > prefixStartIndex && ld32u(src + tA0 - 1) == v0;
-        bool ok1 = valid && tB0 > prefixStartIndex && ld32u(src + tB0 - 1) == v1;
+        ZExt XA, XB;
+        bool ok0, ok1;
+        if (ZWF & 256) {
+            zx_load(XA, I, tA0 - 1);
+            zx_load(XB, I, tB0 - 1);
+            const uint32_t sA = (uint32_t)(tA0 - 1 + (int32_t)I.sh) & 3u, sB = (uint32_t)(tB0 - 1 + (int32_t)I.sh) & 3u;
+            ok0 = valid && tA0 > prefixStartIndex &&
+                  (XA.in ? __builtin_amdgcn_alignbyte(XA.e[2], XA.e[1], sA) : ld32u(src + tA0 - 1)) == v0;
+            ok1 = valid && tB0 > prefixStartIndex &&
+                  (XB.in ? __builtin_amdgcn_alignbyte(XB.e[2], XB.e[1], sB) : ld32u(src + tB0 - 1)) == v1;
+        } else {
+            ok0 = valid && tA0 > prefixStartIndex && ld32u(src + tA0 - 1) == v0;
+            ok1 = valid && tB0 > prefixStartIndex && ld32u(src + tB0 - 1) == v1;
+        }
         int32_t tA = tA0, tB = tB0;
         uint64_t sm = ballot(okr || ok0 || ok1);
         uint64_t commit;
@@ -678,8 +760,56 @@ __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t 
             offset_1 = (uint32_t)(ipX - match0);
             offcode = offset_1 + 2;
             const uint32_t lim = (uint32_t)min(ipX - anchor, match0 - prefixStart);
-            uint32_t mc;
-            if (ZWF & 2) {
+            uint32_t mc = 0;
+            bool fast = false;
+            if (ZWF & 256) {
+                // a short match from the winner's extension and W: catch-up
+                // (<= 4 bytes) and ZSTD_count's first 12 bytes
+                const int32_t t0 = unis(readlanes(f0 ? tA0 : tB0, f));
+                const bool inf = (readlane((uint32_t)(f0 ? XA.in : XB.in), f) & 1u) != 0;
+                if (t0 - 1 == match0 && inf) {
+                    uint32_t u[6];
+#pragma unroll
+                    for (int k = 0; k < 6; k++) u[k] = uni(readlane(f0 ? XA.e[k] : XB.e[k], f));
+                    const uint32_t s = (uint32_t)(match0 + (int32_t)I.sh) & 3u;
+                    const uint32_t L = (uint32_t)(iend - (ipX + 4));
+                    bool okf = false, okb = false;
+                    uint32_t mcf = 0, bk = 0;
+                    if (zw_has(W, I, ipX + 4, 20)) {
+                        const uint64_t c1 = zw_u64(W, I, ipX + 4);
+                        const uint32_t c2 = (uint32_t)zw_u64(W, I, ipX + 12);
+                        const uint64_t m1 = (uint64_t)__builtin_amdgcn_alignbyte(u[3], u[2], s) |
+                                            ((uint64_t)__builtin_amdgcn_alignbyte(u[4], u[3], s) << 32);
+                        const uint32_t m2 = __builtin_amdgcn_alignbyte(u[5], u[4], s);
+                        const uint64_t x1 = c1 ^ m1;
+                        const uint32_t x2 = c2 ^ m2;
+                        const uint32_t j = x1 ? (uint32_t)__builtin_ctzll(x1) >> 3
+                                              : x2 ? 8u + ((uint32_t)__builtin_ctz(x2) >> 3) : 12u;
+                        if (j < 12u || L <= 12u) {
+                            mcf = j < L ? j : L;
+                            okf = true;
+                        }
+                    }
+                    if (lim == 0) {
+                        okb = true;
+                    } else if (zw_has(W, I, ipX - 4, 12)) {
+                        const uint32_t y = (uint32_t)zw_u64(W, I, ipX - 4) ^ __builtin_amdgcn_alignbyte(u[1], u[0], s);
+                        const uint32_t eq = y ? (uint32_t)__builtin_clz(y) >> 3 : 4u;
+                        if (eq < 4u || lim <= 4u) {
+                            bk = eq < lim ? eq : lim;
+                            okb = true;
+                        }
+                    }
+                    if (okf && okb) {
+                        mc = mcf;
+                        back = bk;
+                        fast = true;
+                        C = W;
+                    }
+                }
+            }
+            if (fast) {
+            } else if (ZWF & 2) {
                 mc = count_back(C, I, src, ipX, match0, iend, lim < 64u ? lim : 64u, back, lane);
                 if (back == 64u && lim > 64u) back = 64u + back_wave(src + ipX - 64, src + match0 - 64, lim - 64u, lane);
             } else {
@@ -777,9 +907,13 @@ __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t 
             }
             for (;;) {
                 if (!(ip0 <= ilimit && offset_2 > 0)) break;
-                const uint32_t a = (ZWF & 8) && zw_has(C, I, ip0, 8) ? (uint32_t)zw_u64(C, I, ip0) : uni(ld32u(src + ip0));
+                const uint32_t a = (ZWF & 128) ? zwr_u32(W, C, R, I, src, ip0)
+                                   : (ZWF & 8) && zw_has(C, I, ip0, 8) ? (uint32_t)zw_u64(C, I, ip0)
+                                                                       : uni(ld32u(src + ip0));
                 const int32_t rp = ip0 - (int32_t)offset_2;
-                const uint32_t bq = (ZWF & 8) && zw_has(C, I, rp, 12) ? (uint32_t)zw_u64(C, I, rp) : uni(ld32u(src + rp));
+                const uint32_t bq = (ZWF & 128) ? zwr_u32(W, C, R, I, src, rp)
+                                    : (ZWF & 8) && zw_has(C, I, rp, 12) ? (uint32_t)zw_u64(C, I, rp)
+                                                                        : uni(ld32u(src + rp));
                 if (a != bq) break;
                 const uint64_t h3 = (ZWF & 8) && zw_has(C, I, ip0, 12) ? zw_u64(C, I, ip0) : ld64u(src + ip0);
                 uint32_t b0;
