@@ -49,6 +49,13 @@
 #ifndef JFSX_ZC_K0
 #define JFSX_ZC_K0 2
 #endif
+// the entropy stage's byte loops and the block copies with several loads in
+// flight per lane (bits: 1 block copies, 2 histograms, 4 Huffman emission,
+// 8 FSE state chains, 16 sequence emission and codes; 0: one load per loop
+// iteration, the round-3 code; A/B in profiles/r4/ab_zstdc_win.txt)
+#ifndef JFSX_ZC_MLP
+#define JFSX_ZC_MLP 31
+#endif
 
 namespace jfsx {
 
@@ -1004,6 +1011,85 @@ __device__ __forceinline__ void zero_range(uint8_t *body, uint32_t a, uint32_t b
 }
 
 __device__ __forceinline__ void wave_sync() { __syncthreads(); }
+
+// ---------------------------------------------------------------------------
+// Byte runs and bulk copies with several loads in flight per lane.  A loop
+// that loads a byte and then stores or ORs it pays a memory round trip per
+// iteration: the stores may alias the next iteration's load, so the load
+// waits.  Here each lane loads 16 bytes per step and a step's loads go out
+// before its stores (and before the previous step's work where that helps).
+// ---------------------------------------------------------------------------
+typedef unsigned int zv4a __attribute__((ext_vector_type(4)));
+// 16 bytes at byte offset off of the 4-byte aligned image a; dwords past
+// dlast (the last one holding a wanted byte) read as 0, so no dword without
+// a wanted byte is touched
+__device__ __forceinline__ void ld16r(const uint8_t *a, uint32_t off, uint32_t dlast, uint32_t r[4]) {
+    const uint32_t d = off >> 2, sh = off & 3;
+    uint32_t w[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) w[k] = d + k <= dlast ? ld32a(a + 4 * (d + k)) : 0u;
+#pragma unroll
+    for (int k = 0; k < 4; k++) r[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+}
+__device__ __forceinline__ uint32_t byte_of(const uint32_t r[4], int k) { return (r[k >> 2] >> (8 * (k & 3))) & 255u; }
+
+// dst[0, n) = src[0, n), global to global, any alignment, no overlap: 16 bytes
+// per lane, 4 KiB per wave step, a step's loads before its stores
+__device__ __noinline__ void copy_run(uint8_t *dst, const uint8_t *src, uint32_t n, uint32_t lane) {
+    if (!n) return;
+    const uintptr_t sx = (uintptr_t)src;
+    const uint8_t *sa = (const uint8_t *)(sx & ~(uintptr_t)3);
+    const uint32_t ssh = (uint32_t)(sx & 3), dlast = (ssh + n - 1) >> 2;
+    const bool dal = ((uintptr_t)dst & 3) == 0;
+    for (uint32_t base = 0; base < n; base += 4096) {
+        uint32_t r[4][4];
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const uint32_t o = base + 1024 * g + 16 * lane;
+            if (o < n) ld16r(sa, ssh + o, dlast, r[g]);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const uint32_t o = base + 1024 * g + 16 * lane;
+            if (o < n) {
+                const uint32_t c = min(16u, n - o);
+                uint8_t *d = dst + o;
+                if (c == 16 && dal) {
+#pragma unroll
+                    for (int k = 0; k < 4; k++) *(gu32c *)(d + 4 * k) = r[g][k];
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 16; k++)
+                        if ((uint32_t)k < c) *(gu8c *)(d + k) = (uint8_t)byte_of(r[g], k);
+                }
+            }
+        }
+    }
+}
+// the same, one byte per lane per iteration (the round-3 loop; A/B)
+__device__ __forceinline__ void copy_bytes(uint8_t *dst, const uint8_t *src, uint32_t n, uint32_t lane) {
+#if JFSX_ZC_MLP & 1
+    copy_run(dst, src, n, lane);
+#else
+    for (uint32_t o = lane; o < n; o += 64) *(gu8c *)(dst + o) = (uint8_t)ld8(src + o);
+#endif
+}
+
+// histogram of the bytes p[0, n) (p 4-byte aligned, readable up to the next
+// dword) into LDS counters by atomics
+__device__ __forceinline__ void hist_bytes(uint32_t *cnt, const uint8_t *p, uint32_t n, uint32_t lane) {
+#if JFSX_ZC_MLP & 2
+#pragma unroll 4
+    for (uint32_t i = 4 * lane; i < n; i += 256) {
+        const uint32_t w = ld32a(p + i);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++)
+            if (i + k < n) atomicAdd(&cnt[(w >> (8 * k)) & 255u], 1u);
+    }
+#else
+    for (uint32_t i = lane; i < n; i += 64) atomicAdd(&cnt[ld8(p + i)], 1u);
+#endif
+}
 // diagnostic build (-DJFSX_ZC_TRACE): lane 0 prints each stage of the entropy
 // stage as it is reached (device printf is a hostcall: lines appear while the
 // kernel runs, so a hang shows its last stage)
@@ -1069,6 +1155,7 @@ __device__ uint32_t huf_streams_wave(uint8_t *body, uint32_t o, uint32_t cap, co
     const uint32_t per = (slen + w - 1) / w;
     const uint32_t c0 = min(j * per, slen), c1 = min(c0 + per, slen);
     uint32_t bits = 0;
+#pragma unroll 8
     for (uint32_t i = c0; i < c1; i++) bits += ct.nb[ld8(lit + s0 + i)];
     const uint32_t before = suffix_excl(bits, lane, w);  // symbols after this run come first
     const uint32_t total = __shfl(before + bits, (int)(s * w), 64);  // the stream's bits (group lane 0)
@@ -1087,11 +1174,37 @@ __device__ uint32_t huf_streams_wave(uint8_t *body, uint32_t o, uint32_t cap, co
     wave_sync();
     // this lane's run, last symbol first, from bit `before` of its stream
     uint64_t q = 8ull * my0 + before;
+#if JFSX_ZC_MLP & 4
+    if (c1 > c0) {
+        // the run backwards in 16-byte groups, the next group loaded before
+        // this one's ORs
+        const uintptr_t lx = (uintptr_t)(lit + s0 + c0);
+        const uint8_t *la = (const uint8_t *)(lx & ~(uintptr_t)3);
+        const uint32_t lsh = (uint32_t)(lx & 3), m = c1 - c0, dlast = (lsh + m - 1) >> 2;
+        int32_t gs = (int32_t)((m - 1) & ~15u);
+        uint32_t r[4], rn[4];
+        ld16r(la, lsh + (uint32_t)gs, dlast, r);
+        for (; gs >= 0; gs -= 16) {
+            if (gs >= 16) ld16r(la, lsh + (uint32_t)gs - 16, dlast, rn);
+#pragma unroll
+            for (int k = 15; k >= 0; k--) {
+                if ((uint32_t)(gs + k) < m) {
+                    const uint32_t b = byte_of(r, k);
+                    or_bits((uint32_t *)body, q, ct.val[b], ct.nb[b]);
+                    q += ct.nb[b];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) r[k] = rn[k];
+        }
+    }
+#else
     for (int32_t i = (int32_t)c1 - 1; i >= (int32_t)c0; i--) {
         const uint32_t b = ld8(lit + s0 + i);
         or_bits((uint32_t *)body, q, ct.val[b], ct.nb[b]);
         q += ct.nb[b];
     }
+#endif
     if (j == 0) or_bits((uint32_t *)body, 8ull * my0 + total, 1, 1);  // end mark
     if (!single && lane == 0) {
         jzc::wr16(body + o, sz[0]);
@@ -1107,7 +1220,7 @@ __device__ void hist_literals(jzc::Work &W, const uint8_t *lit, uint32_t n, uint
                               uint32_t &largest) {
     for (uint32_t i = lane; i < 256; i += 64) W.litCount[i] = 0;
     wave_sync();
-    for (uint32_t i = lane; i < n; i += 64) atomicAdd(&W.litCount[ld8(lit + i)], 1u);
+    hist_bytes(W.litCount, lit, n, lane);
     wave_sync();
     uint32_t mx = 0, ms = 0;
     for (uint32_t k = 0; k < 4; k++) {
@@ -1171,7 +1284,7 @@ __device__ uint32_t literals_wave(jzc::Work &W, uint8_t *body, const uint8_t *li
             else if (fl == 2) jzc::wr16(body, jzc::kSetBasic + (1u << 2) + (n << 4));
             else jzc::wr24(body, jzc::kSetBasic + (3u << 2) + (n << 4));
         }
-        for (uint32_t i = lane; i < n; i += 64) *(gu8c *)(body + fl + i) = (uint8_t)ld8(lit + i);
+        copy_bytes(body + fl, lit, n, lane);
         wave_sync();
         return fl + n;
     }
@@ -1194,7 +1307,7 @@ __device__ void hist_codes_wave(jzc::Work &W, const uint8_t *codes, uint32_t n, 
                                 uint32_t &maxSym, uint32_t &mostFreq) {
     W.sw.count[lane] = 0;
     wave_sync();
-    for (uint32_t i = lane; i < n; i += 64) atomicAdd(&W.sw.count[ld8(codes + i)], 1u);
+    hist_bytes(W.sw.count, codes, n, lane);
     wave_sync();
     const uint32_t c = lane <= maxIn ? W.sw.count[lane] : 0u;
     uint32_t mx = c, ms = c ? lane : 0u;
@@ -1233,12 +1346,38 @@ __device__ uint32_t sequences_wave(jzc::Work &W, uint8_t *body, uint32_t o, uint
         gu16c *r = (gu16c *)(rec + (size_t)lane * jzc::kMaxSeq);
         jzc::FseState st;
         jzc::fse_init_state2(st, ct, ld8(cd + n - 1));
+#if JFSX_ZC_MLP & 8
+        // the codes in aligned 16-byte groups (cd is 16-byte aligned), the
+        // next group's load in flight while this one's 16 steps run
+        const int32_t top = (int32_t)n - 2;
+        if (top >= 0) {
+            typedef __attribute__((address_space(1))) const zv4a gzv4;
+            int32_t G = top >> 4;
+            zv4a v = *(gzv4 *)(cd + 16 * G), vn = v;
+            for (; G >= 0; G--) {
+                if (G > 0) vn = *(gzv4 *)(cd + 16 * (G - 1));
+                const uint32_t rr[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int k = 15; k >= 0; k--) {
+                    const int32_t i = 16 * G + k;
+                    if (i <= top) {
+                        const uint32_t c = byte_of(rr, k);
+                        const uint32_t nb = (st.value + ct.dnb[c]) >> 16;
+                        r[i] = (uint16_t)((nb << 12) | (st.value & ((1u << nb) - 1)));
+                        st.value = ct.state[(int32_t)(st.value >> nb) + ct.dfs[c]];
+                    }
+                }
+                v = vn;
+            }
+        }
+#else
         for (int32_t i = (int32_t)n - 2; i >= 0; i--) {
             const uint32_t c = ld8(cd + i);
             const uint32_t nb = (st.value + ct.dnb[c]) >> 16;
             r[i] = (uint16_t)((nb << 12) | (st.value & ((1u << nb) - 1)));
             st.value = ct.state[(int32_t)(st.value >> nb) + ct.dfs[c]];
         }
+#endif
         fin[lane] = st.value;
     }
     wave_sync();
@@ -1247,6 +1386,7 @@ __device__ uint32_t sequences_wave(jzc::Work &W, uint8_t *body, uint32_t o, uint
     const uint32_t c0 = min(lane * per, n), c1 = min(c0 + per, n);
     const gu16c *rOF = (const gu16c *)rec, *rML = rOF + jzc::kMaxSeq, *rLL = rML + jzc::kMaxSeq;
     uint32_t bits = 0;
+#pragma unroll 8
     for (uint32_t i = c0; i < c1; i++) {
         const uint32_t l = ld8(llc + i), m = ld8(mlc + i), f = ld8(ofc + i);
         bits += jzc::kLLBits[l] + jzc::kMLBits[m] + f;
@@ -1263,6 +1403,41 @@ __device__ uint32_t sequences_wave(jzc::Work &W, uint8_t *body, uint32_t o, uint
     wave_sync();
     uint64_t q = 8ull * o + before;
     uint32_t *base = (uint32_t *)body;
+#if JFSX_ZC_MLP & 16
+    constexpr int kG = 4;  // sequences whose inputs are loaded before their ORs
+    for (int32_t i0 = (int32_t)c1 - 1; i0 >= (int32_t)c0; i0 -= kG) {
+        uint32_t L[kG], M[kG], F[kG], RA[kG], RB[kG], RC[kG];
+        jzc::SeqDef D[kG];
+#pragma unroll
+        for (int k = 0; k < kG; k++) {
+            const int32_t i = i0 - k;
+            if (i >= (int32_t)c0) {
+                L[k] = ld8(llc + i), M[k] = ld8(mlc + i), F[k] = ld8(ofc + i);
+                D[k] = seq[i];
+                const bool has = (uint32_t)i + 1 < n;
+                RA[k] = has ? rOF[i] : 0u, RB[k] = has ? rML[i] : 0u, RC[k] = has ? rLL[i] : 0u;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kG; k++) {
+            if (i0 - k >= (int32_t)c0) {
+                const uint32_t a = RA[k], b = RB[k], c = RC[k];
+                or_bits(base, q, a & 0xfff, a >> 12);
+                q += a >> 12;
+                or_bits(base, q, b & 0xfff, b >> 12);
+                q += b >> 12;
+                or_bits(base, q, c & 0xfff, c >> 12);
+                q += c >> 12;
+                or_bits(base, q, D[k].ll, jzc::kLLBits[L[k]]);
+                q += jzc::kLLBits[L[k]];
+                or_bits(base, q, D[k].ml, jzc::kMLBits[M[k]]);
+                q += jzc::kMLBits[M[k]];
+                or_bits(base, q, D[k].offset, F[k]);
+                q += F[k];
+            }
+        }
+    }
+#else
     for (int32_t i = (int32_t)c1 - 1; i >= (int32_t)c0; i--) {
         const uint32_t l = ld8(llc + i), m = ld8(mlc + i), f = ld8(ofc + i);
         const jzc::SeqDef d = seq[i];
@@ -1282,6 +1457,7 @@ __device__ uint32_t sequences_wave(jzc::Work &W, uint8_t *body, uint32_t o, uint
         or_bits(base, q, d.offset, f);
         q += f;
     }
+#endif
     if (lane == 0) {
         uint64_t e = 8ull * o + total;
         or_bits(base, e, fin[1], W.sw.ml.tableLog);
@@ -1319,12 +1495,30 @@ __device__ uint64_t block_body_wave(jzc::Work &W, const WSeq &ss, uint8_t *codes
     op += nbSeq < 128 ? 1 : nbSeq < jzc::kLongNbSeq ? 2 : 3;
     if (nbSeq != 0) {
         uint8_t *llc = codes, *mlc = codes + jzc::kMaxSeq, *ofc = codes + 2 * jzc::kMaxSeq;
+#if JFSX_ZC_MLP & 16
+        for (uint32_t i0 = lane; i0 < nbSeq; i0 += 256) {
+            jzc::SeqDef D[4];
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++)
+                if (i0 + 64 * k < nbSeq) D[k] = ss.seq[i0 + 64 * k];
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) {
+                const uint32_t i = i0 + 64 * k;
+                if (i < nbSeq) {
+                    *(gu8c *)(llc + i) = (uint8_t)jzc::ll_code(D[k].ll);
+                    *(gu8c *)(ofc + i) = (uint8_t)jzc::highbit32(D[k].offset);
+                    *(gu8c *)(mlc + i) = (uint8_t)jzc::ml_code(D[k].ml);
+                }
+            }
+        }
+#else
         for (uint32_t i = lane; i < nbSeq; i += 64) {
             const jzc::SeqDef d = ss.seq[i];
             *(gu8c *)(llc + i) = (uint8_t)jzc::ll_code(d.ll);
             *(gu8c *)(ofc + i) = (uint8_t)jzc::highbit32(d.offset);
             *(gu8c *)(mlc + i) = (uint8_t)jzc::ml_code(d.ml);
         }
+#endif
         wave_sync();
         if (lane == 0) {
             if (ss.long_id == 1) llc[ss.long_pos] = jzc::kMaxLL;
@@ -1417,8 +1611,7 @@ __device__ uint64_t compress_object(const uint8_t *src, uint64_t n, uint8_t *dst
             if (lane == 0) g_zc_parse += t_p1 - t_p0, g_zc_nseq += ss.nseq;
 #endif
             ZT("zc: parsed nseq %u lastLL %u\n", ss.nseq, lastLL);
-            for (uint32_t o = lane; o < lastLL; o += 64)
-                *(gu8c *)(lits + ss.nlit + o) = (uint8_t)ld8(src + pos + bs - lastLL + o);
+            copy_bytes(lits + ss.nlit, src + pos + bs - lastLL, lastLL, lane);
             ss.nlit += lastLL;
             __syncthreads();  // sequences and literals visible to every lane
 #ifdef JFSX_ZC_LANE0_ENTROPY
@@ -1450,7 +1643,7 @@ __device__ uint64_t compress_object(const uint8_t *src, uint64_t n, uint8_t *dst
         }
         if (cSize == 0) {
             if (lane == 0) jzc::wr24(dst + op, last + (bs << 3));
-            for (uint32_t o = lane; o < bs; o += 64) *(gu8c *)(dst + op + 3 + o) = (uint8_t)ld8(ip + o);
+            copy_bytes(dst + op + 3, ip, bs, lane);
             op += 3 + bs;
         } else if (cSize == 1) {
             if (lane == 0) {
@@ -1460,7 +1653,7 @@ __device__ uint64_t compress_object(const uint8_t *src, uint64_t n, uint8_t *dst
             op += 4;
         } else {
             if (lane == 0) jzc::wr24(dst + op, last + (2u << 1) + ((uint32_t)cSize << 3));
-            for (uint32_t o = lane; o < cSize; o += 64) *(gu8c *)(dst + op + 3 + o) = (uint8_t)ld8(body + o);
+            copy_bytes(dst + op + 3, body, (uint32_t)cSize, lane);
             op += 3 + cSize;
         }
         pos += bs;
