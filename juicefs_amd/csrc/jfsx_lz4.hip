@@ -187,8 +187,7 @@ __device__ __forceinline__ uint32_t hash_of(uint32_t w, uint32_t b4, bool small)
 __device__ __forceinline__ void iwin_copy(uint8_t *dst, const IWin &W, const Img &I, uint32_t pos, uint32_t len,
                                           uint32_t lane) {
     const uint32_t r = pos + I.sh - W.w0;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
+    for (uint32_t k = 0; k < 4 && 64 * k < len; k++) {  // literal runs are short: one pass, mostly
         const uint32_t j = lane + 64 * k, q = r + j;
         const uint32_t d = __shfl(W.w, (int)((q >> 2) & 63), 64);
         if (j < len) st8(dst + j, (d >> (8 * (q & 3))) & 255u);
