@@ -161,22 +161,6 @@ struct WSeq {  // the wave's view of the block's sequence store
     uint32_t nseq, nlit, long_id, long_pos;
 };
 
-// ZSTD_storeSeq's record (the literals already copied), by lane 0
-__device__ __forceinline__ void store_seq_rec(WSeq &ss, uint32_t litLen, uint32_t offCode, uint32_t mlBase,
-                                              uint32_t lane) {
-    if (litLen > 0xFFFF) ss.long_id = 1, ss.long_pos = ss.nseq;
-    if (mlBase > 0xFFFF) ss.long_id = 2, ss.long_pos = ss.nseq;
-    if (lane == 0) {
-        jzc::SeqDef d;
-        d.offset = offCode + 1;
-        d.ll = (uint16_t)litLen;
-        d.ml = (uint16_t)mlBase;
-        ss.seq[ss.nseq] = d;
-    }
-    ss.nseq++;
-    ss.nlit += litLen;
-}
-
 // ZSTD_storeSeq: literals copied by the lanes, the record by lane 0
 __device__ __forceinline__ void store_seq_wave(WSeq &ss, const uint8_t *lits, uint32_t litLen, uint32_t offCode,
                                                uint32_t mlBase, uint32_t lane) {
@@ -244,48 +228,6 @@ __device__ __forceinline__ void zw_load9(const ZWin &W, const ZImg &I, int32_t p
              ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh + 1) << 32);
     }
 }
-// Repcode windows (bit 128): lanes 0..31 hold the 128 image bytes from b1,
-// lanes 32..63 the 128 from b2 (zero outside the object).  A step loads them
-// at its positions minus offset_1 and minus offset_2, in the same round as its
-// table reads, so the step's repcode test and the repcode test after its
-// match read registers.
-struct ZRep {
-    int32_t b1, b2;
-    uint32_t w;
-};
-__device__ __forceinline__ void zr_load(ZRep &R, const ZImg &I, int32_t x1, int32_t x2, uint32_t lane) {
-    R.b1 = (x1 + (int32_t)I.sh) & ~3;
-    R.b2 = (x2 + (int32_t)I.sh) & ~3;
-    const int32_t o = lane < 32 ? R.b1 + 4 * (int32_t)lane : R.b2 + 4 * ((int32_t)lane - 32);
-    R.w = o >= 0 && o < (int32_t)(I.n + I.sh) ? ld32a(I.al + o) : 0u;
-}
-// [pos, pos + len) inside half h
-__device__ __forceinline__ bool zr_has(const ZRep &R, const ZImg &I, int h, int32_t pos, uint32_t len) {
-    const int64_t b = h ? R.b2 : R.b1, x = (int64_t)pos + I.sh;
-    return x >= b && x + len <= b + 128;
-}
-// 4 bytes at a per-lane position of half 0 (zr_has(0, pos, 8); other lanes
-// read some dword of the half, ignored)
-__device__ __forceinline__ uint32_t zr_u32_lane(const ZRep &R, const ZImg &I, int32_t pos) {
-    const uint32_t r = (uint32_t)(pos + (int32_t)I.sh - R.b1), i = (r >> 2) & 31, sh = r & 3;
-    const uint32_t d0 = __shfl(R.w, (int)i, 64), d1 = __shfl(R.w, (int)((i + 1) & 31), 64);
-    return __builtin_amdgcn_alignbyte(d1, d0, sh);
-}
-// 4 bytes at a uniform position of half h (zr_has(h, pos, 8))
-__device__ __forceinline__ uint32_t zr_u32_uni(const ZRep &R, const ZImg &I, int h, int32_t pos) {
-    const uint32_t r = (uint32_t)(pos + (int32_t)I.sh - (h ? R.b2 : R.b1)), i = (r >> 2) + 32u * h, sh = r & 3;
-    return __builtin_amdgcn_alignbyte(readlane(R.w, (int)i + 1), readlane(R.w, (int)i), sh);
-}
-// 4 bytes at a uniform position from W, C, R or memory, the first that holds them
-__device__ __forceinline__ uint32_t zwr_u32(const ZWin &W, const ZWin &C, const ZRep &R, const ZImg &I,
-                                            const uint8_t *src, int32_t pos) {
-    if (zw_has(C, I, pos, 12)) return (uint32_t)zw_u64(C, I, pos);
-    if (zw_has(W, I, pos, 12)) return (uint32_t)zw_u64(W, I, pos);
-    if (zr_has(R, I, 0, pos, 8)) return zr_u32_uni(R, I, 0, pos);
-    if (zr_has(R, I, 1, pos, 8)) return zr_u32_uni(R, I, 1, pos);
-    return uni(ld32u(src + pos));
-}
-
 // Candidate extensions (bit 256): with its 4-byte check a lane loads the 24
 // image bytes from the dword at or below m - 4 (m the candidate), so the
 // winner's catch-up (up to 4 bytes) and first 12 match bytes are in registers
@@ -548,10 +490,10 @@ __device__ uint32_t parse_fast_wave(const uint8_t *src, int32_t istart, int32_t 
 // match, covers the match's end, the next anchor and often the next step.
 // ZWF (JFSX_ZC_WIN bits): 1 search positions, 2 count_back, 4 literal copies,
 // 8 hash inserts and repcode loop, 16 the match window as the next search window,
-// 32 everything after a match from one round of loads (supersedes 4, 8, 16),
-// 64 (with 32) the next step's table reads in that round too, 128 repcode
-// windows (ZRep) for the step's repcode test and the one after its match,
-// 256 candidate extensions (ZExt): a short match needs no count_back
+// 256 candidate extensions (ZExt): a short match needs no count_back.  (Bits
+// 32, 64 and 128 -- everything after a match from one round of loads, the
+// next step's table reads in that round, repcode windows -- were measured
+// slower or equal and removed: profiles/r4/ab_zstdc_win.txt.)
 constexpr int ZWF = JFSX_ZC_WIN == 1 ? 31 : JFSX_ZC_WIN;
 __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t istart, int32_t iend, uint32_t *htab,
                                       jzc::Params P, uint32_t rep[2], WSeq &ss, uint32_t lane) {
@@ -581,13 +523,6 @@ __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t 
     ZWin W, C;
     W.w0 = C.w0 = 0xfffff000u;  // empty
     W.w = C.w = 0;
-    // bit 64: the first step after a match has its table reads issued with
-    // the post-match loads (hashes from C), patched for the match's inserts
-    bool pre = false;
-    int32_t ptA = 0, ptB = 0;
-    ZRep R;
-    R.b1 = R.b2 = -0x40000000;  // empty
-    R.w = 0;
     while (ip0 + 1 < ilimit) {
         // ---- one search step: iterations j = 0..K-1 of the serial loop ----
         const int32_t d0 = ip0 - anchor;
@@ -611,7 +546,6 @@ __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t 
         // hash insert at pf + 2) from W, reloaded at ip0 when it does not cover them
         const int32_t phi = unis(readlanes(p, (int)K - 1));
         const uint32_t span = (uint32_t)(phi - ip0) + 16u;
-        if (ZWF & 128) zr_load(R, I, ip0 + 2 - (int32_t)offset_1, ip0 - (int32_t)offset_2, lane);
         bool win = (ZWF & 1) && zw_has(W, I, ip0, span);
         if ((ZWF & 1) && !win && span <= 240u) {
             zw_load(W, I, (uint32_t)ip0, lane);
@@ -623,12 +557,7 @@ __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t 
         else
             load9(src, pc, w0, w1);
         const uint32_t A = hash_w(w0, hlog, mls), B = hash_w(w1, hlog, mls);
-        int32_t tA0 = ptA, tB0 = ptB;
-        if (!pre) {
-            tA0 = (int32_t)T[A];
-            tB0 = (int32_t)T[B];
-        }
-        pre = false;
+        const int32_t tA0 = (int32_t)T[A], tB0 = (int32_t)T[B];
         const uint32_t v0 = (uint32_t)w0, v1 = (uint32_t)w1, r2 = (uint32_t)(w0 >> 16);
         // the repcode candidate: from W when every active lane's lies inside it
         const int32_t q = pc + 2 - (int32_t)offset_1;
@@ -639,9 +568,6 @@ __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t 
             // would hand 0 to the lanes reading its dword); lanes without a
             // repcode candidate read their own position
             const uint32_t qv = zw_u32_lane(W, I, rq ? q : pc);
-            okr = rq && qv == r2;
-        } else if ((ZWF & 128) && !ballot(rq && !zr_has(R, I, 0, q, 8))) {
-            const uint32_t qv = zr_u32_lane(R, I, q);
             okr = rq && qv == r2;
         } else
             okr = rq && ld32u(src + q) == r2;
@@ -829,73 +755,6 @@ __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t 
             mLength = 4 + back + mc;
         }
         mLength = uni(mLength);
-        if (ZWF & 32) {
-            // after the match, one round of loads: the first 64 literal
-            // bytes, the window at nip - 2 (the second hash insert, the
-            // repcode test's bytes at nip and the next search), the first
-            // insert's bytes and the repcode candidate's; then the stores
-            const uint32_t litLen = (uint32_t)(ip0 - anchor);
-            const int32_t nip = ip0 + (int32_t)mLength;
-            const bool more = nip <= ilimit;
-            const uint32_t lb = lane < litLen ? ld8(src + anchor + (int32_t)lane) : 0u;
-            ZWin Wn;
-            zw_load(Wn, I, (uint32_t)(nip - 2), lane);
-            const uint64_t h1 = zw_has(W, I, current0 + 1, 12) ? zw_u64(W, I, current0 + 1) : ld64u(src + current0 + 1);
-            const uint32_t bq0 = more && offset_2 > 0 ? uni(ld32u(src + nip - (int32_t)offset_2)) : 0u;
-            uint32_t pA = 0, pB = 0;
-            if ((ZWF & 64) && more && zw_has(C, I, nip, 2 * JFSX_ZC_K0 + 16)) {
-                // the next step's positions nip + 2j (j < K0; K restarts at K0)
-                const int32_t pp = nip + 2 * (int32_t)lane;
-                const bool pv = lane < JFSX_ZC_K0 && pp + 1 < ilimit;
-                uint64_t x0, x1;
-                zw_load9(C, I, pv ? pp : nip, x0, x1);
-                pA = hash_w(x0, hlog, mls);
-                pB = hash_w(x1, hlog, mls);
-                ptA = (int32_t)T[pA];
-                ptB = (int32_t)T[pB];
-                pre = true;
-            }
-            if (lane < litLen) *(gu8c *)(ss.lit + ss.nlit + lane) = (uint8_t)lb;
-            for (uint32_t o = 64 + lane; o < litLen; o += 64) *(gu8c *)(ss.lit + ss.nlit + o) = (uint8_t)ld8(src + anchor + o);
-            store_seq_rec(ss, litLen, offcode, mLength - 3, lane);
-            ip0 = anchor = nip;
-            if (more) {
-                const uint64_t h2 = zw_u64(Wn, I, nip - 2);
-                const uint32_t b1 = hash_w(h1, hlog, mls), b2 = hash_w(h2, hlog, mls);
-                if (lane == 0) {
-                    T[b1] = (uint32_t)(current0 + 2);
-                    T[b2] = (uint32_t)(nip - 1);
-                }
-                if (pre) {  // the prefetched reads see these two writes
-                    ptA = pA == b2 ? nip - 1 : pA == b1 ? current0 + 2 : ptA;
-                    ptB = pB == b2 ? nip - 1 : pB == b1 ? current0 + 2 : ptB;
-                }
-                for (bool first_rep = true;; first_rep = false) {
-                    if (!(ip0 <= ilimit && offset_2 > 0)) break;
-                    const int32_t rp = ip0 - (int32_t)offset_2;
-                    const bool inw = zw_has(Wn, I, ip0, 12);
-                    const uint64_t h3 = inw ? zw_u64(Wn, I, ip0) : ld64u(src + ip0);
-                    const uint32_t bq = first_rep ? bq0 : uni(ld32u(src + rp));
-                    if ((uint32_t)h3 != bq) break;
-                    uint32_t b0;
-                    const uint32_t rLength =
-                        ((ZWF & 2) ? count_back(C, I, src, ip0, rp, iend, 0u, b0, lane)
-                                   : uni(count_wave(src + ip0 + 4, src + rp + 4, src + iend, lane))) + 4;
-                    const uint32_t t = offset_2;
-                    offset_2 = offset_1;
-                    offset_1 = t;
-                    if (lane == 0) T[hash_w(h3, hlog, mls)] = (uint32_t)(ip0 + 1);
-                    ip0 += (int32_t)rLength;
-                    store_seq_rec(ss, 0, 0, rLength - 3, lane);
-                    anchor = ip0;
-                    pre = false;  // the next step starts elsewhere
-                }
-            } else {
-                pre = false;
-            }
-            W = Wn;  // the next search starts at anchor (reloaded by the step when not covered)
-            continue;
-        }
         if ((ZWF & 4) && zw_has(W, I, anchor, (uint32_t)(ip0 - anchor)))
             store_seq_win(ss, W, I, anchor, (uint32_t)(ip0 - anchor), offcode, mLength - 3, lane);
         else
@@ -914,13 +773,9 @@ __device__ uint32_t parse_fast_wave_w(const uint8_t *src, const ZImg I, int32_t 
             }
             for (;;) {
                 if (!(ip0 <= ilimit && offset_2 > 0)) break;
-                const uint32_t a = (ZWF & 128) ? zwr_u32(W, C, R, I, src, ip0)
-                                   : (ZWF & 8) && zw_has(C, I, ip0, 8) ? (uint32_t)zw_u64(C, I, ip0)
-                                                                       : uni(ld32u(src + ip0));
+                const uint32_t a = (ZWF & 8) && zw_has(C, I, ip0, 8) ? (uint32_t)zw_u64(C, I, ip0) : uni(ld32u(src + ip0));
                 const int32_t rp = ip0 - (int32_t)offset_2;
-                const uint32_t bq = (ZWF & 128) ? zwr_u32(W, C, R, I, src, rp)
-                                    : (ZWF & 8) && zw_has(C, I, rp, 12) ? (uint32_t)zw_u64(C, I, rp)
-                                                                        : uni(ld32u(src + rp));
+                const uint32_t bq = (ZWF & 8) && zw_has(C, I, rp, 12) ? (uint32_t)zw_u64(C, I, rp) : uni(ld32u(src + rp));
                 if (a != bq) break;
                 const uint64_t h3 = (ZWF & 8) && zw_has(C, I, ip0, 12) ? zw_u64(C, I, ip0) : ld64u(src + ip0);
                 uint32_t b0;
