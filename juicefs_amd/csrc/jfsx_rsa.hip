@@ -23,10 +23,62 @@ namespace jfsx {
 using jfsx_rsa::kLimbs;
 using jfsx_rsa::kModBytes;
 
-// x^e mod m with one Montgomery multiply site in the loop (the unrolled CIOS
-// is ~6K instructions; one copy keeps the loop inside the instruction cache)
+// x^e mod m, left to right with a fixed 4-bit window: x^1..x^15 (Montgomery
+// domain) in private memory, then per digit four squarings and one multiply
+// by the digit's power (none for a zero digit) -- about 1275 products for a
+// 1024-bit exponent instead of 1535 bit by bit.  One Montgomery multiply site
+// in the loop: the unrolled CIOS is ~6K instructions, and one copy keeps the
+// loop inside the instruction cache.  The exponent (the key's) is wave-uniform,
+// so every branch is.
+#ifndef JFSX_RSA_WIN
+#define JFSX_RSA_WIN 1  // 0: bit by bit (A/B)
+#endif
+__device__ __forceinline__ uint32_t exp_digit(const uint32_t *e, int d) { return (e[d >> 3] >> (4 * (d & 7))) & 15u; }
+
 __device__ __forceinline__ void mod_exp_1site(const uint32_t *x, const uint32_t *e, int e_bits, const uint32_t *m,
                                               uint32_t minv, const uint32_t *r2, uint32_t *out) {
+#if JFSX_RSA_WIN
+    uint32_t tab[16][kLimbs];  // tab[j] = x^j R mod m, j >= 1
+    uint32_t acc[kLimbs], b[kLimbs];
+    jfsx_rsa::mont_mul(x, r2, m, minv, acc);  // to the Montgomery domain
+#pragma unroll
+    for (int j = 0; j < kLimbs; j++) tab[1][j] = acc[j];
+    const int ndig = (e_bits + 3) / 4;  // the top digit holds the top set bit: nonzero
+    int k = 2;                          // phase 0: tab[k] = tab[k - 1] * x
+    int d = ndig - 1, phase = 0, nsq = 0;
+    for (;;) {
+        const uint32_t bi = phase == 0 ? 1u : phase == 2 ? exp_digit(e, d) : 0u;
+        if (phase == 1) {
+#pragma unroll
+            for (int j = 0; j < kLimbs; j++) b[j] = acc[j];
+        } else {
+#pragma unroll
+            for (int j = 0; j < kLimbs; j++) b[j] = tab[bi][j];
+        }
+        jfsx_rsa::mont_mul(acc, b, m, minv, acc);
+        if (phase == 0) {
+#pragma unroll
+            for (int j = 0; j < kLimbs; j++) tab[k][j] = acc[j];
+            if (++k < 16) continue;
+            const uint32_t top = exp_digit(e, ndig - 1);
+#pragma unroll
+            for (int j = 0; j < kLimbs; j++) acc[j] = tab[top][j];
+            if (--d < 0) break;
+            phase = 1, nsq = 4;
+        } else if (phase == 1) {
+            if (--nsq) continue;
+            if (exp_digit(e, d)) {
+                phase = 2;
+            } else {
+                if (--d < 0) break;
+                nsq = 4;
+            }
+        } else {
+            if (--d < 0) break;
+            phase = 1, nsq = 4;
+        }
+    }
+#else
     uint32_t xm[kLimbs], acc[kLimbs], b[kLimbs];
     jfsx_rsa::mont_mul(x, r2, m, minv, xm);  // to the Montgomery domain
 #pragma unroll
@@ -45,6 +97,7 @@ __device__ __forceinline__ void mod_exp_1site(const uint32_t *x, const uint32_t 
             bit--;
         }
     }
+#endif
 #pragma unroll
     for (int j = 0; j < kLimbs; j++) b[j] = j == 0;
     jfsx_rsa::mont_mul(acc, b, m, minv, out);  // out of the Montgomery domain

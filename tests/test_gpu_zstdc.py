@@ -105,3 +105,20 @@ def test_mirror_compress_and_upload_blocks(eng):
     # decoder, the call DataDog/zstd's Decompress makes (compress.go:93-102)
     for k, b in zip(keys, blocks):
         assert zstd_lib.decompress(st.d[k], len(b)) == (len(b), b)
+
+
+def test_more_objects_than_waves_round_trip(eng):
+    """5000 objects: more than the compressor's persistent waves (16 per CU)
+    and the block-parallel decoder's (8 per CU), so waves take several
+    objects in turn and every per-object state (hash table, windows,
+    repcodes, entropy tables) is reset between them.  Every frame equals
+    libzstd's level-1 frame and decodes back on the GPU."""
+    rng = np.random.default_rng(5000)
+    n = 5000
+    lens = [int(x) for x in rng.integers(0, 3000, n)]
+    srcs = [lz4_data.sample(lz4_data.KINDS[i % 6], lens[i], seed=9000 + i) for i in range(n)]
+    got = eng.zstd_compress(srcs)
+    for i, (s, g) in enumerate(zip(srcs, got)):
+        assert g == zstd_lib.compress_simple(s, 1), i
+    back = eng.zstd_decompress(got, lens)
+    assert all(st == E.OK and d == s for (st, d), s in zip(back, srcs))
