@@ -394,7 +394,7 @@ __device__ __forceinline__ void cp_task(const char *lds, const Task task, const 
         const uint64_t o = sub0 + 4096 * r + lo;
         uint4 d[4];
 #pragma unroll
-        for (int q = 0; q < 4; q++) d[q] = gld16(src + o + 16 * q);
+        for (int q = 0; q < 4; q++) d[q] = ald16(src + o + 16 * q);
         uint32_t ks[16];
         chacha_block_u(uni, (uint32_t)(o / 64 + 1), ks);
 #pragma unroll
@@ -402,7 +402,7 @@ __device__ __forceinline__ void cp_task(const char *lds, const Task task, const 
             const uint4 x = make_uint4(d[q].x ^ ks[4 * q], d[q].y ^ ks[4 * q + 1], d[q].z ^ ks[4 * q + 2],
                                        d[q].w ^ ks[4 * q + 3]);
             const uint4 c = OPEN ? d[q] : x, p = OPEN ? x : d[q];
-            gst16(dst + o + 16 * q, OPEN ? p : c);
+            ast16(dst + o + 16 * q, OPEN ? p : c);
             const uint4 cq = crc_src<CRCMODE>(c, p);
             st.A = q == 0 ? p_mul_add(st.A, r253, s253, p_from_words(c.x, c.y, c.z, c.w, 1))
                           : p_mul_add(st.A, r1, s1, p_from_words(c.x, c.y, c.z, c.w, 1));

@@ -105,8 +105,14 @@ __device__ __forceinline__ uint32_t crc_u16_nib(const char *lds, uint32_t lb, ui
 // of each).  XPOSE = 1: instruction j loads the span's bytes 1024j + 16l
 // (one fully coalesced 1 KiB row, 8 whole lines); after quad_xpose lane
 // l = 4m + t holds the chunk at 64 (16t + m) of the span.
+// JFSX_CRC_NT = 1: the loads carry the non-temporal hint (the data is read
+// once; A/B in profiles/r4/ab_crc.txt)
+#ifndef JFSX_CRC_NT
+#define JFSX_CRC_NT 1
+#endif
+__device__ __forceinline__ uint4 crc_ld16(const uint8_t *p) { return JFSX_CRC_NT ? gld16_nt(p) : gld16(p); }
 __device__ __forceinline__ uint4 crc_chunk_ld(const uint8_t *seg, uint32_t lane, int r, int j) {
-    return JFSX_CRC_XPOSE ? gld16(seg + 4096 * r + 1024 * j + 16 * lane) : gld16(seg + 4096 * r + 64 * lane + 16 * j);
+    return JFSX_CRC_XPOSE ? crc_ld16(seg + 4096 * r + 1024 * j + 16 * lane) : crc_ld16(seg + 4096 * r + 64 * lane + 16 * j);
 }
 // lane chunk index within a span (the final shift to the segment end)
 __device__ __forceinline__ uint32_t crc_chunk_idx(uint32_t lane) {

@@ -87,9 +87,30 @@ __device__ __forceinline__ uint4 gld16(const uint8_t *p) {
     const v4u v = *(const gv4u *)(p);
     return make_uint4(v.x, v.y, v.z, v.w);
 }
+// the same with the non-temporal hint (a streaming read nothing reuses)
+__device__ __forceinline__ uint4 gld16_nt(const uint8_t *p) {
+    const v4u v = __builtin_nontemporal_load((const gv4u *)(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ void gst16(uint8_t *p, uint4 v) {
     v4u w = {v.x, v.y, v.z, v.w};
     *(gv4u *)(p) = w;
+}
+__device__ __forceinline__ void gst16_nt(uint8_t *p, uint4 v) {
+    v4u w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, (gv4u *)(p));
+}
+// the AEAD kernels' block streams (plaintext in, ciphertext out): JFSX_AEAD_NT
+// bit 1 gives the loads, bit 2 the stores the non-temporal hint (A/B)
+#ifndef JFSX_AEAD_NT
+#define JFSX_AEAD_NT 0
+#endif
+__device__ __forceinline__ uint4 ald16(const uint8_t *p) { return (JFSX_AEAD_NT & 1) ? gld16_nt(p) : gld16(p); }
+__device__ __forceinline__ void ast16(uint8_t *p, uint4 v) {
+    if (JFSX_AEAD_NT & 2)
+        gst16_nt(p, v);
+    else
+        gst16(p, v);
 }
 
 // guarded 16-byte load of [o, o+16) clipped at end (zero fill)

@@ -25,6 +25,12 @@
 #include <cstdio>
 #include <cstdlib>
 
+// plaintext in and ciphertext out as non-temporal block streams (coalesced
+// 1 KiB rows, read or written once): +0.7 % same box (profiles/r4/ab_gcm_rows.txt;
+// the ChaCha kernel's 64-byte lane runs lose 33 % with the hint and keep 0)
+#ifndef JFSX_AEAD_NT
+#define JFSX_AEAD_NT 3
+#endif
 #include "jfsx_dev.h"
 
 #define JFSX_HD __device__ __forceinline__
@@ -593,7 +599,7 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
         constexpr int PF = 4;  // rows of loads in flight
         uint4 pf[PF];
 #pragma unroll
-        for (int q = 0; q < PF; q++) pf[q] = gld16(src + ld0[0] + 1024 * q + lo);
+        for (int q = 0; q < PF; q++) pf[q] = ald16(src + ld0[0] + 1024 * q + lo);
         for (uint64_t sg = 0; sg < nfs; sg++) {
             const uint64_t base = ld0[0] + (uint64_t)kSeg * sg;
             uint32_t ks[128];
@@ -604,10 +610,10 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
             for (int k = 0; k < 32; k++) {
                 const uint4 d = pf[k % PF];
                 const uint64_t o = base + 1024 * k + lo;
-                if (k + PF < 32 || more) pf[k % PF] = gld16(src + o + 1024 * PF);
+                if (k + PF < 32 || more) pf[k % PF] = ald16(src + o + 1024 * PF);
                 const uint4 x = make_uint4(d.x ^ ks[k], d.y ^ ks[32 + k], d.z ^ ks[64 + k], d.w ^ ks[96 + k]);
                 const uint4 c = OPEN ? d : x, p = OPEN ? x : d;
-                gst16(dst + o, OPEN ? p : c);
+                ast16(dst + o, OPEN ? p : c);
                 const uint4 cq = crc_src<CRCMODE>(c, p);
 #ifndef JFSX_ABLATE_GHASH
                 ghash_step(lds, st[0].acc, gl, c);
@@ -631,7 +637,7 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
     uint4 nxt[NS];
 #pragma unroll
     for (int s = 0; s < NS; s++)
-        nxt[s] = r0 < rf ? gld16(src + ld0[s] + 1024 * r0 + lo) : make_uint4(0, 0, 0, 0);
+        nxt[s] = r0 < rf ? ald16(src + ld0[s] + 1024 * r0 + lo) : make_uint4(0, 0, 0, 0);
 #if JFSX_U2
     // UR rows of one stream per iteration (2 in the 16-wave shape; the 8-wave
     // shape has twice the VGPRs and takes JFSX_HYB_UR): the UR AES chains
@@ -640,7 +646,7 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
     if (NS == 1 && act[0] && rf >= r0 + UR) {
         uint4 nn[UR];
 #pragma unroll
-        for (int u = 0; u < UR; u++) nn[u] = gld16(src + ld0[0] + 1024 * (r0 + u) + lo);
+        for (int u = 0; u < UR; u++) nn[u] = ald16(src + ld0[0] + 1024 * (r0 + u) + lo);
 #if JFSX_UCTR
         uint32_t uw[4] = {0, 0, 0, 0};
         uint32_t uw0 = 0;
@@ -667,7 +673,7 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
             const uint64_t o0 = ld0[0] + 1024 * r0 + lo;
             if (r0 + 2 * UR - 1 < rf) {
 #pragma unroll
-                for (int u = 0; u < UR; u++) nn[u] = gld16(src + o0 + 1024 * (UR + u));
+                for (int u = 0; u < UR; u++) nn[u] = ald16(src + o0 + 1024 * (UR + u));
             }
             if (SWP && pend) {
 #pragma unroll
@@ -723,7 +729,7 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
                                            dd[u].w ^ ks2[u][3]);
 #endif
                 const uint4 c = OPEN ? dd[u] : x, p = OPEN ? x : dd[u];
-                gst16(dst + o, OPEN ? p : c);
+                ast16(dst + o, OPEN ? p : c);
                 const uint4 cq = crc_src<CRCMODE>(c, p);
                 if (SWP) {
                     pc[u] = c;
@@ -767,7 +773,7 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
                 st[0].seg0 += kSeg;
             }
         }
-        if (r0 < rf) nxt[0] = gld16(src + ld0[0] + 1024 * r0 + lo);
+        if (r0 < rf) nxt[0] = ald16(src + ld0[0] + 1024 * r0 + lo);
     }
 #endif
     for (uint64_t r = r0; r < rf; r++) {
@@ -777,7 +783,7 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
         for (int s = 0; s < NS; s++) {
             d[s] = nxt[s];
             const uint64_t o = ld0[s] + 1024 * r + lo;
-            if (r + 1 < rf) nxt[s] = gld16(src + o + 1024);
+            if (r + 1 < rf) nxt[s] = ald16(src + o + 1024);
             ctr[s] = (uint32_t)((o >> 4) + 2);
         }
         uint32_t ks[NS][4];
@@ -788,7 +794,7 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
             const uint64_t o = st[s].sub0 + 1024 * r + lo;
             const uint4 x = make_uint4(d[s].x ^ ks[s][0], d[s].y ^ ks[s][1], d[s].z ^ ks[s][2], d[s].w ^ ks[s][3]);
             const uint4 c = OPEN ? d[s] : x, p = OPEN ? x : d[s];
-            gst16(dst + o, OPEN ? p : c);
+            ast16(dst + o, OPEN ? p : c);
             const uint4 cq = crc_src<CRCMODE>(c, p);
             ghash_step(lds, st[s].acc, gl, c);
             if (CRCMODE) st[s].A = crc_piece<kLdsCrc>(lds, st[s].A, cq.x, cq.y, cq.z, cq.w);
