@@ -984,6 +984,43 @@ __device__ void aes_enc_global(const uint32_t *aes, const uint32_t *rk, const ui
     }
 }
 
+// z = x * y in GF(2^128) for a wave-uniform y and a per-lane x, four bits of
+// x per step (Horner from the high coefficients: z = z x^4 + y N_t), the 16
+// multiples y (n3 + n2 x + n1 x^2 + n0 x^3) in LDS.  About 600 instructions
+// against g_mul's 2000; every lane of the wave must call it (barriers).
+#ifndef JFSX_KS_NIB
+#define JFSX_KS_NIB 1  // 0: keysetup with the bit-serial g_mul (A/B)
+#endif
+__device__ __forceinline__ g128 g_mul_uy(const g128 &x, const g128 &y, uint4 *M, uint32_t lane) {
+    const g128 y1 = g_mulx(y), y2 = g_mulx(y1), y3 = g_mulx(y2);
+    __syncthreads();  // the previous call's readers are done with M
+    if (lane < 16) {
+        uint32_t m[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            m[k] = ((lane & 8) ? y.w[k] : 0u) ^ ((lane & 4) ? y1.w[k] : 0u) ^ ((lane & 2) ? y2.w[k] : 0u) ^
+                   ((lane & 1) ? y3.w[k] : 0u);
+        M[lane] = make_uint4(m[0], m[1], m[2], m[3]);
+    }
+    __syncthreads();
+    g128 z = {{0, 0, 0, 0}};
+#pragma unroll 4
+    for (int t = 31; t >= 0; t--) {
+        // z x^4: the four coefficients shifted out (low bits of w[3]) fold
+        // back as in four g_mulx steps
+        const uint32_t sh = z.w[3] & 15u;
+        z.w[3] = __builtin_amdgcn_alignbit(z.w[2], z.w[3], 4);
+        z.w[2] = __builtin_amdgcn_alignbit(z.w[1], z.w[2], 4);
+        z.w[1] = __builtin_amdgcn_alignbit(z.w[0], z.w[1], 4);
+        z.w[0] = (z.w[0] >> 4) ^ ((sh & 1u) ? 0xE1000000u >> 3 : 0u) ^ ((sh & 2u) ? 0xE1000000u >> 2 : 0u) ^
+                 ((sh & 4u) ? 0xE1000000u >> 1 : 0u) ^ ((sh & 8u) ? 0xE1000000u : 0u);
+        const uint32_t n = (x.w[t >> 3] >> (28 - 4 * (t & 7))) & 15u;
+        const uint4 mv = M[n];
+        z.w[0] ^= mv.x, z.w[1] ^= mv.y, z.w[2] ^= mv.z, z.w[3] ^= mv.w;
+    }
+    return z;
+}
+
 __global__ __launch_bounds__(64) void gcm_keysetup_k(const KeyIn *__restrict__ keys, const BlkDev *__restrict__ blks,
                                                     GcmSched *__restrict__ sched, const uint32_t *__restrict__ aes) {
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
@@ -1049,6 +1086,26 @@ __global__ __launch_bounds__(64) void gcm_keysetup_k(const KeyIn *__restrict__ k
         }
         g = g_sqr(g);
     }
+#if JFSX_KS_NIB
+    // H^e for e = lane (bits 0..5: six products by the uniform H^(2^q), each
+    // kept where the lane's bit is set), then H^(64 + e) = H^e H^64, e < 4
+    __shared__ uint4 gM[16];
+    {
+        g128 z = {{0x80000000u, 0, 0, 0}};  // x^0 = 1
+        for (int q = 0; q < 6; q++) {
+            const g128 m = g_mul_uy(z, hs[q], gM, lane);
+            if ((lane >> q) & 1) z = m;
+        }
+        const g128 z64 = g_mul_uy(z, hs[6], gM, lane);
+        uint32_t m[4];
+        g_to_mem(z, m);
+        for (int q = 0; q < 4; q++) sc->hpow[lane][q] = m[q];
+        if (lane < 4) {
+            g_to_mem(z64, m);
+            for (int q = 0; q < 4; q++) sc->hpow[64 + lane][q] = m[q];
+        }
+    }
+#else
     // H^e for e = lane and lane + 64 (< 68)
     for (int rep = 0; rep < 2; rep++) {
         const uint32_t e = lane + 64 * rep;
@@ -1060,6 +1117,7 @@ __global__ __launch_bounds__(64) void gcm_keysetup_k(const KeyIn *__restrict__ k
         g_to_mem(z, m);
         for (int q = 0; q < 4; q++) sc->hpow[e][q] = m[q];
     }
+#endif
     // basis x^i * H^64
     g128 v = hs[6];
     for (int i = 0; i < 128; i++) {
@@ -1071,13 +1129,19 @@ __global__ __launch_bounds__(64) void gcm_keysetup_k(const KeyIn *__restrict__ k
         v = g_mulx(v);
     }
     // init = E_K(J0) ^ (len block) * H, len block = 0^64 || BE64(8*len)
-    if (lane == 0) {
+    {
         const uint64_t bits = blks[b].len * 8;
         g128 L = {{0, 0, (uint32_t)(bits >> 32), (uint32_t)bits}};
-        g128 LH = g_mul(L, H);
-        uint32_t m[4];
-        g_to_mem(LH, m);
-        for (int q = 0; q < 4; q++) sc->init[q] = m[q] ^ EJ0[q];
+#if JFSX_KS_NIB
+        const g128 LH = g_mul_uy(L, H, gM, lane);  // every lane (barriers); lane 0 stores
+#else
+        const g128 LH = lane == 0 ? g_mul(L, H) : L;
+#endif
+        if (lane == 0) {
+            uint32_t m[4];
+            g_to_mem(LH, m);
+            for (int q = 0; q < 4; q++) sc->init[q] = m[q] ^ EJ0[q];
+        }
     }
 }
 
