@@ -10,8 +10,9 @@
 // Decomposition: the greedy parse of a frame is sequential from its first
 // byte to its last (one hash table and one set of repcodes and entropy
 // tables carried over all 128 KiB blocks), so one wave owns one object.
-// Persistent waves take objects from a queue; each has a global scratch (hash
-// table, sequences, literals, codes) and its entropy tables in LDS.
+// Persistent waves take objects w, w + W, ... (W waves; a ticket queue is an
+// A/B switch); each has a global scratch (hash table, sequences, literals,
+// codes) and its entropy tables in LDS.
 //
 // The parser (ZSTD_compressBlock_fast_generic) runs on the 64 lanes:
 //   * a search step evaluates 64 consecutive iterations of the serial loop at
