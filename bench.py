@@ -46,6 +46,8 @@ def parse():
                     help="aggcodec: the Compress / Decompress call of cachedStore.upload / load measured in the "
                          "reference's call shape")
     ap.add_argument("--agg-window-us", type=int, default=500, help="agg: aggregation window")
+    ap.add_argument("--agg-max-mb", type=int, default=16,
+                    help="agg: byte cap of one aggregated batch (several batches pipeline at once)")
     ap.add_argument("--algo", choices=["aes256gcm", "chacha20poly1305"], default="aes256gcm")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
@@ -66,6 +68,18 @@ def parse():
                     help="AES-GCM keystream kernel: T-table AES in LDS, or bitsliced AES on the VALU")
     ap.add_argument("--lz4-data", choices=["text", "random"], default="text",
                     help="lz4/unlz4 modes (SURVEY 8f-4): word text (compressible) or SplitMix64 bytes")
+    ap.add_argument("--engine", choices=["process", "mctx"], default="process",
+                    help="process: one process per GPU (torch.distributed ranks, the driver's form); mctx: ONE process "
+                         "drives --gpus GPUs through the multi-device context (jfsx_mctx_*), the path the Go shim "
+                         "ships (INTEGRATION.md)")
+    ap.add_argument("--total-gib", type=float, default=0.0,
+                    help="strong scaling: a fixed total of GiB per step split across the GPUs "
+                         "(juicefs_amd.shard.shard_strong); each GPU loops over a resident batch of at most "
+                         "--blocks blocks (device) or --host-pool-gib (host) to make up its share.  "
+                         "configs[3]: --mode open --total-gib 2048")
+    ap.add_argument("--host-pool-gib", type=float, default=8.0,
+                    help="host mode: pinned input pool per GPU (the output pool is the same size), NUMA-local to "
+                         "the GPU; a step loops over it to make up the GPU's blocks")
     ap.add_argument("--dry-run", action="store_true",
                     help="test hook: the launcher, process group, shard layout, barrier and max-over-ranks timing "
                          "with no engine (no GPU); prints the JSON line with value null")
@@ -182,37 +196,80 @@ def cpu_baseline(args, mode="seal", lens=None):
             "sample": "%d x %s %s, %d threads (%s), %s" % (reps, blocks, what, threads, note, cpu_model())}
 
 
-def dry_run(args, world, rank, local, dist):
-    """No engine: exercises the rank launch, the shard layout, the barrier and
-    the max-over-ranks timing the real bench uses (tests/test_dist_gloo.py)."""
+def shard_plan(args, nshard, s):
+    """The blocks of shard s (a rank, or one GPU of --engine mctx): (base
+    global block index, blocks per step, resident blocks, blocks per loop).
+    Weak scaling: --blocks per shard, one call per step.  Strong scaling
+    (--total-gib): the fixed total is split by shard.shard_strong, and the
+    shard loops over a resident batch (at most --blocks on the device, or the
+    --host-pool-gib pinned pool in host mode) until its share is done."""
     from juicefs_amd import shard
-    blocks = shard.shard(args.blocks, rank)
+    L = args.block_bytes
+    cap = args.blocks if args.mem == "device" else max(1, int(args.host_pool_gib * 2**30) // L)
+    if args.total_gib:
+        total = max(nshard, int(round(args.total_gib * 2**30 / L)))
+        r = shard.shard_strong(total, s, nshard)
+        base, count = r.start, len(r)
+    else:
+        base, count = s * args.blocks, args.blocks
+    resident = max(1, min(cap, count))
+    loops = [resident] * (count // resident) + ([count % resident] if count % resident else [])
+    return base, count, resident, loops
+
+
+def dry_run(args, world, rank, local, dist):
+    """No engine: exercises the rank launch, the shard layout (weak or strong),
+    the barrier and the max-over-ranks timing the real bench uses
+    (tests/test_dist_gloo.py)."""
+    from juicefs_amd import shard
+    base, count, resident, loops = shard_plan(args, world, rank)
     barrier(dist)
     t0 = time.perf_counter()
     barrier(dist)
     el = max_over_ranks(dist, time.perf_counter() - t0 + 0.001 * rank, local)
-    first = max_over_ranks(dist, float(blocks[0]), local)
+    first = max_over_ranks(dist, float(base), local)
+    total = shard.sum_over_ranks(dist, count, local)
+    lo = -max_over_ranks(dist, -float(base), local)
+    hi = max_over_ranks(dist, float(base + count), local)
+    per_max = max_over_ranks(dist, float(count), local)
     if rank == 0:
         print(json.dumps({"metric": "dry run (no engine)", "value": None, "unit": "GB/s", "n_gpus": world,
                           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3, 3),
-                          "dry_run": True, "last_rank_first_block": int(first),
-                          "config": {"blocks_per_gpu": args.blocks,
+                          "dry_run": True, "last_rank_first_block": int(first), "scaling": scaling(args),
+                          "blocks_total": int(total), "block_range": [int(lo), int(hi)],
+                          "per_gpu_blocks_max": int(per_max), "resident_blocks": resident, "loops_per_step": len(loops),
+                          "config": {"blocks_per_gpu": args.blocks, "total_gib": args.total_gib or None,
                                      "parallelism": "block-sharded x%d, no collective" % world}}), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
 
+def scaling(args):
+    return "strong" if args.total_gib else "weak"
+
+
 def main():
     args = parse()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    if args.engine == "mctx":
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            raise SystemExit("bench: --engine mctx is one process over --gpus GPUs; run it without the launcher")
+        if args.mode not in ("seal", "open", "decrypt", "crc"):
+            raise SystemExit("bench: --engine mctx measures the seal / open / decrypt / crc modes")
+    elif args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args))
+    if args.total_gib and args.ragged:
+        raise SystemExit("bench: --total-gib splits 4 MiB blocks; ragged batches are weak-scaled")
     world, rank, local, dist = dist_setup(args)
-    if args.gpus > 1 and world != args.gpus:
+    if args.gpus > 1 and args.engine == "process" and world != args.gpus:
         raise SystemExit("bench: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     if args.dry_run:
         return dry_run(args, world, rank, local, dist)
     from juicefs_amd import engine as E
 
+    if args.mem == "host":
+        return host_ingest(args, world, rank, local, dist)
+    if args.mode in ("seal", "open", "decrypt", "crc"):
+        return resident_bench(args, world, rank, local, dist)
     eng = E.Engine(local, E.CTX_BITSLICE if args.aes == "bitslice" else 0)
     if args.mode == "agg":
         return agg_bench(args, world, rank, local, dist, eng)
@@ -222,194 +279,418 @@ def main():
         return lz4_bench(args, world, rank, local, dist, eng)
     if args.mode == "unzstd":
         return zstd_bench(args, world, rank, local, dist, eng)
-    if args.mode == "zstd":
-        return zstdc_bench(args, world, rank, local, dist, eng)
-    if args.mem == "host":
-        return host_ingest(args, world, rank, local, dist, eng)
-    nb, L = args.blocks, args.block_bytes
-    algo = E.AES256GCM if args.algo == "aes256gcm" else E.CHACHA20P1305
-    nseg = -(-L // E.SEG)
-    src = eng.alloc(nb * L)
-    dst = eng.alloc(nb * L) if args.mode != "crc" else None
-    crc = eng.alloc(nb * 4 * nseg)
-    base = rank * nb  # global block index: blocks shard across ranks (juicefs_amd.shard.shard)
+    return zstdc_bench(args, world, rank, local, dist, eng)
+
+
+def open_engines(args, local):
+    """(MultiEngine or None, [Engine per shard]): one context for this rank's
+    GPU, or every context of a multi-device context over --gpus GPUs."""
+    from juicefs_amd import engine as E
+    flags = E.CTX_BITSLICE if args.aes == "bitslice" else 0
+    if args.engine == "mctx":
+        m = E.MultiEngine((1 << args.gpus) - 1, flags)
+        return m, [m.member(k) for k in range(m.ndev)]
+    return None, [E.Engine(local, flags)]
+
+
+class Shard:
+    """The resident blocks one GPU holds: buffers, lengths, descriptors' place
+    in the combined array (off)."""
+
+
+def make_shard(args, E, eng, nshard, s):
+    sh = Shard()
+    sh.eng, sh.s = eng, s
+    sh.base, sh.count, sh.nb, sh.loops = shard_plan(args, nshard, s)
+    nb, L = sh.nb, args.block_bytes
+    sh.nseg = -(-L // E.SEG)
     # block b occupies slot [b*L, b*L + lens[b]); ragged lengths are a seeded
-    # draw per global block index, so every rank and rerun sees the same batch
-    lens = [ragged_len(SEED, base + b, L) if args.ragged else (args.fixed_len or L) for b in range(nb)]
+    # draw per global block index, so every shard and rerun sees the same batch
+    lens = [ragged_len(SEED, sh.base + b, L) if args.ragged else (args.fixed_len or L) for b in range(nb)]
     if args.ragged and args.ragged_align:
         lens = [min(L, -(-x // args.ragged_align) * args.ragged_align) for x in lens]
+    sh.lens = lens
+    sh.src = eng.alloc(nb * L)
+    sh.dst = eng.alloc(nb * L) if args.mode != "crc" else None
+    sh.crc = eng.alloc(nb * 4 * sh.nseg)
     if args.packed:
         offs, o = [], 0
         for x in lens:
             offs.append(o)
             o += -(-x // 256) * 256
         for b in range(nb):
-            eng.gen_synthetic_batch(src, L, [lens[b]], SEED, base + b, offset=offs[b])
+            eng.gen_synthetic_batch(sh.src, L, [lens[b]], SEED, sh.base + b, offset=offs[b])
     else:
         offs = [b * L for b in range(nb)]
-        eng.gen_synthetic_batch(src, L, lens, SEED, base)  # one launch for the whole batch
-
+        eng.gen_synthetic_batch(sh.src, L, lens, SEED, sh.base)  # one launch for the whole batch
+    sh.offs = offs
     if args.mode == "crc":
-        ranges = (E.jfsx_range * nb)()
+        sh.specs = [(sh.src.ptr + offs[b], lens[b], sh.crc.ptr + 4 * sh.nseg * b) for b in range(nb)]
+    else:
+        sh.specs = []
         for b in range(nb):
-            ranges[b].data, ranges[b].len, ranges[b].crc = src.ptr + offs[b], lens[b], crc.ptr + 4 * nseg * b
-        eng.crc32c_segments(ranges, nb, E.CRC_GEN, E.MEM_DEVICE)
+            key, nonce = E.gen_key(SEED, sh.base + b)
+            sh.specs.append({"key": key, "nonce": nonce, "src": sh.src.ptr + offs[b], "dst": sh.dst.ptr + offs[b],
+                             "len": lens[b], "crc": sh.crc.ptr + 4 * sh.nseg * b})
+    return sh
+
+
+def make_ranges(specs):
+    import ctypes
+    from juicefs_amd import engine as E
+    arr = (E.jfsx_range * max(len(specs), 1))()
+    for i, (d, n, c) in enumerate(specs):
+        arr[i].data, arr[i].len, arr[i].crc = d, n, c
+    return arr
+
+
+def loop_arrays(A, shards):
+    """The calls of one step: loop j runs, on every shard, the first
+    sh.loops[j] of its resident blocks.  (array, n, [(shard, offset, count)])
+    per loop; a loop that covers every shard's whole batch uses the combined
+    array itself, a shorter last loop a compacted copy of the prefixes."""
+    import ctypes
+    J = max(len(sh.loops) for sh in shards)
+    out = []
+    for j in range(J):
+        cnts = [sh.loops[j] if j < len(sh.loops) else 0 for sh in shards]
+        if all(c == sh.nb for c, sh in zip(cnts, shards)):
+            out.append((A, sum(cnts), [(sh, sh.off, sh.nb) for sh in shards]))
+        elif len(shards) == 1:
+            out.append((A, cnts[0], [(shards[0], 0, cnts[0])]))
+        else:
+            T = type(A[0])
+            n = sum(cnts)
+            B = (T * max(n, 1))()
+            o, parts = 0, []
+            for c, sh in zip(cnts, shards):
+                if c:
+                    ctypes.memmove(ctypes.addressof(B[o]), ctypes.addressof(A[sh.off]), c * ctypes.sizeof(T))
+                    parts.append((sh, o, c))
+                o += c
+            out.append((B, n, parts))
+    return out
+
+
+def resident_bench(args, world, rank, local, dist):
+    """BASELINE configs[1] (seal), configs[3] (open / decrypt + CRC verify)
+    and configs[4] (--ragged), and the cache-hit verify (crc): blocks resident
+    in HBM, one call per loop of every shard's resident batch.  --engine
+    process: this rank's GPU; --engine mctx: one jfsx_mctx_* call over every
+    GPU's blocks (each block runs on the GPU that owns it)."""
+    import ctypes
+    from concurrent.futures import ThreadPoolExecutor
+    from juicefs_amd import engine as E
+    from juicefs_amd import shard as S
+    m, engs = open_engines(args, local)
+    nshard = len(engs) if m else world
+    shards = [make_shard(args, E, e, nshard, k if m else rank) for k, e in enumerate(engs)]
+    off = 0
+    for sh in shards:
+        sh.off = off
+        off += sh.nb
+    algo = E.AES256GCM if args.algo == "aes256gcm" else E.CHACHA20P1305
+    front = m if m else engs[0]
+    specs = [x for sh in shards for x in sh.specs]
+    mode = args.mode
+    if mode == "crc":
+        R = make_ranges(specs)
+        front.crc32c_segments(R, len(specs), E.CRC_GEN, E.MEM_DEVICE)  # the cache files' stored CRCs
+        loops = loop_arrays(R, shards)
 
         def step():
-            eng.crc32c_segments(ranges, nb, E.CRC_VERIFY, E.MEM_DEVICE)
-        algo_bytes = sum(lb + 4 * -(-lb // E.SEG) for lb in lens)
+            for arr, n, _ in loops:
+                front.crc32c_segments(arr, n, E.CRC_VERIFY, E.MEM_DEVICE)
+        per_blk = [[lb + 4 * -(-lb // E.SEG) for lb in sh.lens] for sh in shards]
     else:
-        specs = []
-        for b in range(nb):
-            key, nonce = E.gen_key(SEED, base + b)
-            specs.append({"key": key, "nonce": nonce, "src": src.ptr + offs[b], "dst": dst.ptr + offs[b], "len": lens[b],
-                          "crc": crc.ptr + 4 * nseg * b})
-        blks, n = eng.make_blocks(specs)
-        if args.mode == "seal":
+        A, _ = E.Engine.make_blocks(specs)
+        if mode == "seal":
+            loops = loop_arrays(A, shards)
+            crc_mode = E.CRC_GEN if args.crc == "full" else E.CRC_NONE
+
             def step():
-                eng.seal_batch(algo, blks, n, E.CRC_GEN if args.crc == "full" else E.CRC_NONE, E.MEM_DEVICE)
+                for arr, n, _ in loops:
+                    front.seal_batch(algo, arr, n, crc_mode, E.MEM_DEVICE)
         else:
-            # Open + CRC verify (BASELINE configs[3]): make a sealed image first
-            eng.seal_batch(algo, blks, n, E.CRC_GEN, E.MEM_DEVICE)
-            oblks, _ = eng.make_blocks([dict(s, src=s["dst"], dst=s["src"], tag=bytes(blks[i].tag))
-                                        for i, s in enumerate(specs)])
-            if args.mode == "open":
+            # Open + CRC verify (BASELINE configs[3]): seal an image first
+            front.seal_batch(algo, A, len(specs), E.CRC_GEN, E.MEM_DEVICE)
+            O, _ = E.Engine.make_blocks([dict(sp, src=sp["dst"], dst=sp["src"], tag=bytes(A[i].tag))
+                                         for i, sp in enumerate(specs)])
+            loops = loop_arrays(O, shards)
+            if mode == "open":
                 def step():
-                    eng.open_batch(algo, oblks, n, E.CRC_VERIFY, E.MEM_DEVICE)
+                    for arr, n, _ in loops:
+                        front.open_batch(algo, arr, n, E.CRC_VERIFY, E.MEM_DEVICE)
             else:
                 # Decrypt end to end: every object's key arrives RSA-OAEP
-                # wrapped (encrypt.go:196-216); each step unwraps all n keys on
-                # the GPU straight into the descriptors, then opens
-                import ctypes
+                # wrapped (encrypt.go:196-216); each loop unwraps its blocks'
+                # keys on their GPUs straight into the descriptors, then opens
                 import numpy as np
                 from juicefs_amd import encrypt as enc
                 rsae = enc.NewRSAEncryptor(enc.GenerateRsaKey(2048))
-                dkey = eng.rsa_key(*enc.rsa_crt_components(rsae.privKey))
-                wrapped = np.frombuffer(b"".join(rsae.Encrypt(bytes(specs[i]["key"])) for i in range(n)), np.uint8)
-                wlen = np.full(n, 256, np.uint32)
-                mlen = np.zeros(n, np.int32)
-                for i in range(n):
-                    ctypes.memset(ctypes.addressof(oblks[i]) + E.jfsx_blk.key.offset, 0, 32)
+                comps = enc.rsa_crt_components(rsae.privKey)
+                for sh in shards:
+                    sh.dkey = sh.eng.rsa_key(*comps)
+                    sh.wrapped = np.frombuffer(b"".join(rsae.Encrypt(bytes(sp["key"])) for sp in sh.specs), np.uint8)
+                    sh.wlen = np.full(sh.nb, 256, np.uint32)
+                    sh.mlen = np.zeros(sh.nb, np.int32)
+                for arr, n, _ in loops:
+                    for i in range(n):
+                        ctypes.memset(ctypes.addressof(arr[i]) + E.jfsx_blk.key.offset, 0, 32)
+                pool = ThreadPoolExecutor(len(shards))
+
+                def unwrap(part, arr):
+                    sh, o, c = part
+                    sh.eng._check(sh.eng.L.jfsx_rsa_oaep_decrypt_batch(
+                        sh.eng.ctx, sh.dkey, c, sh.wrapped.ctypes.data, 256, sh.wlen.ctypes.data,
+                        ctypes.addressof(arr[o]) + E.jfsx_blk.key.offset, ctypes.sizeof(E.jfsx_blk),
+                        sh.mlen.ctypes.data), "unwrap")
 
                 def step():
-                    eng._check(eng.L.jfsx_rsa_oaep_decrypt_batch(
-                        eng.ctx, dkey, n, wrapped.ctypes.data, 256, wlen.ctypes.data,
-                        ctypes.addressof(oblks[0]) + E.jfsx_blk.key.offset, ctypes.sizeof(E.jfsx_blk),
-                        mlen.ctypes.data), "unwrap")
-                    eng.open_batch(algo, oblks, n, E.CRC_VERIFY, E.MEM_DEVICE)
-        algo_bytes = sum(2 * lb + 16 + 4 * -(-lb // E.SEG) + 44 for lb in lens)
+                    for arr, n, parts in loops:
+                        if len(parts) == 1:
+                            unwrap(parts[0], arr)
+                        else:
+                            list(pool.map(lambda p: unwrap(p, arr), parts))
+                        front.open_batch(algo, arr, n, E.CRC_VERIFY, E.MEM_DEVICE)
+        per_blk = [[2 * lb + 16 + 4 * -(-lb // E.SEG) + 44 for lb in sh.lens] for sh in shards]
+    # algorithmic bytes and plaintext bytes one step moves on each shard
+    step_algo = [sum(sum(pb[:c]) for c in sh.loops) for pb, sh in zip(per_blk, shards)]
+    step_plain = [sum(sum(sh.lens[:c]) for c in sh.loops) for sh in shards]
 
     for _ in range(args.warmup):
         step()
-    eng.sync()
-    eng.kernel_time(reset=True)
-    eng.set_timing(True)
+    for e in engs:
+        e.sync()
+        e.kernel_time(reset=True)
+        e.set_timing(True)
     barrier(dist)
-    eng.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    eng.sync()
+    for e in engs:
+        e.sync()
     barrier(dist)
     t1 = time.perf_counter()
-    eng.set_timing(False)
+    for e in engs:
+        e.set_timing(False)
     el = max_over_ranks(dist, t1 - t0, local)
-    k_ms, k_n = eng.kernel_time(reset=True)
-    k_avg_ms = k_ms / max(k_n, 1)
+    ktimes = [e.kernel_time(reset=True) for e in engs]
 
-    # post-timing spot check of a few blocks against the oracle (checker only)
-    verified = 0
-    if args.mode in ("open", "decrypt"):
-        bad = [i for i in range(nb) if oblks[i].status != E.OK]
-        if args.mode == "decrypt":
-            bad += [i for i in range(nb) if mlen[i] != 32 or bytes(oblks[i].key) != bytes(specs[i]["key"])]
-        if bad:
-            raise SystemExit("bench: %d blocks failed to open (first %d)" % (len(bad), bad[0]))
-        verified = nb
-    rsa = None
-    if args.mode == "decrypt":
-        # the unwrap alone (GPU batch) beside the reference's host path
-        # (libcrypto RSA-OAEP, one thread) on a bounded sample
-        t = time.perf_counter()
-        eng._check(eng.L.jfsx_rsa_oaep_decrypt_batch(eng.ctx, dkey, n, wrapped.ctypes.data, 256, wlen.ctypes.data,
-                                                     None, 0, mlen.ctypes.data), "unwrap")
-        gpu_s = time.perf_counter() - t
-        sample = [bytes(wrapped[256 * i:256 * i + 256]) for i in range(min(n, 200))]
-        t = time.perf_counter()
-        for w in sample:
-            rsae.Decrypt(w)
-        host_s = (time.perf_counter() - t) / len(sample)
-        rsa = {"unwraps": n, "gpu_ms_per_batch": round(gpu_s * 1e3, 3), "gpu_unwraps_per_s": round(n / gpu_s),
-               "host_us_per_unwrap_1thread": round(host_s * 1e6, 1),
-               "host_sample": "%d libcrypto RSA-OAEP decrypts, 1 thread" % len(sample)}
-        eng.rsa_key_free(dkey)
-    full = None
-    if args.verify and args.mode in ("seal", "open", "crc") and (args.crc == "full" or args.mode != "seal"):
-        # every block's tag and CRC array against the oracle (host cores)
-        full = full_check(args, E, blks if args.mode != "crc" else None,
-                          crc.download(nb * 4 * nseg).reshape(nb, 4 * nseg), lens, base)
-    if args.verify and args.mode == "seal":
-        # and the ciphertext bytes of a few blocks
-        from oracle import oracle as orc
-        for b in range(0, nb, max(1, nb // args.verify))[:args.verify]:
-            p = orc.gen_block(SEED, base + b, lens[b])
-            key, nonce = orc.gen_key(SEED, base + b)
-            c, tag = orc.seal(orc.AES256GCM if algo == E.AES256GCM else orc.CHACHA20P1305, key, nonce, p,
-                              fast=algo == E.AES256GCM)
-            if bytes(blks[b].tag) != tag or dst.download(lens[b], offset=offs[b]).tobytes() != c:
-                raise SystemExit("bench: block %d differs from the oracle" % b)
-    if full:
-        verified = nb
+    # checker only, after the timed region: every block against the oracle
+    full, rsa = None, None
+    if args.verify:
+        full = check_resident(args, E, shards, A if mode != "crc" else None, O if mode in ("open", "decrypt") else None,
+                              R if mode == "crc" else None, loops, algo)
+    if mode == "decrypt":
+        rsa = rsa_line(shards[0], rsae)
+        for sh in shards:
+            sh.eng.rsa_key_free(sh.dkey)
 
-    total_plain = world * sum(lens) * args.steps
+    total_plain = S.sum_over_ranks(dist, sum(step_plain), local) * args.steps
     value = total_plain / el / 1e9
-    achieved = algo_bytes / (k_avg_ms / 1e3) / 1e9 if k_n else None
+    # per GPU: its algorithmic bytes over its own summed main-kernel time
+    ach = [step_algo[k] * args.steps / (ms / 1e3) / 1e9 for k, (ms, n) in enumerate(ktimes) if n]
+    achieved = sum(ach) / len(ach) if ach else None
+    k_avg_ms = sum(ms / max(n, 1) for ms, n in ktimes) / len(ktimes)
+    launches = sum(n for _, n in ktimes)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args, "open" if args.mode in ("open", "decrypt") else args.mode,
-                           lens if args.ragged else None)
-        if args.mode == "decrypt" and rsa:
+        cpu = cpu_baseline(args, "open" if mode in ("open", "decrypt") else mode,
+                           shards[0].lens if args.ragged else None)
+        if mode == "decrypt" and rsa:
             # each object also pays one RSA-OAEP private-key unwrap on the host
             # (encrypt.go:207-210): per thread, block time + unwrap time
             per_block = cpu["cores"] * BLOCK / (cpu["value"] * 1e9)
             cpu["value"] = round(cpu["cores"] * BLOCK / (per_block + rsa["host_us_per_unwrap_1thread"] * 1e-6) / 1e9, 3)
             cpu["sample"] += "; plus one libcrypto RSA-OAEP unwrap per block (%.1f us, measured on 1 thread)" % (
                 rsa["host_us_per_unwrap_1thread"])
-    traffic, traffic_src, binding = pmc_traffic(args, sum(lens))
+    resident_plain = sum(shards[0].lens)
+    traffic, traffic_src, binding = pmc_traffic(args, resident_plain)
+    ngpu = len(engs) if m else world
     if rank == 0:
+        what = {"seal": "sealed+checksummed GB/s, %s", "open": "opened+verified GB/s, %s",
+                "decrypt": "decrypted (RSA unwrap + open + verify) GB/s, %s", "crc": "CRC32C-verified GB/s, %s"}[mode]
+        blocks_txt = "ragged 64 KiB-4 MiB blocks" if args.ragged else "4 MiB blocks"
+        sh0 = shards[0]
+        if args.total_gib:
+            workload = ("%s GiB per step split across %d GPUs (%s GiB each), %s %s + CRC32C %s; each GPU loops %d x "
+                        "over a resident batch of %d blocks" % (
+                            args.total_gib, ngpu, round(sh0.count * args.block_bytes / 2**30, 3), args.algo, mode,
+                            "full" if mode == "seal" else "verify", len(sh0.loops), sh0.nb))
+        else:
+            workload = "%s GiB device-resident batch of %s blocks per GPU, %s %s + CRC32C %s" % (
+                round(resident_plain / 2**30, 3), "ragged 64 KiB-4 MiB" if args.ragged else "4 MiB", args.algo, mode,
+                "full" if mode == "seal" else "verify")
         line = {
-            "metric": ("sealed+checksummed GB/s, %s" if args.mode == "seal" else
-                       ("opened+verified GB/s, %s" if args.mode == "open" else
-                        ("decrypted (RSA unwrap + open + verify) GB/s, %s" if args.mode == "decrypt" else
-                         "CRC32C-verified GB/s, %s"))) % (
-                          "ragged 64 KiB-4 MiB blocks" if args.ragged else "4 MiB blocks"),
-            "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic (SplitMix64 blocks, "
-            "per-block SplitMix64 keys/nonces), device-resident",
-            "config": {"workload": "%s GiB device-resident batch of %s blocks per GPU, %s %s + CRC32C %s" % (
-                round(sum(lens) / 2**30, 3), "ragged 64 KiB-4 MiB" if args.ragged else "4 MiB", args.algo, args.mode,
-                "full" if args.mode == "seal" else "verify"),
-                "blocks_per_gpu": nb, "block_bytes": "ragged" if args.ragged else L, "algo": args.algo,
-                "mode": args.mode, "aes_kernel": args.aes if args.algo == "aes256gcm" and args.mode != "crc" else None,
-                "parallelism": "block-sharded x%d, no collective" % world},
+            "metric": what % blocks_txt, "value": round(value, 2), "unit": "GB/s", "n_gpus": ngpu,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": scaling(args), "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (SplitMix64 blocks, per-block SplitMix64 keys/nonces), device-resident",
+            "config": {"workload": workload, "blocks_per_gpu": sh0.count, "resident_blocks_per_gpu": sh0.nb,
+                       "block_bytes": "ragged" if args.ragged else args.block_bytes, "algo": args.algo,
+                       "mode": mode, "aes_kernel": args.aes if args.algo == "aes256gcm" and mode != "crc" else None,
+                       "engine": "jfsx_mctx (one process, %d GPUs)" % ngpu if m else "one process per GPU",
+                       "total_gib": args.total_gib or None,
+                       "parallelism": "block-sharded x%d, no collective" % ngpu},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None, "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         "kernel": ("crc_segments_k" if args.mode == "crc" else
+                         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": ("crc_segments_k" if mode == "crc" else
                                     ("gcm_main_k" if args.algo == "aes256gcm" else "cp_main_k")),
-                         "kernel_avg_ms": round(k_avg_ms, 3), "algorithmic_bytes_per_launch": algo_bytes,
-                         "plain_bytes_per_launch": sum(lens), "binding": binding},
+                         "kernel_avg_ms": round(k_avg_ms, 3), "kernel_launches": launches,
+                         "achieved_basis": "per GPU: algorithmic bytes of its launches / its summed main-kernel "
+                                           "time (HIP events on the context's stream); mean over GPUs",
+                         "algorithmic_bytes_per_launch": sum(per_blk[0]),
+                         "plain_bytes_per_launch": resident_plain, "binding": binding},
             "cpu_baseline": cpu,
-            "verified_blocks": verified,
+            "verified_blocks": full["blocks"] if full else 0,
             "full_check": full,
             **({"rsa_unwrap": rsa} if rsa else {}),
         }
+        if m and len(ach) > 1:
+            line["roofline"]["achieved_per_gpu"] = [round(a, 1) for a in ach]
         print(json.dumps(line), flush=True)
-    eng.close()
+    for sh in shards:
+        for b in (sh.src, sh.dst, sh.crc):
+            if b is not None:
+                b.free()
+    if m:
+        m.close()
+    else:
+        engs[0].close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def rsa_line(sh, rsae):
+    """The unwrap alone (one GPU batch of the shard's keys) beside the
+    reference's host path (libcrypto RSA-OAEP, one thread) on a bounded
+    sample."""
+    t = time.perf_counter()
+    sh.eng._check(sh.eng.L.jfsx_rsa_oaep_decrypt_batch(sh.eng.ctx, sh.dkey, sh.nb, sh.wrapped.ctypes.data, 256,
+                                                       sh.wlen.ctypes.data, None, 0, sh.mlen.ctypes.data), "unwrap")
+    gpu_s = time.perf_counter() - t
+    sample = [bytes(sh.wrapped[256 * i:256 * i + 256]) for i in range(min(sh.nb, 200))]
+    t = time.perf_counter()
+    for w in sample:
+        rsae.Decrypt(w)
+    host_s = (time.perf_counter() - t) / len(sample)
+    return {"unwraps": sh.nb, "gpu_ms_per_batch": round(gpu_s * 1e3, 3), "gpu_unwraps_per_s": round(sh.nb / gpu_s),
+            "host_us_per_unwrap_1thread": round(host_s * 1e6, 1),
+            "host_sample": "%d libcrypto RSA-OAEP decrypts, 1 thread" % len(sample)}
+
+
+def check_resident(args, E, all_shards, A, O, R, loops, algo):
+    """Every block of every shard against the oracle (host cores), after the
+    timed region; exits non-zero on a difference.
+      seal   the timed call's tags and CRC arrays, all blocks; ciphertext of a
+             few blocks per shard
+      open / decrypt
+             setup: the sealed image's tags and CRC arrays, all blocks;
+             timed: every block's Open status OK (tag and stored CRCs
+             verified, keys unwrapped for decrypt), a few plaintexts per
+             shard equal to the oracle's, and two negative controls -- a
+             flipped tag fails (ETAG, output zeroed) and a corrupted stored
+             CRC fails at its segment (ECRC)
+      crc    setup: the GEN arrays, all blocks; timed: every VERIFY status
+             OK and a corrupted stored CRC caught at its segment"""
+    import ctypes
+    from oracle import oracle as orc
+    mode = args.mode
+    out = {"blocks": 0}
+    tags, crcs = [], []
+    shards = all_shards
+    if mode == "seal" and args.crc != "full":
+        shards = []  # CRC ablation: no CRC arrays to compare; the ciphertext samples below
+    for sh in shards:
+        got = sh.crc.download(sh.nb * 4 * sh.nseg).reshape(sh.nb, 4 * sh.nseg)
+        blks = [A[sh.off + i] for i in range(sh.nb)] if A is not None else None
+        f = full_check(args, E, blks, got, sh.lens, sh.base)
+        out["blocks"] += f["blocks"]
+        tags.append(f.get("tags_sha256"))
+        crcs.append(f["crc_arrays_sha256"])
+        out["oracle_s"] = round(out.get("oracle_s", 0) + f["oracle_s"], 2)
+        out["oracle_threads"] = f["oracle_threads"]
+    out["crc_arrays_sha256"] = crcs[0] if len(crcs) == 1 else crcs
+    if A is not None:
+        out["tags_sha256"] = tags[0] if len(tags) == 1 else tags
+    n = out["blocks"]
+    if mode == "seal":
+        samples = 0
+        for sh in all_shards:
+            for b in range(0, sh.nb, max(1, sh.nb // args.verify))[:args.verify]:
+                p = orc.gen_block(SEED, sh.base + b, sh.lens[b])
+                key, nonce = orc.gen_key(SEED, sh.base + b)
+                c, tag = orc.seal(orc.AES256GCM if algo == E.AES256GCM else orc.CHACHA20P1305, key, nonce, p,
+                                  fast=algo == E.AES256GCM)
+                if bytes(A[sh.off + b].tag) != tag or sh.dst.download(sh.lens[b], offset=sh.offs[b]).tobytes() != c:
+                    raise SystemExit("bench: block %d of GPU %d differs from the oracle" % (b, sh.s))
+                samples += 1
+        out["ciphertext_samples"] = samples
+        if not shards:
+            out["blocks"] = samples
+            out["what"] = "timed Seal (CRC none): %d tags and ciphertexts equal to the oracle's" % samples
+        else:
+            out["what"] = ("timed Seal: tags and CRC arrays of all %d blocks, and %d ciphertexts, equal to the "
+                           "oracle's" % (n, samples))
+        return out
+    # the timed calls' own results: the last loop that ran each block
+    st_bad = 0
+    for arr, cnt, _ in loops:
+        for i in range(cnt):
+            st_bad += arr[i].status != E.OK
+    if mode == "decrypt":
+        for sh in shards:
+            st_bad += int((sh.mlen[:max(sh.loops)] != 32).sum())
+        for arr, cnt, parts in loops:
+            for s_, o, c in parts:
+                st_bad += sum(bytes(arr[o + i].key) != bytes(s_.specs[i]["key"]) for i in range(c))
+    if st_bad:
+        raise SystemExit("bench: %d timed %s results failed" % (st_bad, mode))
+    sh = shards[0]
+    scratch = sh.eng.alloc(max(sh.lens[0], 16) + 4 * sh.nseg)
+    bad_crc = bytearray(sh.crc.download(4 * sh.nseg).tobytes())
+    seg = min(3, len(bad_crc) // 4 - 1)
+    bad_crc[4 * seg] ^= 0x40
+    scratch.upload(bytes(bad_crc), max(sh.lens[0], 16))
+    if mode == "crc":
+        one = make_ranges([(sh.src.ptr + sh.offs[0], sh.lens[0], scratch.ptr + max(sh.lens[0], 16))])
+        sh.eng.crc32c_segments(one, 1, E.CRC_VERIFY, E.MEM_DEVICE)
+        if one[0].status != E.ECRC or one[0].bad_seg != seg:
+            raise SystemExit("bench: a corrupted stored CRC was not caught (%d, %d)" % (one[0].status, one[0].bad_seg))
+        out["what"] = ("setup: CRC arrays of all %d blocks equal to the oracle's; timed VERIFY: all %d statuses OK, "
+                       "and a corrupted stored CRC caught at segment %d (ECRC)" % (n, n, seg))
+        scratch.free()
+        return out
+    # plaintext of a few blocks per shard: Open wrote it back over the source
+    samples = 0
+    for s in shards:
+        for b in range(0, s.nb, max(1, s.nb // args.verify))[:args.verify]:
+            if s.src.download(s.lens[b], offset=s.offs[b]).tobytes() != orc.gen_block(SEED, s.base + b, s.lens[b]).tobytes():
+                raise SystemExit("bench: opened block %d of GPU %d differs from the oracle" % (b, s.s))
+            samples += 1
+    # negative controls on GPU 0's block 0 (output to scratch)
+    key, nonce = E.gen_key(SEED, sh.base)
+    tag = bytes(A[sh.off].tag)
+    base = {"key": key, "nonce": nonce, "src": sh.dst.ptr + sh.offs[0], "dst": scratch.ptr, "len": sh.lens[0]}
+    one, _ = E.Engine.make_blocks([dict(base, tag=bytes([tag[0] ^ 1]) + tag[1:], crc=sh.crc.ptr)])
+    sh.eng.open_batch(algo, one, 1, E.CRC_VERIFY, E.MEM_DEVICE)
+    zeroed = not scratch.download(sh.lens[0]).any()
+    one2, _ = E.Engine.make_blocks([dict(base, tag=tag, crc=scratch.ptr + max(sh.lens[0], 16))])
+    sh.eng.open_batch(algo, one2, 1, E.CRC_VERIFY, E.MEM_DEVICE)
+    if one[0].status != E.ETAG or not zeroed or one2[0].status != E.ECRC or one2[0].crc_bad_seg != seg:
+        raise SystemExit("bench: negative controls failed (%d %s %d %d)" % (one[0].status, zeroed, one2[0].status,
+                                                                           one2[0].crc_bad_seg))
+    scratch.free()
+    out["plaintext_samples"] = samples
+    out["what"] = ("setup (the sealed image): tags and CRC arrays of all %d blocks equal to the oracle's; timed %s: "
+                   "all %d blocks tag- and CRC-verified (status OK%s), %d plaintexts equal to the oracle's, a flipped "
+                   "tag fails (ETAG, output zeroed) and a corrupted stored CRC fails at segment %d (ECRC)" % (
+                       n, "Decrypt" if mode == "decrypt" else "Open", n,
+                       ", every key unwrapped to the data key" if mode == "decrypt" else "", samples, seg))
+    return out
 
 
 def full_check(args, E, blks, got, lens, base):
@@ -521,108 +802,191 @@ def pmc_traffic(args, plain_per_launch):
     return traffic, src, binding
 
 
-def pcie_probe(eng, nbytes=1 << 30):
-    """jfsx_pcie_probe: GB/s between engine-pinned host memory and HBM on the
-    ring's own H2D and D2H streams, each direction alone and both at once
-    (8 chunks per direction issued alternately, as the ring issues them)."""
-    return eng.pcie_probe(nbytes)
+def parse_cpulist(text):
+    cpus = set()
+    for part in text.strip().split(","):
+        if "-" in part:
+            a, b = part.split("-")
+            cpus |= set(range(int(a), int(b) + 1))
+        elif part:
+            cpus.add(int(part))
+    return cpus
 
 
-def host_ingest(args, world, rank, local, dist, eng):
+def numa_pin(node):
+    """Restrict this process to those of its CPUs that sit on NUMA node
+    `node` (the GPU's socket); returns the CPUs it now runs on, or 0 when the
+    node's CPUs are unknown or none of them is allowed (affinity unchanged)."""
+    try:
+        cpus = parse_cpulist(open("/sys/devices/system/node/node%d/cpulist" % node).read())
+    except (OSError, ValueError):
+        return 0
+    inter = os.sched_getaffinity(0) & cpus
+    if not inter:
+        return 0
+    os.sched_setaffinity(0, inter)
+    return len(inter)
+
+
+PCIE_GEN5_X16_GBS = 64.0  # per direction, 32 GT/s x 16 lanes (before 128b/130b and TLP overhead)
+
+
+def host_ingest(args, world, rank, local, dist):
     """BASELINE configs[2]: blocks in pinned host memory, sealed through the
-    engine's H2D | transform | D2H ring (JFSX_MEM_HOST); value = plaintext
-    bytes / s including both PCIe transfers."""
+    engine's H2D | transform | D2H pipeline (JFSX_MEM_HOST); value = plaintext
+    bytes / s including both PCIe transfers.  Each GPU's pinned pool is capped
+    (--host-pool-gib in, the same out) and bound to the GPU's NUMA node; a step
+    loops over the pool to make up the GPU's blocks (weak: --blocks per GPU;
+    strong: its share of --total-gib)."""
     import ctypes
     import numpy as np
     from juicefs_amd import engine as E
-    nb, L = args.blocks, args.block_bytes
-    nseg = -(-L // E.SEG)
+    from juicefs_amd import shard as S
+    if args.mode != "seal":
+        raise SystemExit("bench: host ingest measures the seal path (configs[2])")
+    m, engs = open_engines(args, local)
+    nshard = len(engs) if m else world
+    L = args.block_bytes
     algo = E.AES256GCM if args.algo == "aes256gcm" else E.CHACHA20P1305
-    pcie_before = pcie_probe(eng)
-    hin = eng.alloc_pinned(nb * L)
-    hout = eng.alloc_pinned(nb * L)
-    hcrc = eng.alloc_pinned(nb * 4 * nseg)
-    tmp = eng.alloc(L)
-    base = rank * nb
-    for b in range(nb):  # synthetic input: generated on device, copied once into pinned memory
-        eng.gen_synthetic(tmp, L, SEED, base + b)
-        eng.sync()
-        eng.L.jfsx_memcpy_d2h(eng.ctx, hin + b * L, tmp.ptr, L)
-    tmp.free()
-    specs = []
-    for b in range(nb):
-        key, nonce = E.gen_key(SEED, base + b)
-        specs.append({"key": key, "nonce": nonce, "src": hin + b * L, "dst": hout + b * L, "len": L,
-                      "crc": hcrc + 4 * nseg * b})
-    blks, n = eng.make_blocks(specs)
+    shards, specs = [], []
+    for k, eng in enumerate(engs):
+        sh = Shard()
+        sh.eng, sh.s = eng, (k if m else rank)
+        sh.base, sh.count, sh.nb, sh.loops = shard_plan(args, nshard, sh.s)
+        sh.nseg = -(-L // E.SEG)
+        sh.lens = [L] * sh.nb
+        sh.node = eng.numa_node()
+        # one process per GPU: run on the GPU's socket (the pool's pages are
+        # bound to its node either way, by memory policy, not by first touch)
+        sh.cpus = numa_pin(sh.node) if (not m and sh.node >= 0) else 0
+        sh.pcie_before = eng.pcie_probe()
+        sh.hin = eng.alloc_pinned_node(sh.nb * L, sh.node)
+        sh.hout = eng.alloc_pinned_node(sh.nb * L, sh.node)
+        sh.hcrc = eng.alloc_pinned_node(sh.nb * 4 * sh.nseg, sh.node)
+        sh.pool_node = E.host_numa_node(sh.hin, sh.nb * L)
+        chunk = min(sh.nb, 256)
+        tmp = eng.alloc(chunk * L)
+        for b0 in range(0, sh.nb, chunk):  # synthetic input: generated on the device, copied once into the pool
+            c = min(chunk, sh.nb - b0)
+            eng.gen_synthetic_batch(tmp, L, [L] * c, SEED, sh.base + b0)
+            eng.L.jfsx_memcpy_d2h(eng.ctx, sh.hin + b0 * L, tmp.ptr, c * L)
+        tmp.free()
+        sh.off = len(specs)
+        for b in range(sh.nb):
+            key, nonce = E.gen_key(SEED, sh.base + b)
+            specs.append({"key": key, "nonce": nonce, "src": sh.hin + b * L, "dst": sh.hout + b * L, "len": L,
+                          "crc": sh.hcrc + 4 * sh.nseg * b})
+        shards.append(sh)
+    A, _ = E.Engine.make_blocks(specs)
+    loops = loop_arrays(A, shards)
+    front = m if m else engs[0]
 
     def step():
-        eng.seal_batch(algo, blks, n, E.CRC_GEN, E.MEM_HOST)
+        for arr, n, _ in loops:
+            front.seal_batch(algo, arr, n, E.CRC_GEN, E.MEM_HOST)
     for _ in range(args.warmup):
         step()
-    eng.kernel_time(reset=True)
-    eng.set_timing(True)
+    for e in engs:
+        e.sync()
+        e.kernel_time(reset=True)
+        e.set_timing(True)
     barrier(dist)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    eng.sync()
+    for e in engs:
+        e.sync()
     barrier(dist)
     el = max_over_ranks(dist, time.perf_counter() - t0, local)
-    eng.set_timing(False)
-    k_ms, k_n = eng.kernel_time(reset=True)
-    # the link probed again right after the ring (the probe before it has read
-    # below what the ring itself moved on some boxes); the faster of the two
-    pcie_after = pcie_probe(eng)
-    pcie = {k: max(pcie_before.get(k, 0.0), pcie_after.get(k, 0.0)) for k in set(pcie_before) | set(pcie_after)}
-    pcie_runs = {"before_ring": pcie_before, "after_ring": pcie_after}
-    verified = 0
-    if args.verify:
-        from oracle import oracle as orc
-        for b in range(0, nb, max(1, nb // args.verify))[:args.verify]:
-            p = orc.gen_block(SEED, base + b, L)
-            key, nonce = orc.gen_key(SEED, base + b)
-            c, tag = orc.seal(orc.AES256GCM if algo == E.AES256GCM else orc.CHACHA20P1305, key, nonce, p, fast=True)
-            got = np.ctypeslib.as_array((ctypes.c_uint8 * L).from_address(hout + b * L)).tobytes()
-            if bytes(blks[b].tag) != tag or got != c:
-                raise SystemExit("bench: block %d differs from the oracle" % b)
-            verified += 1
+    for e in engs:
+        e.set_timing(False)
+    ktimes = [e.kernel_time(reset=True) for e in engs]
+    # the link probed again right after the run (the probe before it has read
+    # below what the pipeline itself moved on some boxes); the faster of the two
+    for sh in shards:
+        after = sh.eng.pcie_probe()
+        sh.pcie = {k: max(sh.pcie_before.get(k, 0.0), after.get(k, 0.0)) for k in set(sh.pcie_before) | set(after)}
+        sh.pcie_runs = {"before_run": sh.pcie_before, "after_run": after}
+        # the pipeline moves equal bytes both ways at once: its bound is the
+        # slower direction of the simultaneous (duplex) probe
+        sh.peak = min(sh.pcie.get("duplex_h2d", sh.pcie["h2d"]), sh.pcie.get("duplex_d2h", sh.pcie["d2h"]))
     full = None
     if args.verify:
-        crcs = np.ctypeslib.as_array((ctypes.c_uint8 * (nb * 4 * nseg)).from_address(hcrc)).reshape(nb, 4 * nseg)
-        full = full_check(args, E, blks, crcs.copy(), [L] * nb, base)
-        verified = nb
-    value = world * nb * L * args.steps / el / 1e9
+        from oracle import oracle as orc
+        full = {"blocks": 0, "oracle_s": 0.0}
+        samples = 0
+        for sh in shards:
+            for b in range(0, sh.nb, max(1, sh.nb // args.verify))[:args.verify]:
+                p = orc.gen_block(SEED, sh.base + b, L)
+                key, nonce = orc.gen_key(SEED, sh.base + b)
+                c, tag = orc.seal(orc.AES256GCM if algo == E.AES256GCM else orc.CHACHA20P1305, key, nonce, p,
+                                  fast=True)
+                got = np.ctypeslib.as_array((ctypes.c_uint8 * L).from_address(sh.hout + b * L)).tobytes()
+                if bytes(A[sh.off + b].tag) != tag or got != c:
+                    raise SystemExit("bench: block %d of GPU %d differs from the oracle" % (b, sh.s))
+                samples += 1
+            crcs = np.ctypeslib.as_array((ctypes.c_uint8 * (sh.nb * 4 * sh.nseg)).from_address(sh.hcrc))
+            f = full_check(args, E, [A[sh.off + i] for i in range(sh.nb)], crcs.reshape(sh.nb, 4 * sh.nseg).copy(),
+                           sh.lens, sh.base)
+            full["blocks"] += f["blocks"]
+            full["oracle_s"] = round(full["oracle_s"] + f["oracle_s"], 2)
+            full["oracle_threads"] = f["oracle_threads"]
+            full.setdefault("tags_sha256", []).append(f["tags_sha256"])
+            full.setdefault("crc_arrays_sha256", []).append(f["crc_arrays_sha256"])
+        full["ciphertext_samples"] = samples
+        full["what"] = ("timed Seal: tags and CRC arrays of all %d pool blocks, and %d ciphertexts, equal to the "
+                        "oracle's" % (full["blocks"], samples))
+    step_plain = sum(sum(sh.loops) * L for sh in shards)
+    value = S.sum_over_ranks(dist, step_plain, local) * args.steps / el / 1e9
+    ngpu = len(engs) if m else world
+    peak = S.sum_over_ranks(dist, sum(sh.peak for sh in shards), local)
     cpu = cpu_baseline(args, "seal") if rank == 0 and world == 1 and not args.no_cpu else None
-    plain_launch = int(nb * L * args.steps / max(k_n, 1))
+    launches = sum(n for _, n in ktimes)
+    plain_launch = int(step_plain * args.steps / max(launches, 1))
     traffic, traffic_src, binding = pmc_traffic(args, plain_launch)
+    pinned = sum(2 * sh.nb * L + sh.nb * 4 * sh.nseg for sh in shards)
     if rank == 0:
-        # the ring moves equal bytes both ways at once: its bound is the
-        # slower direction of the simultaneous (duplex) probe
-        peak = min(pcie.get("duplex_h2d", pcie["h2d"]), pcie.get("duplex_d2h", pcie["d2h"]))
+        sh0 = shards[0]
         print(json.dumps({
             "metric": "sealed+checksummed GB/s, 4 MiB blocks (host ingest)", "value": round(value, 2), "unit": "GB/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "n_gpus": ngpu, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": scaling(args),
             "vs_baseline": None, "dtype": "u8", "data": "synthetic (SplitMix64), pinned host memory",
-            "config": {"workload": "host-ingest: %s GiB pinned per step x %d steps per GPU, %s seal + CRC32C full, "
-                                   "3-slot H2D|transform|D2H ring" % (nb * L / 2**30, args.steps, args.algo),
-                       "blocks_per_gpu": nb, "block_bytes": L, "algo": args.algo, "mem": "host"},
-            "roofline": {"bound": "pcie", "achieved": round(value, 2), "peak": peak, "unit": "GB/s",
+            "config": {"workload": "host-ingest: %s GiB per GPU per step (%d pass(es) over a %s GiB pinned pool), "
+                                   "%s seal + CRC32C full, 8-slot H2D|transform|D2H pipeline" % (
+                                       round(sh0.count * L / 2**30, 3), len(sh0.loops), round(sh0.nb * L / 2**30, 3),
+                                       args.algo),
+                       "blocks_per_gpu": sh0.count, "pool_blocks_per_gpu": sh0.nb, "block_bytes": L,
+                       "algo": args.algo, "mem": "host", "total_gib": args.total_gib or None,
+                       "engine": "jfsx_mctx (one process, %d GPUs)" % ngpu if m else "one process per GPU",
+                       "pinned_bytes_per_process": pinned,
+                       "numa": [{"gpu_node": sh.node, "pool_node": sh.pool_node, "cpus_on_node": sh.cpus}
+                                for sh in shards],
+                       "parallelism": "block-sharded x%d, no collective" % ngpu},
+            "roofline": {"bound": "pcie", "achieved": round(value, 2), "peak": round(peak, 2), "unit": "GB/s",
                          "frac": round(value / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
-                         "traffic_note": "HBM bytes per launch of gcm_main_k (one launch per ring slot)",
-                         "peak_basis": "min over directions of simultaneous H2D + D2H copies of 1 GiB on the "
-                                       "ring's streams (jfsx_pcie_probe, the better of a probe before and one after "
-                                       "the ring); one-way rates in pcie_measured",
-                         "frac_of_one_way_d2h": round(value / pcie["d2h"], 4),
-                         "pcie_measured": pcie, "pcie_probes": pcie_runs,
-                         "kernel_avg_ms": round(k_ms / max(k_n, 1), 3),
-                         "kernel_launches": k_n, "plain_bytes_per_launch": plain_launch, "binding": binding},
-            "cpu_baseline": cpu, "verified_blocks": verified, "full_check": full}), flush=True)
-    eng.free_pinned(hin)
-    eng.free_pinned(hout)
-    eng.free_pinned(hcrc)
-    eng.close()
+                         "traffic_note": "HBM bytes per launch of gcm_main_k (one launch per pipeline group)",
+                         "peak_basis": "sum over GPUs of min over directions of simultaneous H2D + D2H copies of "
+                                       "1 GiB on the pipeline's streams (jfsx_pcie_probe, the better of a probe "
+                                       "before and one after the run); one-way rates in pcie_measured",
+                         "link_peak": PCIE_GEN5_X16_GBS * ngpu,
+                         "frac_of_link": round(value / (PCIE_GEN5_X16_GBS * ngpu), 4),
+                         "link_basis": "PCIe Gen5 x16 per direction, 64 GB/s per GPU (32 GT/s x 16 lanes); each "
+                                       "direction carries the plaintext rate",
+                         "frac_of_one_way_d2h": round(value / S.sum_over_ranks(
+                             dist, sum(sh.pcie["d2h"] for sh in shards), local), 4),
+                         "pcie_measured": [sh.pcie for sh in shards] if m else sh0.pcie,
+                         "pcie_probes": [sh.pcie_runs for sh in shards] if m else sh0.pcie_runs,
+                         "kernel_avg_ms": round(sum(ms for ms, _ in ktimes) / max(launches, 1), 3),
+                         "kernel_launches": launches, "plain_bytes_per_launch": plain_launch, "binding": binding},
+            "cpu_baseline": cpu, "verified_blocks": full["blocks"] if full else 0, "full_check": full}), flush=True)
+    for sh in shards:
+        for h in (sh.hin, sh.hout, sh.hcrc):
+            sh.eng.free_pinned(h)
+    if m:
+        m.close()
+    else:
+        engs[0].close()
     if dist is not None:
         dist.destroy_process_group()
 
@@ -683,7 +1047,7 @@ def agg_bench(args, world, rank, local, dist, eng):
     d_steps = max(1, args.steps // 5)
     run(direct, 1)
     d_el = run(direct, d_steps)
-    with E.Aggregator(eng, window_us=args.agg_window_us) as agg:
+    with E.Aggregator(eng, window_us=args.agg_window_us, max_bytes=args.agg_max_mb << 20) as agg:
         def through(b):
             agg.seal(algo, blks[b], E.CRC_GEN, E.MEM_HOST)
         run(through, args.warmup)
@@ -702,8 +1066,16 @@ def agg_bench(args, world, rank, local, dist, eng):
             if bytes(blks[b].tag) != tag or got != c:
                 raise SystemExit("bench: block %d differs from the oracle" % b)
             verified += 1
+    full = None
+    if args.verify:
+        crcs = np.ctypeslib.as_array((ctypes.c_uint8 * (nb * 4 * nseg)).from_address(hcrc)).reshape(nb, 4 * nseg)
+        full = full_check(args, E, blks, crcs.copy(), [L] * nb, base)
+        full["what"] = "per-object Seal calls through the aggregator: " + full["what"]
+        verified = nb
     value = world * nb * L * args.steps / el / 1e9
     cpu = cpu_baseline(args, "seal") if rank == 0 and world == 1 and not args.no_cpu else None
+    pcie = eng.pcie_probe()
+    duplex = min(pcie["duplex_h2d"], pcie["duplex_d2h"])
     if rank == 0:
         print(json.dumps({
             "metric": "per-object sealed+checksummed GB/s, %d threads, 4 MiB host blocks (aggregator)" % T,
@@ -712,11 +1084,18 @@ def agg_bench(args, world, rank, local, dist, eng):
             "vs_baseline": None, "dtype": "u8", "data": "synthetic (SplitMix64), pinned host memory",
             "config": {"workload": "%d one-block Seal calls per step from %d threads, %s + CRC32C full, JFSX_MEM_HOST"
                                    % (nb, T, args.algo), "blocks_per_gpu": nb, "block_bytes": L, "algo": args.algo,
-                       "mode": "agg", "window_us": args.agg_window_us},
+                       "mode": "agg", "window_us": args.agg_window_us, "max_batch_bytes": args.agg_max_mb << 20,
+                       "dispatchers_per_gpu": int(os.environ.get("JFSX_AGG_DISPATCHERS", "4"))},
             "aggregator": {"calls": c1 - c0, "batches": b1 - b0,
                            "mean_batch_blocks": round((k1 - k0) / max(b1 - b0, 1), 2)},
             "direct_one_block_calls_GBs": round(nb * L * d_steps / d_el / 1e9, 2),
-            "roofline": None, "cpu_baseline": cpu, "verified_blocks": verified}), flush=True)
+            "direct_note": "the same calls as one-block jfsx_seal_batch calls from the same threads, no aggregator "
+                           "(host batches share the context's pipeline)",
+            "roofline": {"bound": "pcie", "achieved": round(value, 2), "peak": duplex, "unit": "GB/s",
+                         "frac": round(value / duplex, 4), "peak_basis": "min over directions of simultaneous H2D + "
+                         "D2H copies (jfsx_pcie_probe, after the run)", "pcie_measured": pcie,
+                         "frac_of_link": round(value / PCIE_GEN5_X16_GBS, 4)},
+            "cpu_baseline": cpu, "verified_blocks": verified, "full_check": full}), flush=True)
     for h in (hin, hout, hcrc):
         eng.free_pinned(h)
     eng.close()

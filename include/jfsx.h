@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define JFSX_ABI_VERSION 7
+#define JFSX_ABI_VERSION 8
 
 /* algorithms (encrypt.go:142-145) */
 #define JFSX_AES256GCM 0     /* "aes256gcm-rsa" (also the "" default)   */
@@ -181,17 +181,43 @@ typedef struct jfsx_metrics {
 int jfsx_ctx_metrics(jfsx_ctx *ctx, jfsx_metrics *out, int reset);
 
 /* memory helpers (engine-owned pinned staging, device buffers); pinned memory
- * is portable: any context of the process (any GPU) may stream from it */
+ * is portable: any context of the process (any GPU) may stream from it.
+ * Device buffers from jfsx_alloc_device are registered by address, so a
+ * multi-device context can route a device-memory block to the GPU that owns
+ * it (jfsx_mctx_seal_batch with JFSX_MEM_DEVICE). */
 int jfsx_alloc_pinned(jfsx_ctx *ctx, size_t bytes, void **p);
 int jfsx_free_pinned(jfsx_ctx *ctx, void *p);
 int jfsx_alloc_device(jfsx_ctx *ctx, size_t bytes, void **p);
 int jfsx_free_device(jfsx_ctx *ctx, void *p);
+
+/* NUMA placement of pinned staging, so that at N GPUs on a multi-socket node
+ * every GPU streams from memory on its own socket (the reference's uploaders
+ * fill Go-heap pages wherever the scheduler ran them, pkg/chunk/page.go:33-60;
+ * the shim copies them into this staging).
+ *   jfsx_device_numa_node  host NUMA node closest to `device` (-1 unknown)
+ *   jfsx_alloc_pinned_node pinned portable memory whose pages are bound to
+ *                          `node` while they are allocated (-1: the node of the
+ *                          context's device); where the node cannot be bound
+ *                          (a cpuset without it) the default placement is used
+ *   jfsx_host_numa_node    node of the pages of [p, p+bytes), sampled every
+ *                          64 MiB: -1 unknown, -2 pages on more than one node
+ * Free with jfsx_free_pinned. */
+int jfsx_device_numa_node(int device, int *node);
+int jfsx_alloc_pinned_node(jfsx_ctx *ctx, size_t bytes, int node, void **p);
+int jfsx_host_numa_node(const void *p, size_t bytes, int *node);
 int jfsx_memcpy_h2d(jfsx_ctx *ctx, void *dst, const void *src, size_t bytes);
 int jfsx_memcpy_d2h(jfsx_ctx *ctx, void *dst, const void *src, size_t bytes);
 
 /* Batched AEAD over blocks, fused with CRC32C segment checksums of the
  * plaintext.  mem = JFSX_MEM_DEVICE or JFSX_MEM_HOST.  Synchronous: returns
- * when tags, CRCs and statuses are written back into blks. */
+ * when tags, CRCs and statuses are written back into blks.
+ * JFSX_MEM_HOST batches stream through the context's pipeline of 8 staging
+ * slots (H2D | transform | D2H on three streams).  The pipeline is shared by
+ * every thread calling on the context and never drains between calls: a call
+ * enqueues its groups and then waits for its own groups only, so concurrent
+ * callers (the aggregator's dispatchers, per-object shims) keep both copy
+ * directions busy back to back.  Device batches hold the context for the
+ * whole call. */
 int jfsx_seal_batch(jfsx_ctx *ctx, int algo, int n, jfsx_blk *blks, int crc_mode, int mem);
 int jfsx_open_batch(jfsx_ctx *ctx, int algo, int n, jfsx_blk *blks, int crc_mode, int mem);
 
@@ -232,16 +258,38 @@ int jfsx_agg_open(jfsx_agg *agg, int algo, jfsx_blk *blk, int crc_mode, int mem)
 int jfsx_agg_crc32c(jfsx_agg *agg, jfsx_range *range, int mode, int mem);
 /* requests taken, batches issued, requests those batches carried */
 int jfsx_agg_stats(jfsx_agg *agg, uint64_t *calls, uint64_t *batches, uint64_t *blocks);
+/* Dispatch: each context gets several dispatcher threads (4; the environment
+ * variable JFSX_AGG_DISPATCHERS overrides, 1..32), so several batches of one
+ * device are in flight at once (host batches pipeline, see jfsx_seal_batch).
+ * A group waits for its window only while the engine is idle; while another
+ * of the aggregator's batches is running, a free dispatcher takes what is
+ * queued at once (the time spent queued behind the running batch is the
+ * batching).  For per-object callers in host memory keep max_bytes near
+ * 16 MiB, so that a 20-caller closed loop (max-uploads) is cut into several
+ * batches in flight instead of one batch that all callers wait for. */
+
+/* dataEncryptor.Encrypt / Decrypt (encrypt.go:164-216) through the
+ * aggregator: the same object format and results as jfsx_data_encrypt /
+ * jfsx_data_decrypt, with the Seal / Open issued as one aggregated request, so
+ * the shim's per-object Encrypt from max-uploads goroutines batches. */
+int jfsx_agg_data_encrypt(jfsx_agg *agg, int algo, const uint8_t key[32], const uint8_t nonce[12],
+                          const uint8_t *wrapped, int wlen, const void *plaintext, uint64_t len, void *out,
+                          uint64_t out_cap, uint64_t *out_len, uint32_t *obj_crc);
+int jfsx_agg_data_decrypt(jfsx_agg *agg, int algo, const uint8_t key[32], const void *obj, uint64_t olen, void *out,
+                          uint64_t out_cap, uint64_t *out_len, const uint32_t *expect_crc, uint32_t *got_crc);
 
 /* Multi-device context (SURVEY §8b jfsx_open_ctx(dev_mask), §8e): one
  * jfsx_ctx per selected GPU (bit d of dev_mask = device d; 0 = every visible
- * device).  Blocks are independent (own key, nonce, tag, CRCs), so a host-
- * memory batch is cut into one contiguous run of blocks per device, balanced
- * by bytes, and the runs execute concurrently, one host thread per device; no
- * device-to-device traffic.  Results land in blks exactly as with a single
- * context.  Batches on a multi-device context take JFSX_MEM_HOST only (device
- * pointers belong to one GPU: use that GPU's jfsx_mctx_ctx).  A batch-level
- * error of any device is returned (the first one, in device order). */
+ * device).  Blocks are independent (own key, nonce, tag, CRCs), so the parts
+ * of a batch run concurrently, one persistent worker thread per device; no
+ * device-to-device traffic.  A JFSX_MEM_HOST batch is cut into one contiguous
+ * run of blocks per device, balanced by bytes.  A JFSX_MEM_DEVICE batch is
+ * routed by ownership: every block goes to the GPU whose memory holds its
+ * src, dst and crc (buffers from jfsx_alloc_device on a member context, or any
+ * device allocation); a block whose buffers span GPUs, or live on a GPU
+ * outside the context, fails the batch with JFSX_EINVAL before anything runs.
+ * Results land in blks exactly as with a single context.  A batch-level error
+ * of any device is returned (the first one, in device order). */
 typedef struct jfsx_mctx jfsx_mctx;
 int jfsx_mctx_open(uint64_t dev_mask, uint32_t flags, jfsx_mctx **out);
 int jfsx_mctx_close(jfsx_mctx *m);

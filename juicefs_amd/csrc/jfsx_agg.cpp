@@ -21,6 +21,9 @@
 //     time window measured from the oldest waiting request.
 #include <chrono>
 #include <condition_variable>
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -194,7 +197,8 @@ using jfsx::kZstdd;
 using jfsx::kZstdc;
 
 struct jfsx_agg {
-    std::vector<jfsx_ctx *> cs;  // one dispatcher thread per context (device)
+    std::vector<jfsx_ctx *> cs;  // context of each dispatcher thread
+    std::vector<int> dev;        // device slot (jfsx_agg_dev_batches) of each dispatcher
     int max_blocks;
     uint64_t max_bytes;
     std::chrono::microseconds window;
@@ -202,6 +206,8 @@ struct jfsx_agg {
     std::condition_variable cv_work, cv_done;
     std::deque<Req *> q;
     bool stop = false;
+    int busy = 0;             // dispatchers running a pipelined batch
+    std::vector<int> serial;  // per device: dispatchers running a non-pipelined batch
     uint64_t calls = 0, batches = 0, blocks = 0;
     std::vector<uint64_t> dev_batches;
     std::vector<std::thread> ths;
@@ -253,8 +259,18 @@ struct jfsx_agg {
         }
     }
 
+    // Host-memory Seal / Open pipeline through the context (jfsx_seal_batch):
+    // several such batches of one device run at once.  Everything else holds
+    // its context for the whole call, so a device runs one of those at a time.
+    static bool piped(const Req &r) { return (r.op == kSeal || r.op == kOpen) && r.mem == JFSX_MEM_HOST; }
+
     // Dispatcher k: take the group of the oldest request once it is full (block
-    // or byte cap) or its window has closed, run it on context k.  Several
+    // or byte cap) or its window has closed -- or, for a pipelined group, as
+    // soon as another pipelined batch is running (the engine is busy: the time
+    // the group spent queued behind that batch was its batching, and holding it
+    // longer would only idle the pipeline) -- then run it on context cs[k].  A
+    // non-pipelined group waits while its device runs another one, so requests
+    // arriving meanwhile join one batch instead of several small ones.  The
     // dispatchers share the queue: after every wait the head is re-read, since
     // another dispatcher may have taken the group in the meantime.
     void run(int k) {
@@ -263,12 +279,17 @@ struct jfsx_agg {
             cv_work.wait(lk, [&] { return stop || !q.empty(); });
             if (q.empty()) return;  // stop, and nothing left to run
             const Req *head = q.front();
+            const bool pipe = piped(*head);
+            if (!pipe && !stop && serial[dev[k]] > 0) {
+                cv_work.wait(lk);
+                continue;
+            }
             int cnt = 0;
             uint64_t bytes = 0;
             for (Req *r : q)
                 if (r->same(*head)) cnt++, bytes += r->bytes;
             const Clock::time_point deadline = head->t0 + window;
-            if (!(stop || cnt >= max_blocks || bytes >= max_bytes || Clock::now() >= deadline)) {
+            if (!(stop || (pipe && busy > 0) || cnt >= max_blocks || bytes >= max_bytes || Clock::now() >= deadline)) {
                 cv_work.wait_until(lk, deadline);
                 continue;
             }
@@ -284,15 +305,19 @@ struct jfsx_agg {
                     ++it;
                 }
             }
-            if (!q.empty()) cv_work.notify_all();  // the next group may be ready for an idle dispatcher
+            int &held = pipe ? busy : serial[dev[k]];
+            held++;
+            if (!q.empty()) cv_work.notify_all();  // the rest may go to an idle dispatcher now
             lk.unlock();
             execute(cs[k], b);
             lk.lock();
+            held--;
             batches++;
-            dev_batches[k]++;
+            dev_batches[dev[k]]++;
             blocks += b.size();
             for (Req *r : b) r->done = true;
             cv_done.notify_all();
+            if (!q.empty()) cv_work.notify_all();
         }
     }
 
@@ -309,14 +334,32 @@ struct jfsx_agg {
 };
 
 namespace {
-int agg_start(std::vector<jfsx_ctx *> cs, int max_blocks, uint64_t max_bytes, uint32_t window_us, jfsx_agg **out) {
+// dispatcher threads per context (JFSX_AGG_DISPATCHERS overrides)
+int dispatchers_per_ctx() {
+    static const int d = [] {
+        const char *e = getenv("JFSX_AGG_DISPATCHERS");
+        const int v = e ? atoi(e) : 0;
+        return v >= 1 && v <= 32 ? v : 4;
+    }();
+    return d;
+}
+
+int agg_start(const std::vector<jfsx_ctx *> &cs, int max_blocks, uint64_t max_bytes, uint32_t window_us,
+              jfsx_agg **out) {
     jfsx_agg *a = new (std::nothrow) jfsx_agg;
     if (!a) return JFSX_ENOMEM;
-    a->cs = std::move(cs);
+    const int per = dispatchers_per_ctx();
+    // dispatcher j serves device j % ndev, so the first dispatchers to wake
+    // are spread over the devices
+    for (int j = 0; j < per * (int)cs.size(); j++) {
+        a->cs.push_back(cs[j % cs.size()]);
+        a->dev.push_back(j % (int)cs.size());
+    }
     a->max_blocks = max_blocks ? max_blocks : 256;
     a->max_bytes = max_bytes ? max_bytes : (uint64_t)1 << 30;
     a->window = std::chrono::microseconds(window_us);
-    a->dev_batches.assign(a->cs.size(), 0);
+    a->dev_batches.assign(cs.size(), 0);
+    a->serial.assign(cs.size(), 0);
     for (size_t k = 0; k < a->cs.size(); k++) a->ths.emplace_back([a, k] { a->run((int)k); });
     *out = a;
     return 0;
@@ -325,7 +368,7 @@ int agg_start(std::vector<jfsx_ctx *> cs, int max_blocks, uint64_t max_bytes, ui
 // dispatcher may take a group, so only host memory is accepted there (as the
 // jfsx_mctx_*_batch entry points do)
 bool agg_mem_ok(const jfsx_agg *a, int mem) {
-    return valid_mem(mem) && !(mem == JFSX_MEM_DEVICE && a->cs.size() > 1);
+    return valid_mem(mem) && !(mem == JFSX_MEM_DEVICE && a->dev_batches.size() > 1);
 }
 }  // namespace
 
@@ -413,8 +456,45 @@ int jfsx_agg_stats(jfsx_agg *a, uint64_t *calls, uint64_t *batches, uint64_t *bl
 // multi-device context (SURVEY §8b jfsx_open_ctx(dev_mask), §8e): one jfsx_ctx
 // per GPU, built on the public single-device entry points only
 
+namespace jfsx {
+// device owning a device pointer, with its allocation's bounds; -1 for host
+// memory (jfsx_api.cpp; the host harness stubs it)
+int device_of(const void *p, uintptr_t *lo, uintptr_t *hi);
+}  // namespace jfsx
+
+namespace {
+// a persistent worker thread running one device's part of each batch
+struct MWorker {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::function<void()>> q;
+    bool stop = false;
+    std::thread th;
+
+    void run() {
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            cv.wait(lk, [&] { return stop || !q.empty(); });
+            if (q.empty()) return;
+            std::function<void()> f = std::move(q.front());
+            q.pop_front();
+            lk.unlock();
+            f();
+            lk.lock();
+        }
+    }
+    void post(std::function<void()> f) {
+        std::lock_guard<std::mutex> g(mu);
+        q.push_back(std::move(f));
+        cv.notify_one();
+    }
+};
+}  // namespace
+
 struct jfsx_mctx {
     std::vector<jfsx_ctx *> cs;
+    std::vector<int> devs;                      // device ordinal of cs[k]
+    std::vector<std::unique_ptr<MWorker>> ws;   // ws[k] runs device k's parts (k >= 1)
 };
 
 namespace {
@@ -439,29 +519,111 @@ std::vector<int> split_runs(int n, int nd, const std::function<uint64_t(int)> &l
     return cut;
 }
 
-// run f(k, b0, b1) for every non-empty run, device 0's on the calling thread
-int fan_out(const std::vector<int> &cut, const std::function<int(int, int, int)> &f) {
-    const int nd = (int)cut.size() - 1;
+// run f(k) for every device k with work (has[k]): device parts 1.. on their
+// persistent workers, the first on the calling thread; the first error in
+// device order is returned
+int fan_out(jfsx_mctx *m, const std::vector<char> &has, const std::function<int(int)> &f) {
+    const int nd = (int)m->cs.size();
     std::vector<int> rc(nd, 0);
-    std::vector<std::thread> th;
-    for (int k = 1; k < nd; k++)
-        if (cut[k + 1] > cut[k]) th.emplace_back([&, k] { rc[k] = f(k, cut[k], cut[k + 1]); });
-    if (cut[1] > cut[0]) rc[0] = f(0, cut[0], cut[1]);
-    for (std::thread &t : th) t.join();
+    std::mutex mu;
+    std::condition_variable cv;
+    int left = 0, first = -1;
+    for (int k = 0; k < nd; k++)
+        if (has[k]) {
+            if (first < 0) first = k;
+            else left++;
+        }
+    if (first < 0) return 0;
+    for (int k = first + 1; k < nd; k++) {
+        if (!has[k]) continue;
+        m->ws[k]->post([&, k] {
+            const int r = f(k);
+            std::lock_guard<std::mutex> g(mu);
+            rc[k] = r;
+            if (--left == 0) cv.notify_all();
+        });
+    }
+    rc[first] = f(first);
+    {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return left == 0; });
+    }
     for (int k = 0; k < nd; k++)
         if (rc[k]) return rc[k];
     return 0;
 }
 
-int mctx_aead(jfsx_mctx *m, bool open, int algo, int n, jfsx_blk *blks, int crc_mode, int mem) {
-    if (!m || n < 0 || (n && !blks)) return JFSX_EINVAL;
-    if (mem != JFSX_MEM_HOST && !(mem == JFSX_MEM_DEVICE && m->cs.size() == 1)) return JFSX_EINVAL;
+// Per-device parts of a batch of T items.  Host memory: contiguous runs
+// balanced by bytes.  Device memory: each item goes to the device that owns
+// the pointers ptrs(item) lists (all on one member device, else JFSX_EINVAL).
+// A device whose items are one contiguous run of the caller's array runs it in
+// place; otherwise its items are gathered, run, and scattered back.
+template <class T>
+int mctx_run(jfsx_mctx *m, int n, T *items, int mem, const std::function<uint64_t(const T &)> &bytes,
+             const std::function<int(const T &, const void **)> &ptrs,
+             const std::function<int(jfsx_ctx *, int, T *)> &run) {
+    if (!m || n < 0 || (n && !items) || (mem != JFSX_MEM_HOST && mem != JFSX_MEM_DEVICE)) return JFSX_EINVAL;
     if (n == 0) return 0;
-    const std::vector<int> cut = split_runs(n, (int)m->cs.size(), [&](int i) { return blks[i].len; });
-    return fan_out(cut, [&](int k, int b0, int b1) {
-        return open ? jfsx_open_batch(m->cs[k], algo, b1 - b0, blks + b0, crc_mode, mem)
-                    : jfsx_seal_batch(m->cs[k], algo, b1 - b0, blks + b0, crc_mode, mem);
+    const int nd = (int)m->cs.size();
+    std::vector<char> has(nd, 0);
+    if (mem == JFSX_MEM_HOST || nd == 1) {
+        const std::vector<int> cut = nd == 1 ? std::vector<int>{0, n}
+                                             : split_runs(n, nd, [&](int i) { return bytes(items[i]); });
+        for (int k = 0; k < nd; k++) has[k] = cut[k + 1] > cut[k];
+        return fan_out(m, has, [&](int k) { return run(m->cs[k], cut[k + 1] - cut[k], items + cut[k]); });
+    }
+    // ownership routing
+    int maxdev = 0;
+    for (int d : m->devs) maxdev = std::max(maxdev, d);
+    std::vector<int> slot_of(maxdev + 1, -1);
+    for (int k = 0; k < nd; k++) slot_of[m->devs[k]] = k;
+    std::vector<int> owner(n);
+    uintptr_t lo = 1, hi = 0;
+    int cdev = -1;  // allocation of the last lookup
+    for (int i = 0; i < n; i++) {
+        const void *p[4];
+        const int np = ptrs(items[i], p);
+        int d = -2;
+        for (int j = 0; j < np; j++) {
+            const uintptr_t a = (uintptr_t)p[j];
+            if (!(a >= lo && a < hi)) cdev = jfsx::device_of(p[j], &lo, &hi);
+            if (cdev < 0 || cdev > maxdev || slot_of[cdev] < 0 || (d != -2 && d != cdev)) return JFSX_EINVAL;
+            d = cdev;
+        }
+        owner[i] = d == -2 ? 0 : slot_of[d];  // an item with no buffers runs anywhere
+        has[owner[i]] = 1;
+    }
+    std::vector<std::vector<int>> idx(nd);
+    for (int i = 0; i < n; i++) idx[owner[i]].push_back(i);
+    return fan_out(m, has, [&](int k) {
+        const std::vector<int> &ix = idx[k];
+        if (ix.back() - ix.front() + 1 == (int)ix.size()) return run(m->cs[k], (int)ix.size(), items + ix.front());
+        std::vector<T> tmp(ix.size());
+        for (size_t j = 0; j < ix.size(); j++) tmp[j] = items[ix[j]];
+        const int rc = run(m->cs[k], (int)ix.size(), tmp.data());
+        for (size_t j = 0; j < ix.size(); j++) items[ix[j]] = tmp[j];
+        return rc;
     });
+}
+
+int blk_ptrs(const jfsx_blk &b, int crc_mode, const void **p) {
+    int np = 0;
+    if (b.len) {
+        p[np++] = b.src;
+        p[np++] = b.dst;
+    }
+    if (crc_mode && b.crc) p[np++] = b.crc;
+    return np;
+}
+
+int mctx_aead(jfsx_mctx *m, bool open, int algo, int n, jfsx_blk *blks, int crc_mode, int mem) {
+    return mctx_run<jfsx_blk>(
+        m, n, blks, mem, [](const jfsx_blk &b) { return b.len; },
+        [&](const jfsx_blk &b, const void **p) { return blk_ptrs(b, crc_mode, p); },
+        [&](jfsx_ctx *c, int cnt, jfsx_blk *part) {
+            return open ? jfsx_open_batch(c, algo, cnt, part, crc_mode, mem)
+                        : jfsx_seal_batch(c, algo, cnt, part, crc_mode, mem);
+        });
 }
 
 }  // namespace
@@ -485,6 +647,14 @@ int jfsx_mctx_open(uint64_t dev_mask, uint32_t flags, jfsx_mctx **out) {
             return rc;
         }
         m->cs.push_back(c);
+        m->devs.push_back(d);
+    }
+    for (size_t k = 0; k < m->cs.size(); k++) {
+        m->ws.emplace_back(new MWorker);
+        if (k) {
+            MWorker *w = m->ws.back().get();
+            w->th = std::thread([w] { w->run(); });
+        }
     }
     *out = m;
     return 0;
@@ -492,6 +662,15 @@ int jfsx_mctx_open(uint64_t dev_mask, uint32_t flags, jfsx_mctx **out) {
 
 int jfsx_mctx_close(jfsx_mctx *m) {
     if (!m) return JFSX_EINVAL;
+    for (auto &w : m->ws) {
+        if (!w->th.joinable()) continue;
+        {
+            std::lock_guard<std::mutex> g(w->mu);
+            w->stop = true;
+            w->cv.notify_all();
+        }
+        w->th.join();
+    }
     for (jfsx_ctx *c : m->cs) jfsx_ctx_close(c);
     delete m;
     return 0;
@@ -512,38 +691,46 @@ int jfsx_mctx_open_batch(jfsx_mctx *m, int algo, int n, jfsx_blk *blks, int crc_
 }
 
 int jfsx_mctx_crc32c_segments(jfsx_mctx *m, int n, jfsx_range *ranges, int mode, int mem) {
-    if (!m || n < 0 || (n && !ranges)) return JFSX_EINVAL;
-    if (mem != JFSX_MEM_HOST && !(mem == JFSX_MEM_DEVICE && m->cs.size() == 1)) return JFSX_EINVAL;
-    if (n == 0) return 0;
-    const std::vector<int> cut = split_runs(n, (int)m->cs.size(), [&](int i) { return ranges[i].len; });
-    return fan_out(cut, [&](int k, int b0, int b1) {
-        return jfsx_crc32c_segments(m->cs[k], b1 - b0, ranges + b0, mode, mem);
-    });
+    return mctx_run<jfsx_range>(
+        m, n, ranges, mem, [](const jfsx_range &r) { return r.len; },
+        [](const jfsx_range &r, const void **p) {
+            int np = 0;
+            if (r.len) p[np++] = r.data;
+            if (r.crc) p[np++] = r.crc;
+            return np;
+        },
+        [&](jfsx_ctx *c, int cnt, jfsx_range *part) { return jfsx_crc32c_segments(c, cnt, part, mode, mem); });
 }
 
-static int mctx_lz4(jfsx_mctx *m, int op, int n, jfsx_zblk *z, int mem) {
-    if (!m || n < 0 || (n && !z)) return JFSX_EINVAL;
-    if (mem != JFSX_MEM_HOST && !(mem == JFSX_MEM_DEVICE && m->cs.size() == 1)) return JFSX_EINVAL;
-    if (n == 0) return 0;
-    const std::vector<int> cut = split_runs(n, (int)m->cs.size(), [&](int i) { return z[i].src_len; });
-    return fan_out(cut, [&](int k, int b0, int b1) {
-        return op == kLz4c   ? jfsx_lz4_compress_batch(m->cs[k], b1 - b0, z + b0, mem)
-               : op == kLz4d ? jfsx_lz4_decompress_batch(m->cs[k], b1 - b0, z + b0, mem)
-               : op == kZstdc ? jfsx_zstd_compress_batch(m->cs[k], b1 - b0, z + b0, mem)
-                              : jfsx_zstd_decompress_batch(m->cs[k], b1 - b0, z + b0, mem);
-    });
+static int mctx_codec(jfsx_mctx *m, int op, int n, jfsx_zblk *z, int mem) {
+    return mctx_run<jfsx_zblk>(
+        m, n, z, mem, [](const jfsx_zblk &b) { return b.src_len; },
+        [](const jfsx_zblk &b, const void **p) {
+            int np = 0;
+            if (b.src_len) p[np++] = b.src;
+            if (b.dst_cap) p[np++] = b.dst;
+            return np;
+        },
+        [&](jfsx_ctx *c, int cnt, jfsx_zblk *part) {
+            return op == kLz4c    ? jfsx_lz4_compress_batch(c, cnt, part, mem)
+                   : op == kLz4d  ? jfsx_lz4_decompress_batch(c, cnt, part, mem)
+                   : op == kZstdc ? jfsx_zstd_compress_batch(c, cnt, part, mem)
+                                  : jfsx_zstd_decompress_batch(c, cnt, part, mem);
+        });
 }
 
-int jfsx_mctx_lz4_compress_batch(jfsx_mctx *m, int n, jfsx_zblk *blks, int mem) { return mctx_lz4(m, kLz4c, n, blks, mem); }
+int jfsx_mctx_lz4_compress_batch(jfsx_mctx *m, int n, jfsx_zblk *blks, int mem) {
+    return mctx_codec(m, kLz4c, n, blks, mem);
+}
 int jfsx_mctx_lz4_decompress_batch(jfsx_mctx *m, int n, jfsx_zblk *blks, int mem) {
-    return mctx_lz4(m, kLz4d, n, blks, mem);
+    return mctx_codec(m, kLz4d, n, blks, mem);
 }
 int jfsx_mctx_zstd_decompress_batch(jfsx_mctx *m, int n, jfsx_zblk *blks, int mem) {
-    return mctx_lz4(m, kZstdd, n, blks, mem);
+    return mctx_codec(m, kZstdd, n, blks, mem);
 }
 
 int jfsx_mctx_zstd_compress_batch(jfsx_mctx *m, int n, jfsx_zblk *blks, int mem) {
-    return mctx_lz4(m, kZstdc, n, blks, mem);
+    return mctx_codec(m, kZstdc, n, blks, mem);
 }
 
 int jfsx_agg_new_mctx(jfsx_mctx *m, int max_blocks, uint64_t max_bytes, uint32_t window_us, jfsx_agg **out) {

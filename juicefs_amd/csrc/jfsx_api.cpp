@@ -4,13 +4,22 @@
 // A batch runs as: H2D of descriptors (one pinned copy) -> keysetup kernel ->
 // main transform kernel (one workgroup per task) -> finalize kernel -> D2H of
 // per-block results (tags, status, first failing CRC) -> stream sync.
+#include <ctype.h>
 #include <errno.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <functional>
+#include <map>
 #include <mutex>
+#include <shared_mutex>
 #include <vector>
 
 #include "jfsx_internal.h"
@@ -63,6 +72,21 @@ struct CtxScope {
     explicit CtxScope(jfsx_ctx *c) : prev(tl_ctx) { tl_ctx = c; }
     ~CtxScope() { tl_ctx = prev; }
 };
+
+// Device allocations made through jfsx_alloc_device, by address: a
+// multi-device context routes each block of a device-memory batch to the GPU
+// that owns its buffers (jfsx_mctx_seal_batch and friends).
+std::shared_mutex g_alloc_mu;
+std::map<uintptr_t, std::pair<uintptr_t, int>> g_allocs;  // base -> (end, device)
+
+void note_alloc(void *p, size_t bytes, int device) {
+    std::unique_lock<std::shared_mutex> g(g_alloc_mu);
+    g_allocs[(uintptr_t)p] = {(uintptr_t)p + bytes, device};
+}
+void forget_alloc(void *p) {
+    std::unique_lock<std::shared_mutex> g(g_alloc_mu);
+    g_allocs.erase((uintptr_t)p);
+}
 
 // ---------------------------------------------------------------------------
 // table construction (host)
@@ -181,12 +205,37 @@ struct Workspace {
     int n = 0;              // blocks of the batch in flight
     uint64_t nt = 0;        // tasks of the batch in flight
     const void *dout = nullptr;  // device BlkOut[n] of the batch in flight
+    bool timed = false;     // the batch's main kernel is bracketed by timing events
 };
 
-#ifndef JFSX_RING
-#define JFSX_RING 3
+constexpr int kRing = 1;  // workspace of the synchronous paths (device batches, CRC, codecs, generator)
+#ifndef JFSX_PIPE
+#define JFSX_PIPE 8
 #endif
-constexpr int kRing = JFSX_RING;  // host-ingest pipeline depth (H2D | transform | D2H)
+// Host-memory AEAD pipeline (run_aead_host): kPipe staging slots shared by every
+// thread that calls on the context.  A batch is cut into groups; each group
+// takes the next slot, is enqueued as H2D (s_in) -> keysetup/main/finalize
+// (stream) -> D2H (s_out) and the call moves on; it then waits for its own
+// groups' D2H events only.  The ring never drains between calls: while one
+// caller waits for its results, the next caller's H2D is already running
+// (per-object callers: the aggregator's dispatchers, cached_store.go:415-472).
+constexpr int kPipe = JFSX_PIPE;
+
+struct PipeGroup;
+struct PipeSlot {
+    std::mutex mu;               // held while the slot is completed or refilled
+    Workspace w;
+    hipEvent_t ev_in = nullptr, ev_comp = nullptr, ev_out = nullptr;
+    hipEvent_t ev_k0 = nullptr, ev_k1 = nullptr;  // main-kernel timing
+    PipeGroup *owner = nullptr;  // group in flight in this slot (its results not yet collected)
+};
+// one group of one host batch: where its results go once its D2H is done
+struct PipeGroup {
+    PipeSlot *slot = nullptr;
+    jfsx_blk *dv = nullptr;  // the call's per-block result records of this group
+    bool open = false;
+    int rc = 0;
+};
 
 }  // namespace
 
@@ -195,13 +244,15 @@ struct jfsx_ctx {
     hipStream_t stream = nullptr;  // transform stream
     hipStream_t s_in = nullptr;    // host-ingest H2D
     hipStream_t s_out = nullptr;   // host-ingest D2H
-    std::mutex mu;
+    std::mutex mu;                 // enqueue order on the streams; the synchronous paths' workspace
     uint32_t *d_tab = nullptr;  // aes | crc | crcx
     DevTables tabs{};
     Workspace ws[kRing];
-    hipEvent_t ev_in[kRing] = {}, ev_comp[kRing] = {}, ev_out[kRing] = {};
-    hipEvent_t ev_k0[kRing] = {}, ev_k1[kRing] = {};  // main-kernel timing per slot
-    size_t slot_bytes = (size_t)256 << 20;
+    hipEvent_t ev_k0[kRing] = {}, ev_k1[kRing] = {};  // main-kernel timing of the synchronous paths
+    PipeSlot pipe[kPipe];
+    int pipe_next = 0;  // next pipeline slot (under mu)
+    std::mutex stat_mu; // met, ms_total, launches
+    std::atomic<size_t> slot_bytes{(size_t)256 << 20};
     int ncu = 256;  // compute units: persistent transform kernels launch one workgroup per CU
     size_t zstd_arena_budget = 0;  // device bytes the block-parallel zstd decoder may hold (see run_codec)
     bool timing = false;
@@ -221,8 +272,14 @@ struct jfsx_ctx {
 };
 
 namespace {
-// jfsx_ctx_metrics tallies, under c->mu, after a batch returned 0
+void add_kernel_ms(jfsx_ctx *c, float ms) {
+    std::lock_guard<std::mutex> g(c->stat_mu);
+    c->ms_total += ms;
+    c->launches += 1;
+}
+// jfsx_ctx_metrics tallies after a batch returned 0
 void tally_aead(jfsx_ctx *c, bool open, int n, const jfsx_blk *b) {
+    std::lock_guard<std::mutex> g(c->stat_mu);
     jfsx_metrics &m = c->met;
     uint64_t bytes = 0, fail = 0;
     for (int i = 0; i < n; i++) {
@@ -241,6 +298,7 @@ void tally_aead(jfsx_ctx *c, bool open, int n, const jfsx_blk *b) {
     }
 }
 void tally_crc(jfsx_ctx *c, int n, const jfsx_range *r) {
+    std::lock_guard<std::mutex> g(c->stat_mu);
     jfsx_metrics &m = c->met;
     m.crc_batches++;
     m.crc_ranges += n;
@@ -249,7 +307,9 @@ void tally_crc(jfsx_ctx *c, int n, const jfsx_range *r) {
         m.crc_fail += r[i].status != JFSX_OK;
     }
 }
-void tally_codec(uint64_t &blocks, uint64_t &in, uint64_t &out, uint64_t *fail, int n, const jfsx_zblk *z) {
+void tally_codec(jfsx_ctx *c, uint64_t &blocks, uint64_t &in, uint64_t &out, uint64_t *fail, int n,
+                 const jfsx_zblk *z) {
+    std::lock_guard<std::mutex> g(c->stat_mu);
     blocks += n;
     for (int i = 0; i < n; i++) {
         in += z[i].src_len;
@@ -378,8 +438,9 @@ int check_aead_args(int algo, int n, const jfsx_blk *blks, int crc_mode, bool de
 // collect = false the caller downloads the BlkOut results on its own stream.
 // The compute stream then carries kernels only, so the H2D and D2H DMA of
 // neighbouring slots run concurrently (full duplex).
-int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, int k, int algo, bool open, int n, const jfsx_blk *blks,
-                 int crc_mode, hipStream_t up = nullptr, hipEvent_t up_ev = nullptr, bool collect = true) {
+int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEvent_t k1, int algo, bool open, int n,
+                 const jfsx_blk *blks, int crc_mode, hipStream_t up = nullptr, hipEvent_t up_ev = nullptr,
+                 bool collect = true) {
     const bool gcm = algo == JFSX_AES256GCM;
     std::vector<uint64_t> lens(n);
     uint64_t crc_calc_words = 0;
@@ -467,19 +528,19 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, int k, int algo, bool
         GcmSched *dsch = (GcmSched *)(d + o_sched);
         launch_begin();
         launch_gcm_keysetup(s, n, dk, db, dsch, c->tabs);
-        if (c->timing) HIP_OK(hipEventRecord(c->ev_k0[k], s));
+        if (c->timing) HIP_OK(hipEventRecord(k0, s));
         launch_gcm_main(s, (int)nt, c->ncu, (uint32_t *)(d + o_queue), open, crc_mode, c->bitslice, dt, db, dsch, dpart,
                         dpexp, c->tabs);
-        if (c->timing) HIP_OK(hipEventRecord(c->ev_k1[k], s));
+        if (c->timing) HIP_OK(hipEventRecord(k1, s));
         launch_gcm_finalize(s, n, open, crc_mode, db, dsch, dpart, dpexp, dout);
     } else {
         CpSched *dsch = (CpSched *)(d + o_sched);
         launch_begin();
         launch_cp_keysetup(s, n, dk, db, dsch);
-        if (c->timing) HIP_OK(hipEventRecord(c->ev_k0[k], s));
+        if (c->timing) HIP_OK(hipEventRecord(k0, s));
         launch_cp_main(s, (int)nt, c->ncu, (uint32_t *)(d + o_queue), open, crc_mode, dt, db, dsch, dpart, dpexp,
                        c->tabs);
-        if (c->timing) HIP_OK(hipEventRecord(c->ev_k1[k], s));
+        if (c->timing) HIP_OK(hipEventRecord(k1, s));
         launch_cp_finalize(s, n, open, crc_mode, db, dsch, dpart, dpexp, dout);
     }
     HIP_OK(hipGetLastError());
@@ -487,16 +548,17 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, int k, int algo, bool
     if (collect) HIP_OK(hipMemcpyAsync(h, dout, sizeof(BlkOut) * n, hipMemcpyDeviceToHost, s));
     w.n = n;
     w.nt = nt;
+    w.timed = c->timing;
     return 0;
 }
 
 // After the batch's stream work completed: per-block results into blks.
-int finish_aead(jfsx_ctx *c, Workspace &w, int k, bool open, jfsx_blk *blks) {
-    if (c->timing && w.nt) {
+int finish_aead(jfsx_ctx *c, Workspace &w, hipEvent_t k0, hipEvent_t k1, bool open, jfsx_blk *blks) {
+    if (w.timed && w.nt) {
         float ms = 0;
-        HIP_OK(hipEventElapsedTime(&ms, c->ev_k0[k], c->ev_k1[k]));
-        c->ms_total += ms;
-        c->launches += 1;
+        w.timed = false;
+        HIP_OK(hipEventElapsedTime(&ms, k0, k1));
+        add_kernel_ms(c, ms);
     }
     const BlkOut *ho = (const BlkOut *)w.h;
     for (int i = 0; i < w.n; i++) {
@@ -537,176 +599,206 @@ int wipe_failed(hipStream_t s, int n, const jfsx_blk *blks, int crc_mode, bool d
     return 0;
 }
 
-// Device-resident batch: one enqueue, one sync.
+// Device-resident batch: one enqueue, one sync (under c->mu).
 int run_aead(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mode) {
     int rc = check_aead_args(algo, n, blks, crc_mode, true);
     if (rc || n == 0) return rc;
-    if ((rc = enqueue_aead(c, c->ws[0], c->stream, 0, algo, open, n, blks, crc_mode))) {
+    if ((rc = enqueue_aead(c, c->ws[0], c->stream, c->ev_k0[0], c->ev_k1[0], algo, open, n, blks, crc_mode))) {
         (void)hipStreamSynchronize(c->stream);  // nothing of this batch left in flight
+        c->ws[0].timed = false;
         return rc;
     }
     HIP_OK(hipStreamSynchronize(c->stream));
-    if ((rc = finish_aead(c, c->ws[0], 0, open, blks))) return rc;
+    if ((rc = finish_aead(c, c->ws[0], c->ev_k0[0], c->ev_k1[0], open, blks))) return rc;
     return open ? wipe_failed(c->stream, n, blks, crc_mode, true) : 0;
 }
 
-// Host-memory batch (host ingest): blocks are grouped into slots of up to
-// slot_bytes and streamed through a ring of kRing device staging buffers:
-// H2D on s_in, transform on stream, D2H on s_out, chained by events, so the
-// copies of one slot overlap the transform of the next.  Open releases no
-// plaintext of a block whose tag failed: its destination is wiped before the
-// call returns.
-int run_aead_host_ring(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mode);
+// staging bytes of one host block in a pipeline slot: data, then its CRC array
+inline size_t host_need(const jfsx_blk &b, int crc_mode) {
+    return align256(b.len) + (crc_mode ? align256(4 * nseg_of(b.len)) : 0);
+}
 
-// On an error inside the ring, slots still in flight would keep copying into
-// the caller's dst/crc after the call returned: wait for all three streams
-// first, so an error return means nothing of the batch is still running.
+// The groups of a host batch: runs of blocks of up to slot_bytes; a batch
+// smaller than a few slots is cut into about 6 groups (>= 16 MiB each) so that
+// its own copies and transforms overlap too.
+std::vector<std::pair<int, int>> host_groups(const jfsx_ctx *c, int n, const jfsx_blk *blks, int crc_mode) {
+    std::vector<std::pair<int, int>> groups;  // [b0, b1)
+    size_t total = 0;
+    for (int i = 0; i < n; i++) total += host_need(blks[i], crc_mode);
+    const size_t slot = std::min(c->slot_bytes.load(), std::max<size_t>((size_t)16 << 20, total / 6));
+    int b0 = 0;
+    size_t acc = 0;
+    for (int i = 0; i < n; i++) {
+        const size_t need = host_need(blks[i], crc_mode);
+        if (i > b0 && acc + need > slot) {
+            groups.push_back({b0, i});
+            b0 = i;
+            acc = 0;
+        }
+        acc += need;
+    }
+    groups.push_back({b0, n});
+    return groups;
+}
+
+// Collect the group in flight in slot s (s.mu held; called by the group's own
+// caller, or by any caller that needs the slot next): wait for its D2H and
+// write its per-block results into the owner's records.
+void pipe_collect(jfsx_ctx *c, PipeSlot &s) {
+    PipeGroup *g = s.owner;
+    if (!g) return;
+    s.owner = nullptr;
+    const hipError_t e = hipEventSynchronize(s.ev_out);
+    if (e != hipSuccess) {
+        note_hip_error(e, __FILE__, __LINE__, "hipEventSynchronize(pipeline slot)");
+        g->rc = JFSX_EIO;
+        s.w.n = 0;
+        s.w.nt = 0;
+        s.w.timed = false;
+        return;
+    }
+    g->rc = finish_aead(c, s.w, s.ev_k0, s.ev_k1, g->open, g->dv);
+}
+
+// One group into an empty slot (c->mu and s.mu held): the blocks' data runs up
+// on s_in into the slot's staging (all data first, coalesced where the
+// caller's blocks are adjacent, then the CRC arrays), keysetup / main /
+// finalize on the transform stream, and the outputs, CRC arrays and BlkOut
+// records down on s_out, chained by the slot's events.  dv[i] (the call's copy
+// of blks[i]) is pointed at the staging copy.
+int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, int algo, bool open, int nb, const jfsx_blk *blks, jfsx_blk *dv,
+                 int crc_mode) {
+    Workspace &w = s.w;
+    size_t need = 0;
+    for (int i = 0; i < nb; i++) need += host_need(blks[i], crc_mode);
+    int rc;
+    if ((rc = ensure_dev(c, &w.stage, &w.scap, std::max<size_t>(need, 256)))) return rc;
+    size_t off = 0, coff = 0;
+    for (int i = 0; i < nb; i++) coff += align256(blks[i].len);
+    const char *run_h = nullptr;
+    char *run_d = nullptr;
+    size_t run_n = 0;
+    auto flush_in = [&]() -> int {
+        if (run_n) HIP_OK(hipMemcpyAsync(run_d, run_h, run_n, hipMemcpyHostToDevice, c->s_in));
+        run_n = 0;
+        return 0;
+    };
+    for (int i = 0; i < nb; i++) {
+        char *buf = w.stage + off;
+        off += align256(blks[i].len);
+        if (blks[i].len) {
+            const char *hs = (const char *)blks[i].src;
+            if (!(run_n && run_h + run_n == hs && run_d + run_n == buf) && (rc = flush_in())) return rc;
+            if (!run_n) {
+                run_h = hs;
+                run_d = buf;
+            }
+            run_n += blks[i].len;
+            if (align256(blks[i].len) != blks[i].len && (rc = flush_in())) return rc;
+        }
+        dv[i].src = buf;
+        dv[i].dst = buf;
+        if (crc_mode) {
+            char *cb = w.stage + coff;
+            coff += align256(4 * nseg_of(blks[i].len));
+            if ((crc_mode & 3) == JFSX_CRC_VERIFY)
+                HIP_OK(hipMemcpyAsync(cb, blks[i].crc, 4 * nseg_of(blks[i].len), hipMemcpyHostToDevice, c->s_in));
+            dv[i].crc = (uint8_t *)cb;
+        }
+    }
+    if ((rc = flush_in())) return rc;
+    if ((rc = enqueue_aead(c, w, c->stream, s.ev_k0, s.ev_k1, algo, open, nb, dv, crc_mode, c->s_in, s.ev_in, false)))
+        return rc;
+    HIP_OK(hipEventRecord(s.ev_comp, c->stream));
+    HIP_OK(hipStreamWaitEvent(c->s_out, s.ev_comp, 0));
+    char *oh = nullptr;
+    const char *od = nullptr;
+    size_t on = 0;
+    auto flush_out = [&]() -> int {
+        if (on) HIP_OK(hipMemcpyAsync(oh, od, on, hipMemcpyDeviceToHost, c->s_out));
+        on = 0;
+        return 0;
+    };
+    for (int i = 0; i < nb; i++) {
+        if (!blks[i].len) continue;
+        char *hd = (char *)blks[i].dst;
+        const char *dd = (const char *)dv[i].dst;
+        if (!(on && oh + on == hd && od + on == dd) && (rc = flush_out())) return rc;
+        if (!on) {
+            oh = hd;
+            od = dd;
+        }
+        on += blks[i].len;
+        if (align256(blks[i].len) != blks[i].len && (rc = flush_out())) return rc;
+    }
+    if ((rc = flush_out())) return rc;
+    if ((crc_mode & 3) == JFSX_CRC_GEN) {
+        // CRC arrays: one copy per run that is contiguous on both sides
+        for (int i = 0; i < nb; i++) {
+            const size_t cn = 4 * nseg_of(blks[i].len);
+            char *hd = (char *)blks[i].crc;
+            const char *dd = (const char *)dv[i].crc;
+            if (!(on && oh + on == hd && od + on == dd) && (rc = flush_out())) return rc;
+            if (!on) {
+                oh = hd;
+                od = dd;
+            }
+            on += cn;
+            if (align256(cn) != cn && (rc = flush_out())) return rc;
+        }
+        if ((rc = flush_out())) return rc;
+    }
+    HIP_OK(hipMemcpyAsync(w.h, w.dout, sizeof(BlkOut) * nb, hipMemcpyDeviceToHost, c->s_out));
+    HIP_OK(hipEventRecord(s.ev_out, c->s_out));
+    return 0;
+}
+
+// Host-memory batch (host ingest and the per-object shim).  No lock is held
+// while the call waits: groups are enqueued one at a time under c->mu into the
+// next pipeline slot (collecting whatever group still occupies it), then the
+// call waits for its own groups' D2H events.  So concurrent callers keep the
+// H2D and D2H engines busy back to back instead of filling and draining the
+// ring once per call.  Open releases no plaintext of a block whose tag failed:
+// its destination is wiped before the call returns.  On an enqueue error the
+// three streams are drained first, so an error return means nothing of the
+// batch is still copying into the caller's buffers.
 int run_aead_host(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mode) {
     int rc = check_aead_args(algo, n, blks, crc_mode, false);
     if (rc || n == 0) return rc;
-    rc = run_aead_host_ring(c, algo, open, n, blks, crc_mode);
-    if (rc) {
-        (void)hipStreamSynchronize(c->s_in);
-        (void)hipStreamSynchronize(c->stream);
-        (void)hipStreamSynchronize(c->s_out);
-        for (int k = 0; k < kRing; k++) {
-            c->ws[k].n = 0;
-            c->ws[k].nt = 0;
-        }
-    }
-    return rc;
-}
-
-int run_aead_host_ring(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mode) {
-    int rc = 0;
-    // group blocks into slots; a batch smaller than the ring is cut into about
-    // 2*kRing slots (>= 16 MiB each) so that its copies and transforms still
-    // overlap -- the aggregator's batches are tens of MiB
-    std::vector<std::pair<int, int>> groups;  // [b0, b1)
-    {
-        size_t total = 0;
-        for (int i = 0; i < n; i++)
-            total += align256(blks[i].len) + (crc_mode ? align256(4 * nseg_of(blks[i].len)) : 0);
-        const size_t slot = std::min(c->slot_bytes, std::max<size_t>((size_t)16 << 20, total / (2 * kRing)));
-        int b0 = 0;
-        size_t acc = 0;
-        for (int i = 0; i < n; i++) {
-            const size_t need = align256(blks[i].len) + (crc_mode ? align256(4 * nseg_of(blks[i].len)) : 0);
-            if (i > b0 && acc + need > slot) {
-                groups.push_back({b0, i});
-                b0 = i;
-                acc = 0;
-            }
-            acc += need;
-        }
-        groups.push_back({b0, n});
-    }
+    const std::vector<std::pair<int, int>> groups = host_groups(c, n, blks, crc_mode);
     std::vector<jfsx_blk> dv(blks, blks + n);
-    int busy[kRing];  // group in flight per slot
-    for (int k = 0; k < kRing; k++) busy[k] = -1;
-    auto drain = [&](int k) -> int {
-        if (busy[k] < 0) return 0;
-        HIP_OK(hipEventSynchronize(c->ev_out[k]));
-        const int g = busy[k];
-        int r = finish_aead(c, c->ws[k], k, open, dv.data() + groups[g].first);
-        busy[k] = -1;
-        return r;
-    };
-    for (size_t g = 0; g < groups.size(); g++) {
-        const int k = (int)(g % kRing);
-        if ((rc = drain(k))) return rc;
-        Workspace &w = c->ws[k];
+    std::vector<PipeGroup> recs(groups.size());
+    size_t issued = 0;
+    for (size_t g = 0; g < groups.size() && !rc; g++) {
+        std::lock_guard<std::mutex> lk(c->mu);
+        PipeSlot &s = c->pipe[c->pipe_next];
+        c->pipe_next = (c->pipe_next + 1) % kPipe;
+        std::lock_guard<std::mutex> sl(s.mu);
+        pipe_collect(c, s);
         const int b0 = groups[g].first, b1 = groups[g].second;
-        size_t need = 0;
-        for (int i = b0; i < b1; i++)
-            need += align256(blks[i].len) + (crc_mode ? align256(4 * nseg_of(blks[i].len)) : 0);
-        if ((rc = ensure_dev(c, &w.stage, &w.scap, std::max<size_t>(need, 256)))) return rc;
-        // slot layout: all block data first (coalesced DMA runs over blocks
-        // adjacent in both the caller's memory and the slot), then the CRCs
-        size_t off = 0, coff = 0;
-        for (int i = b0; i < b1; i++) coff += align256(blks[i].len);
-        const char *run_h = nullptr;
-        char *run_d = nullptr;
-        size_t run_n = 0;
-        auto flush_in = [&]() -> int {
-            if (run_n) HIP_OK(hipMemcpyAsync(run_d, run_h, run_n, hipMemcpyHostToDevice, c->s_in));
-            run_n = 0;
-            return 0;
-        };
-        for (int i = b0; i < b1; i++) {
-            char *buf = w.stage + off;
-            off += align256(blks[i].len);
-            if (blks[i].len) {
-                const char *hs = (const char *)blks[i].src;
-                if (!(run_n && run_h + run_n == hs && run_d + run_n == buf) && (rc = flush_in())) return rc;
-                if (!run_n) {
-                    run_h = hs;
-                    run_d = buf;
-                }
-                run_n += blks[i].len;
-                if (align256(blks[i].len) != blks[i].len && (rc = flush_in())) return rc;
-            }
-            dv[i].src = buf;
-            dv[i].dst = buf;
-            if (crc_mode) {
-                char *cb = w.stage + coff;
-                coff += align256(4 * nseg_of(blks[i].len));
-                if ((crc_mode & 3) == JFSX_CRC_VERIFY)
-                    HIP_OK(hipMemcpyAsync(cb, blks[i].crc, 4 * nseg_of(blks[i].len), hipMemcpyHostToDevice, c->s_in));
-                dv[i].crc = (uint8_t *)cb;
-            }
+        rc = pipe_enqueue(c, s, algo, open, b1 - b0, blks + b0, dv.data() + b0, crc_mode);
+        if (rc) {
+            (void)hipStreamSynchronize(c->s_in);
+            (void)hipStreamSynchronize(c->stream);
+            (void)hipStreamSynchronize(c->s_out);
+            s.w.n = 0;
+            s.w.nt = 0;
+            s.w.timed = false;
+            break;
         }
-        if ((rc = flush_in())) return rc;
-        if ((rc = enqueue_aead(c, w, c->stream, k, algo, open, b1 - b0, dv.data() + b0, crc_mode, c->s_in, c->ev_in[k],
-                               false)))
-            return rc;
-        HIP_OK(hipEventRecord(c->ev_comp[k], c->stream));
-        HIP_OK(hipStreamWaitEvent(c->s_out, c->ev_comp[k], 0));
-        {
-            char *oh = nullptr;
-            const char *od = nullptr;
-            size_t on = 0;
-            auto flush_out = [&]() -> int {
-                if (on) HIP_OK(hipMemcpyAsync(oh, od, on, hipMemcpyDeviceToHost, c->s_out));
-                on = 0;
-                return 0;
-            };
-            for (int i = b0; i < b1; i++) {
-                if (!blks[i].len) continue;
-                char *hd = (char *)blks[i].dst;
-                const char *dd = (const char *)dv[i].dst;
-                if (!(on && oh + on == hd && od + on == dd) && (rc = flush_out())) return rc;
-                if (!on) {
-                    oh = hd;
-                    od = dd;
-                }
-                on += blks[i].len;
-                if (align256(blks[i].len) != blks[i].len && (rc = flush_out())) return rc;
-            }
-            if ((rc = flush_out())) return rc;
-            if ((crc_mode & 3) == JFSX_CRC_GEN) {
-                // CRC arrays: one copy per run that is contiguous on both sides
-                for (int i = b0; i < b1; i++) {
-                    const size_t cn = 4 * nseg_of(blks[i].len);
-                    char *hd = (char *)blks[i].crc;
-                    const char *dd = (const char *)dv[i].crc;
-                    if (!(on && oh + on == hd && od + on == dd) && (rc = flush_out())) return rc;
-                    if (!on) {
-                        oh = hd;
-                        od = dd;
-                    }
-                    on += cn;
-                    if (align256(cn) != cn && (rc = flush_out())) return rc;
-                }
-                if ((rc = flush_out())) return rc;
-            }
-            HIP_OK(hipMemcpyAsync(w.h, w.dout, sizeof(BlkOut) * (b1 - b0), hipMemcpyDeviceToHost, c->s_out));
-        }
-        HIP_OK(hipEventRecord(c->ev_out[k], c->s_out));
-        busy[k] = (int)g;
+        recs[g].slot = &s;
+        recs[g].dv = dv.data() + b0;
+        recs[g].open = open;
+        s.owner = &recs[g];
+        issued++;
     }
-    for (int k = 0; k < kRing; k++)
-        if ((rc = drain(k))) return rc;
+    for (size_t g = 0; g < issued; g++) {
+        PipeSlot &s = *recs[g].slot;
+        std::lock_guard<std::mutex> sl(s.mu);
+        if (s.owner == &recs[g]) pipe_collect(c, s);
+        if (recs[g].rc && !rc) rc = recs[g].rc;
+    }
+    if (rc) return rc;
     for (int i = 0; i < n; i++) {
         blks[i].status = dv[i].status;
         blks[i].crc_bad_seg = dv[i].crc_bad_seg;
@@ -773,8 +865,7 @@ int run_crc(jfsx_ctx *c, int n, jfsx_range *r, int mode) {
     if (c->timing && nt) {
         float ms = 0;
         HIP_OK(hipEventElapsedTime(&ms, c->ev_k0[0], c->ev_k1[0]));
-        c->ms_total += ms;
-        c->launches += 1;
+        add_kernel_ms(c, ms);
     }
     const BlkOut *ho = (const BlkOut *)h;
     for (int i = 0; i < n; i++) {
@@ -918,15 +1009,17 @@ int run_codec(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, CodecOp op) {
     if (c->timing) {
         float ms = 0;
         HIP_OK(hipEventElapsedTime(&ms, c->ev_k0[0], c->ev_k1[0]));
-        c->ms_total += ms;
-        c->launches += 1;
+        add_kernel_ms(c, ms);
     }
     for (int i = 0; i < n; i++) {
         z[i].out_len = ho[i].out_len;
         z[i].status = ho[i].status;
         if (op == kZstdDecomp) {
             z[i].reserved = zd_waves ? ho[i].fallback : 0;
-            if (zd_waves) c->met.zstd_serial += ho[i].fallback != 0;
+            if (zd_waves && ho[i].fallback) {
+                std::lock_guard<std::mutex> g(c->stat_mu);
+                c->met.zstd_serial++;
+            }
         }
         if (mem == JFSX_MEM_HOST && ho[i].out_len)
             HIP_OK(hipMemcpyAsync(z[i].dst, sdst[i], ho[i].out_len, hipMemcpyDeviceToHost, s));
@@ -936,6 +1029,34 @@ int run_codec(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, CodecOp op) {
 }
 
 }  // namespace
+
+namespace jfsx {
+// The device that owns p, with the bounds [lo, hi) of the allocation it lies
+// in (so a caller can skip lookups for neighbouring pointers); -1 when p is
+// not device memory.  jfsx_alloc_device allocations are found in the
+// registry; other pointers are asked of the HIP runtime.
+int device_of(const void *p, uintptr_t *lo, uintptr_t *hi) {
+    const uintptr_t a = (uintptr_t)p;
+    {
+        std::shared_lock<std::shared_mutex> g(g_alloc_mu);
+        auto it = g_allocs.upper_bound(a);
+        if (it != g_allocs.begin()) {
+            --it;
+            if (a < it->second.first) {
+                *lo = it->first;
+                *hi = it->second.first;
+                return it->second.second;
+            }
+        }
+    }
+    *lo = a;
+    *hi = a + 1;
+    hipPointerAttribute_t at;
+    if (p && hipPointerGetAttributes(&at, p) == hipSuccess && at.type == hipMemoryTypeDevice) return at.device;
+    (void)hipGetLastError();
+    return -1;
+}
+}  // namespace jfsx
 
 // ===========================================================================
 // exported C-ABI
@@ -1017,10 +1138,16 @@ int jfsx_ctx_open(int device, uint32_t flags, jfsx_ctx **out) {
     c->tabs.crc = c->d_tab + aes.size();
     c->tabs.crcx = c->d_tab + aes.size() + crc.size();
     for (int k = 0; k < kRing; k++) {
-        if (hipEventCreateWithFlags(&c->ev_in[k], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c->ev_comp[k], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c->ev_out[k], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreate(&c->ev_k0[k]) != hipSuccess || hipEventCreate(&c->ev_k1[k]) != hipSuccess) {
+        if (hipEventCreate(&c->ev_k0[k]) != hipSuccess || hipEventCreate(&c->ev_k1[k]) != hipSuccess) {
+            jfsx_ctx_close(c);
+            return JFSX_EIO;
+        }
+    }
+    for (PipeSlot &p : c->pipe) {
+        if (hipEventCreateWithFlags(&p.ev_in, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&p.ev_comp, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&p.ev_out, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreate(&p.ev_k0) != hipSuccess || hipEventCreate(&p.ev_k1) != hipSuccess) {
             jfsx_ctx_close(c);
             return JFSX_EIO;
         }
@@ -1043,7 +1170,15 @@ int jfsx_ctx_close(jfsx_ctx *c) {
         if (w.d) (void)hipFree(w.d);
         if (w.stage) (void)hipFree(w.stage);
         if (w.h) (void)hipHostFree(w.h);
-        hipEvent_t evs[5] = {c->ev_in[k], c->ev_comp[k], c->ev_out[k], c->ev_k0[k], c->ev_k1[k]};
+        hipEvent_t evs[2] = {c->ev_k0[k], c->ev_k1[k]};
+        for (hipEvent_t e : evs)
+            if (e) (void)hipEventDestroy(e);
+    }
+    for (PipeSlot &p : c->pipe) {
+        if (p.w.d) (void)hipFree(p.w.d);
+        if (p.w.stage) (void)hipFree(p.w.stage);
+        if (p.w.h) (void)hipHostFree(p.w.h);
+        hipEvent_t evs[5] = {p.ev_in, p.ev_comp, p.ev_out, p.ev_k0, p.ev_k1};
         for (hipEvent_t e : evs)
             if (e) (void)hipEventDestroy(e);
     }
@@ -1065,8 +1200,6 @@ int jfsx_ctx_sync(jfsx_ctx *c) {
 
 int jfsx_ctx_set_slot_bytes(jfsx_ctx *c, uint64_t bytes) {
     if (!c || bytes < (1u << 20)) return JFSX_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
-    CtxScope es_(c);
     c->slot_bytes = (size_t)bytes;
     return 0;
 }
@@ -1083,8 +1216,7 @@ int jfsx_ctx_set_timing(jfsx_ctx *c, int enable) {
 
 int jfsx_ctx_kernel_time(jfsx_ctx *c, double *ms_total, uint64_t *launches, int reset) {
     if (!c) return JFSX_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
-    CtxScope es_(c);
+    std::lock_guard<std::mutex> g(c->stat_mu);
     if (ms_total) *ms_total = c->ms_total;
     if (launches) *launches = c->launches;
     if (reset) {
@@ -1163,7 +1295,7 @@ int jfsx_pcie_probe(jfsx_ctx *c, uint64_t bytes, double out[4]) {
 
 int jfsx_ctx_metrics(jfsx_ctx *c, jfsx_metrics *out, int reset) {
     if (!c || !out) return JFSX_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::mutex> g(c->stat_mu);
     *out = c->met;
     out->kernel_ms = c->ms_total;
     out->kernel_launches = c->launches;
@@ -1185,6 +1317,76 @@ int jfsx_alloc_pinned(jfsx_ctx *c, size_t bytes, void **p) {
     note_hip_error(e, __FILE__, __LINE__, "hipHostMalloc(pinned)");
     return JFSX_ENOMEM;
 }
+int jfsx_device_numa_node(int device, int *node) {
+    if (!node) return JFSX_EINVAL;
+    *node = -1;
+    int nd = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess || device < 0 || device >= nd) return JFSX_ENODEV;
+    int v = -1;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeHostNumaId, device) == hipSuccess && v >= 0) {
+        *node = v;
+        return 0;
+    }
+    (void)hipGetLastError();
+    // the PCI function's node, as the kernel reports it
+    char bus[64] = {0}, path[160];
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) return 0;
+    for (char *q = bus; *q; q++) *q = (char)tolower(*q);
+    snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bus);
+    if (FILE *f = fopen(path, "r")) {
+        if (fscanf(f, "%d", &v) == 1 && v >= 0) *node = v;
+        fclose(f);
+    }
+    return 0;
+}
+
+namespace {
+// set_mempolicy / get_mempolicy (numaif.h modes), called directly so the
+// library needs no libnuma
+constexpr int kMpolDefault = 0, kMpolBind = 2, kMpolFNode = 1, kMpolFAddr = 2;
+constexpr unsigned long kMaxNodes = 1024;
+}  // namespace
+
+int jfsx_alloc_pinned_node(jfsx_ctx *c, size_t bytes, int node, void **p) {
+    if (!c || !p || node < -1 || node >= (int)kMaxNodes) return JFSX_EINVAL;
+    CtxScope es_(c);
+    HIP_OK(hipSetDevice(c->device));
+    if (node < 0 && jfsx_device_numa_node(c->device, &node)) node = -1;
+    // Bind this thread's allocations to the node while the runtime allocates
+    // and pins the pages (hipHostMallocNumaUser: they follow the caller's
+    // policy), then restore the thread's own policy.  Where the node cannot be
+    // bound (a cpuset without it), the default placement is used.
+    unsigned long old_mask[kMaxNodes / 64] = {0}, mask[kMaxNodes / 64] = {0};
+    int old_mode = kMpolDefault;
+    bool bound = false;
+    if (node >= 0 && syscall(SYS_get_mempolicy, &old_mode, old_mask, kMaxNodes, nullptr, 0) == 0) {
+        mask[node / 64] = 1ul << (node % 64);
+        bound = syscall(SYS_set_mempolicy, kMpolBind, mask, kMaxNodes) == 0;
+    }
+    const hipError_t e = hipHostMalloc(p, bytes, hipHostMallocPortable | (bound ? hipHostMallocNumaUser : 0));
+    if (bound) (void)syscall(SYS_set_mempolicy, old_mode, old_mode == kMpolDefault ? nullptr : old_mask, kMaxNodes);
+    if (e == hipSuccess) return 0;
+    note_hip_error(e, __FILE__, __LINE__, "hipHostMalloc(pinned, NUMA node)");
+    return JFSX_ENOMEM;
+}
+
+int jfsx_host_numa_node(const void *p, size_t bytes, int *node) {
+    if (!p || !node) return JFSX_EINVAL;
+    *node = -1;
+    const size_t page = 4096, step = (size_t)64 << 20;
+    for (size_t o = 0; o < std::max<size_t>(bytes, 1); o += step) {
+        int nd = -1;
+        void *a = (void *)(((uintptr_t)p + o) & ~(uintptr_t)(page - 1));
+        if (syscall(SYS_get_mempolicy, &nd, nullptr, 0, a, kMpolFNode | kMpolFAddr) != 0) return 0;
+        if (*node == -1) *node = nd;
+        else if (*node != nd) {
+            *node = -2;
+            return 0;
+        }
+    }
+    return 0;
+}
+
 int jfsx_free_pinned(jfsx_ctx *c, void *p) {
     if (!c) return JFSX_EINVAL;
     HIP_OK(hipHostFree(p));
@@ -1195,12 +1397,16 @@ int jfsx_alloc_device(jfsx_ctx *c, size_t bytes, void **p) {
     CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
     const hipError_t e = hipMalloc(p, bytes);
-    if (e == hipSuccess) return 0;
+    if (e == hipSuccess) {
+        note_alloc(*p, bytes, c->device);
+        return 0;
+    }
     note_hip_error(e, __FILE__, __LINE__, "hipMalloc(device buffer)");
     return JFSX_ENOMEM;
 }
 int jfsx_free_device(jfsx_ctx *c, void *p) {
     if (!c) return JFSX_EINVAL;
+    forget_alloc(p);
     HIP_OK(hipFree(p));
     return 0;
 }
@@ -1221,26 +1427,32 @@ int jfsx_memcpy_d2h(jfsx_ctx *c, void *dst, const void *src, size_t bytes) {
     return 0;
 }
 
-int jfsx_seal_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *blks, int crc_mode, int mem) {
+namespace {
+// host batches lock per group inside the pipeline (the call waits unlocked);
+// device batches hold the context for the whole call
+int aead_entry(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mode, int mem) {
     if (!c || (n > 0 && !blks)) return JFSX_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    if (mem != JFSX_MEM_HOST && mem != JFSX_MEM_DEVICE) return JFSX_EINVAL;
     CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
-    const int rc = mem == JFSX_MEM_HOST ? run_aead_host(c, algo, false, n, blks, crc_mode)
-                                        : run_aead(c, algo, false, n, blks, crc_mode);
-    if (rc == 0) tally_aead(c, false, n, blks);
+    int rc;
+    if (mem == JFSX_MEM_HOST) {
+        rc = run_aead_host(c, algo, open, n, blks, crc_mode);
+    } else {
+        std::lock_guard<std::mutex> g(c->mu);
+        rc = run_aead(c, algo, open, n, blks, crc_mode);
+    }
+    if (rc == 0) tally_aead(c, open, n, blks);
     return rc;
+}
+}  // namespace
+
+int jfsx_seal_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *blks, int crc_mode, int mem) {
+    return aead_entry(c, algo, false, n, blks, crc_mode, mem);
 }
 
 int jfsx_open_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *blks, int crc_mode, int mem) {
-    if (!c || (n > 0 && !blks)) return JFSX_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
-    CtxScope es_(c);
-    HIP_OK(hipSetDevice(c->device));
-    const int rc = mem == JFSX_MEM_HOST ? run_aead_host(c, algo, true, n, blks, crc_mode)
-                                        : run_aead(c, algo, true, n, blks, crc_mode);
-    if (rc == 0) tally_aead(c, true, n, blks);
-    return rc;
+    return aead_entry(c, algo, true, n, blks, crc_mode, mem);
 }
 
 int jfsx_crc32c_segments(jfsx_ctx *c, int n, jfsx_range *ranges, int mode, int mem) {
@@ -1261,7 +1473,7 @@ int jfsx_lz4_compress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
     CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
     const int rc = run_codec(c, n, blks, mem, kLz4Comp);
-    if (rc == 0) tally_codec(c->met.lz4c_blocks, c->met.lz4c_in, c->met.lz4c_out, nullptr, n, blks);
+    if (rc == 0) tally_codec(c, c->met.lz4c_blocks, c->met.lz4c_in, c->met.lz4c_out, nullptr, n, blks);
     return rc;
 }
 
@@ -1271,7 +1483,7 @@ int jfsx_lz4_decompress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
     CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
     const int rc = run_codec(c, n, blks, mem, kLz4Decomp);
-    if (rc == 0) tally_codec(c->met.lz4d_blocks, c->met.lz4d_in, c->met.lz4d_out, &c->met.lz4d_fail, n, blks);
+    if (rc == 0) tally_codec(c, c->met.lz4d_blocks, c->met.lz4d_in, c->met.lz4d_out, &c->met.lz4d_fail, n, blks);
     return rc;
 }
 
@@ -1281,7 +1493,7 @@ int jfsx_zstd_decompress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
     CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
     const int rc = run_codec(c, n, blks, mem, kZstdDecomp);
-    if (rc == 0) tally_codec(c->met.zstdd_blocks, c->met.zstdd_in, c->met.zstdd_out, &c->met.zstdd_fail, n, blks);
+    if (rc == 0) tally_codec(c, c->met.zstdd_blocks, c->met.zstdd_in, c->met.zstdd_out, &c->met.zstdd_fail, n, blks);
     return rc;
 }
 
@@ -1293,7 +1505,7 @@ int jfsx_zstd_compress_batch(jfsx_ctx *c, int n, jfsx_zblk *blks, int mem) {
     CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
     const int rc = run_codec(c, n, blks, mem, kZstdComp);
-    if (rc == 0) tally_codec(c->met.zstdc_blocks, c->met.zstdc_in, c->met.zstdc_out, nullptr, n, blks);
+    if (rc == 0) tally_codec(c, c->met.zstdc_blocks, c->met.zstdc_in, c->met.zstdc_out, nullptr, n, blks);
     return rc;
 }
 
@@ -1489,11 +1701,19 @@ int jfsx_object_crc32c(const void *hdr, uint64_t hlen, const uint8_t *seg_crcs, 
     return 0;
 }
 
-int jfsx_data_encrypt(jfsx_ctx *c, int algo, const uint8_t key[32], const uint8_t nonce[12], const uint8_t *wrapped,
-                      int wlen, const void *plaintext, uint64_t len, void *out, uint64_t out_cap, uint64_t *out_len,
-                      uint32_t *obj_crc) {
+}  // extern "C"
+
+namespace {
+// dataEncryptor.Encrypt / Decrypt around one Seal / Open, issued either as a
+// one-block batch on a context or through the aggregator (jfsx_agg_data_*)
+using AeadFn = std::function<int(jfsx_blk *, int crc_mode)>;
+
+int data_encrypt(const AeadFn &seal, int algo, const uint8_t key[32], const uint8_t nonce[12], const uint8_t *wrapped,
+                 int wlen, const void *plaintext, uint64_t len, void *out, uint64_t out_cap, uint64_t *out_len,
+                 uint32_t *obj_crc) {
     // encrypt.go:182-193: [BE16 klen][nlen][wrapped key][nonce][Seal(plaintext)]
-    if (!c || !key || !nonce || wlen < 0 || wlen > 65535 || (wlen && !wrapped) || !out) return JFSX_EINVAL;
+    if (!key || !nonce || wlen < 0 || wlen > 65535 || (wlen && !wrapped) || !out) return JFSX_EINVAL;
+    if (algo != JFSX_AES256GCM && algo != JFSX_CHACHA20P1305) return JFSX_EINVAL;
     const uint64_t hdr = 3 + (uint64_t)wlen + 12;
     if (out_cap < hdr + len + 16) return JFSX_EINVAL;
     uint8_t *o = (uint8_t *)out;
@@ -1514,7 +1734,7 @@ int jfsx_data_encrypt(jfsx_ctx *c, int algo, const uint8_t key[32], const uint8_
         segs.resize(4 * nseg_of(len));
         b.crc = segs.data();
     }
-    int rc = jfsx_seal_batch(c, algo, 1, &b, obj_crc ? JFSX_CRC_GEN | JFSX_CRC_CT : JFSX_CRC_NONE, JFSX_MEM_HOST);
+    int rc = seal(&b, obj_crc ? JFSX_CRC_GEN | JFSX_CRC_CT : JFSX_CRC_NONE);
     if (rc) return rc;
     memcpy(o + hdr + len, b.tag, 16);
     if (obj_crc && (rc = jfsx_object_crc32c(o, hdr, segs.data(), len, b.tag, obj_crc))) return rc;
@@ -1522,11 +1742,11 @@ int jfsx_data_encrypt(jfsx_ctx *c, int algo, const uint8_t key[32], const uint8_
     return 0;
 }
 
-int jfsx_data_decrypt(jfsx_ctx *c, int algo, const uint8_t key[32], const void *obj, uint64_t olen, void *out,
-                      uint64_t out_cap, uint64_t *out_len, const uint32_t *expect_crc, uint32_t *got_crc) {
+int data_decrypt(const AeadFn &open, const uint8_t key[32], const void *obj, uint64_t olen, void *out,
+                 uint64_t out_cap, uint64_t *out_len, const uint32_t *expect_crc, uint32_t *got_crc) {
     // encrypt.go:196-216; with expect_crc, the object checksum the store kept
     // (checksum.go:55-82) is verified in the same pass over C
-    if (!c || !key || !obj || !out) return JFSX_EINVAL;
+    if (!key || !obj || !out) return JFSX_EINVAL;
     int kl = 0, nl = 0;
     int rc = jfsx_parse_header(obj, olen, &kl, &nl);
     if (rc) return rc;
@@ -1550,7 +1770,7 @@ int jfsx_data_decrypt(jfsx_ctx *c, int algo, const uint8_t key[32], const void *
         segs.resize(4 * nseg_of(len));
         b.crc = segs.data();
     }
-    rc = jfsx_open_batch(c, algo, 1, &b, expect_crc ? JFSX_CRC_GEN | JFSX_CRC_CT : JFSX_CRC_NONE, JFSX_MEM_HOST);
+    rc = open(&b, expect_crc ? JFSX_CRC_GEN | JFSX_CRC_CT : JFSX_CRC_NONE);
     if (rc) return rc;
     if (expect_crc) {
         // the store's read fails first ("verify checksum failed"), before Decrypt sees the bytes
@@ -1563,6 +1783,39 @@ int jfsx_data_decrypt(jfsx_ctx *c, int algo, const uint8_t key[32], const void *
     if (b.status == JFSX_ETAG) return JFSX_ETAG;
     if (out_len) *out_len = len;
     return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int jfsx_data_encrypt(jfsx_ctx *c, int algo, const uint8_t key[32], const uint8_t nonce[12], const uint8_t *wrapped,
+                      int wlen, const void *plaintext, uint64_t len, void *out, uint64_t out_cap, uint64_t *out_len,
+                      uint32_t *obj_crc) {
+    if (!c) return JFSX_EINVAL;
+    return data_encrypt([&](jfsx_blk *b, int m) { return jfsx_seal_batch(c, algo, 1, b, m, JFSX_MEM_HOST); }, algo,
+                        key, nonce, wrapped, wlen, plaintext, len, out, out_cap, out_len, obj_crc);
+}
+
+int jfsx_data_decrypt(jfsx_ctx *c, int algo, const uint8_t key[32], const void *obj, uint64_t olen, void *out,
+                      uint64_t out_cap, uint64_t *out_len, const uint32_t *expect_crc, uint32_t *got_crc) {
+    if (!c || (algo != JFSX_AES256GCM && algo != JFSX_CHACHA20P1305)) return JFSX_EINVAL;
+    return data_decrypt([&](jfsx_blk *b, int m) { return jfsx_open_batch(c, algo, 1, b, m, JFSX_MEM_HOST); }, key,
+                        obj, olen, out, out_cap, out_len, expect_crc, got_crc);
+}
+
+int jfsx_agg_data_encrypt(jfsx_agg *a, int algo, const uint8_t key[32], const uint8_t nonce[12],
+                          const uint8_t *wrapped, int wlen, const void *plaintext, uint64_t len, void *out,
+                          uint64_t out_cap, uint64_t *out_len, uint32_t *obj_crc) {
+    if (!a) return JFSX_EINVAL;
+    return data_encrypt([&](jfsx_blk *b, int m) { return jfsx_agg_seal(a, algo, b, m, JFSX_MEM_HOST); }, algo, key,
+                        nonce, wrapped, wlen, plaintext, len, out, out_cap, out_len, obj_crc);
+}
+
+int jfsx_agg_data_decrypt(jfsx_agg *a, int algo, const uint8_t key[32], const void *obj, uint64_t olen, void *out,
+                          uint64_t out_cap, uint64_t *out_len, const uint32_t *expect_crc, uint32_t *got_crc) {
+    if (!a || (algo != JFSX_AES256GCM && algo != JFSX_CHACHA20P1305)) return JFSX_EINVAL;
+    return data_decrypt([&](jfsx_blk *b, int m) { return jfsx_agg_open(a, algo, b, m, JFSX_MEM_HOST); }, key, obj,
+                        olen, out, out_cap, out_len, expect_crc, got_crc);
 }
 
 int jfsx_gen_synthetic(jfsx_ctx *c, void *dst, uint64_t len, uint64_t seed, uint64_t block) {

@@ -44,6 +44,8 @@ EXPORTS = [
     "jfsx_zstd_decompress_batch", "jfsx_agg_zstd_decompress", "jfsx_mctx_zstd_decompress_batch",
     "jfsx_last_error", "jfsx_zstd_bound", "jfsx_zstd_compress_batch", "jfsx_agg_zstd_compress",
     "jfsx_mctx_zstd_compress_batch", "jfsx_ctx_metrics", "jfsx_pcie_probe",
+    "jfsx_device_numa_node", "jfsx_alloc_pinned_node", "jfsx_host_numa_node",
+    "jfsx_agg_data_encrypt", "jfsx_agg_data_decrypt",
 ]
 
 
@@ -141,6 +143,11 @@ def load_library(path=LIB_PATH):
             "jfsx_ctx_metrics": (I, [P, ctypes.POINTER(jfsx_metrics), I]),
             "jfsx_pcie_probe": (I, [P, U64, ctypes.POINTER(ctypes.c_double)]),
             "jfsx_alloc_pinned": (I, [P, SZ, PP]),
+            "jfsx_device_numa_node": (I, [I, ctypes.POINTER(I)]),
+            "jfsx_alloc_pinned_node": (I, [P, SZ, I, PP]),
+            "jfsx_host_numa_node": (I, [P, SZ, ctypes.POINTER(I)]),
+            "jfsx_agg_data_encrypt": (I, [P, I, P, P, P, I, P, U64, P, U64, ctypes.POINTER(U64), P]),
+            "jfsx_agg_data_decrypt": (I, [P, I, P, P, U64, P, U64, ctypes.POINTER(U64), P, P]),
             "jfsx_free_pinned": (I, [P, P]),
             "jfsx_alloc_device": (I, [P, SZ, PP]),
             "jfsx_free_device": (I, [P, P]),
@@ -252,6 +259,20 @@ def zstd_bound(n):
     return load_library().jfsx_zstd_bound(n)
 
 
+def device_numa_node(device):
+    """jfsx_device_numa_node: the host NUMA node closest to a GPU (-1 unknown)."""
+    v = ctypes.c_int(-1)
+    load_library().jfsx_device_numa_node(device, ctypes.byref(v))
+    return v.value
+
+
+def host_numa_node(ptr, nbytes):
+    """jfsx_host_numa_node: NUMA node of host pages (sampled; -1 unknown, -2 mixed)."""
+    v = ctypes.c_int(-1)
+    load_library().jfsx_host_numa_node(ptr, nbytes, ctypes.byref(v))
+    return v.value
+
+
 def device_count():
     n = ctypes.c_int()
     rc = load_library().jfsx_device_count(ctypes.byref(n))
@@ -312,7 +333,8 @@ class Engine:
 
     def close(self):
         if getattr(self, "ctx", None):
-            self.L.jfsx_ctx_close(self.ctx)
+            if not getattr(self, "_borrowed", False):
+                self.L.jfsx_ctx_close(self.ctx)
             self.ctx = None
 
     def __del__(self):
@@ -355,6 +377,17 @@ class Engine:
 
     def free_pinned(self, ptr):
         self.L.jfsx_free_pinned(self.ctx, ptr)
+
+    def alloc_pinned_node(self, nbytes, node=-1):
+        """Pinned host memory bound to NUMA node `node` (-1: this GPU's node)."""
+        p = ctypes.c_void_p()
+        self._check(self.L.jfsx_alloc_pinned_node(self.ctx, max(nbytes, 16), node, ctypes.byref(p)),
+                    "alloc_pinned_node")
+        return p.value
+
+    def numa_node(self):
+        """Host NUMA node closest to this GPU (-1 unknown)."""
+        return device_numa_node(self.device)
 
     def set_timing(self, on):
         self.L.jfsx_ctx_set_timing(self.ctx, 1 if on else 0)
@@ -652,8 +685,10 @@ class ChecksumError(Exception):
 class MultiEngine:
     """jfsx_mctx: one context per selected GPU (dev_mask bit d = device d, 0 =
     all visible).  Host-memory batches are cut into one contiguous run of
-    blocks per device, balanced by bytes, and run concurrently (SURVEY §8e:
-    independent blocks, no collective)."""
+    blocks per device, balanced by bytes; device-memory batches run each block
+    on the GPU that owns its buffers.  The parts run concurrently on one
+    persistent worker per device (independent blocks, no
+    collective)."""
 
     def __init__(self, dev_mask=0, flags=0):
         self.L = load_library()
@@ -662,10 +697,23 @@ class MultiEngine:
         if rc:
             raise EngineError(rc, "jfsx_mctx_open(0x%x)" % dev_mask)
         self.m = m.value
+        self.devices = [d for d in range(device_count()) if not dev_mask or (dev_mask >> d) & 1]
 
     @property
     def ndev(self):
         return self.L.jfsx_mctx_ndev(self.m)
+
+    def member(self, i):
+        """An Engine view of device slot i's context (owned by the MultiEngine:
+        closing the view does not close the context)."""
+        e = Engine.__new__(Engine)
+        e.L = self.L
+        e.ctx = self.L.jfsx_mctx_ctx(self.m, i)
+        if not e.ctx:
+            raise EngineError(EINVAL, "jfsx_mctx_ctx(%d)" % i)
+        e.device = self.devices[i]
+        e._borrowed = True
+        return e
 
     def close(self):
         if getattr(self, "m", None):
@@ -782,6 +830,31 @@ class Aggregator:
     def zstd_compress(self, z, mem=MEM_HOST):
         """z: a jfsx_zblk, dst_cap >= zstd_bound(src_len)."""
         self.eng._check(self.L.jfsx_agg_zstd_compress(self.h, ctypes.byref(z), mem), "jfsx_agg_zstd_compress")
+
+    def data_encrypt(self, algo, key, nonce, wrapped, plaintext, obj_crc=False):
+        """dataEncryptor.Encrypt through the aggregator (jfsx_agg_data_encrypt):
+        the object bytes, and its object-store CRC32C when obj_crc."""
+        p = _u8(plaintext)
+        w = _u8(wrapped)
+        out = np.empty(3 + w.size + 12 + p.size + 16, np.uint8)
+        olen = ctypes.c_uint64()
+        crc = ctypes.c_uint32()
+        self.eng._check(self.L.jfsx_agg_data_encrypt(self.h, algo, _u8(key).ctypes.data, _u8(nonce).ctypes.data,
+                                                     w.ctypes.data, w.size, p.ctypes.data, p.size, out.ctypes.data,
+                                                     out.size, ctypes.byref(olen),
+                                                     ctypes.byref(crc) if obj_crc else None),
+                        "jfsx_agg_data_encrypt")
+        return (out.tobytes(), crc.value) if obj_crc else out.tobytes()
+
+    def data_decrypt(self, algo, key, obj):
+        """dataEncryptor.Decrypt (after the key unwrap) through the aggregator."""
+        o = _u8(obj)
+        out = np.empty(max(o.size, 1), np.uint8)
+        n = ctypes.c_uint64()
+        self.eng._check(self.L.jfsx_agg_data_decrypt(self.h, algo, _u8(key).ctypes.data, o.ctypes.data, o.size,
+                                                     out.ctypes.data, out.size, ctypes.byref(n), None, None),
+                        "jfsx_agg_data_decrypt")
+        return out[:n.value].tobytes()
 
     def stats(self):
         """(calls, batches, blocks carried by those batches)"""

@@ -58,3 +58,16 @@ def max_over_ranks(dist, x, local=0):
     t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def sum_over_ranks(dist, x, local=0):
+    """Sum of x over the ranks (the whole job's blocks under strong scaling)."""
+    if dist is None:
+        return x
+    import torch
+    dev = "cpu"
+    if dist.get_backend() == "nccl":
+        dev = "cuda:%d" % local
+    t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())

@@ -19,13 +19,17 @@ std::vector<int> h_ops;     // 0 seal, 1 open, 2 crc, 3 lz4 compress, 4 lz4 deco
 std::vector<int> h_modes;
 std::vector<intptr_t> h_ctxs;  // context of each batch
 std::vector<uint64_t> h_first;  // len of the first block of each batch
+std::vector<std::vector<uintptr_t>> h_srcs;  // src pointers of each AEAD batch, in order
 int h_sleep_us = 2000;
 int h_ndev = 4;
 int h_open_ctx = 0;  // contexts opened and not closed
 
-int stub(jfsx_ctx *c, int op, int n, int mode, uint64_t first_len = 0) {
+int stub(jfsx_ctx *c, int op, int n, int mode, uint64_t first_len = 0, const jfsx_blk *b = nullptr) {
     {
         std::lock_guard<std::mutex> g(h_mu);
+        std::vector<uintptr_t> srcs;
+        for (int i = 0; b && i < n; i++) srcs.push_back((uintptr_t)b[i].src);
+        h_srcs.push_back(srcs);
         h_sizes.push_back(n);
         h_ops.push_back(op);
         h_modes.push_back(mode);
@@ -37,14 +41,32 @@ int stub(jfsx_ctx *c, int op, int n, int mode, uint64_t first_len = 0) {
 }
 }  // namespace
 
+// Fake device memory: device d owns [(d+1) << 40, (d+2) << 40); anything
+// below 1 << 40 is host memory.
+namespace jfsx {
+int device_of(const void *p, uintptr_t *lo, uintptr_t *hi) {
+    const uintptr_t a = (uintptr_t)p;
+    if (a < ((uintptr_t)1 << 40)) {
+        *lo = a;
+        *hi = a + 1;
+        return -1;
+    }
+    const int d = (int)(a >> 40) - 1;
+    *lo = (uintptr_t)(d + 1) << 40;
+    *hi = (uintptr_t)(d + 2) << 40;
+    return d;
+}
+}  // namespace jfsx
+
 extern "C" {
 
 // fake transform: tag[i] = key[i] ^ (len >> 8*(i&7)); reserved != 0 -> EINVAL
 int jfsx_seal_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *b, int crc_mode, int mem) {
     for (int i = 0; i < n; i++)
         if (b[i].reserved) return JFSX_EINVAL;
-    if (mem == JFSX_MEM_DEVICE && (intptr_t)c == 0x1300) return JFSX_EIO;  // fake device 3 fails device batches
-    stub(c, 0, n, crc_mode, n ? b[0].len : 0);
+    // fake device 3 fails device batches of 100-byte blocks
+    if (mem == JFSX_MEM_DEVICE && (intptr_t)c == 0x1300 && n && b[0].len == 100) return JFSX_EIO;
+    stub(c, 0, n, crc_mode, n ? b[0].len : 0, b);
     for (int i = 0; i < n; i++) {
         for (int k = 0; k < 16; k++) b[i].tag[k] = b[i].key[k] ^ (uint8_t)(b[i].len >> (8 * (k & 7))) ^ (uint8_t)algo;
         b[i].status = JFSX_OK;
@@ -55,7 +77,7 @@ int jfsx_seal_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *b, int crc_mode, int
 int jfsx_open_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *b, int crc_mode, int mem) {
     for (int i = 0; i < n; i++)
         if (b[i].reserved) return JFSX_EINVAL;
-    stub(c, 1, n, crc_mode, n ? b[0].len : 0);
+    stub(c, 1, n, crc_mode, n ? b[0].len : 0, b);
     for (int i = 0; i < n; i++) {
         bool ok = true;
         for (int k = 0; k < 16; k++)
@@ -133,6 +155,7 @@ int jfsx_ctx_close(jfsx_ctx *) {
 
 void harness_reset(int sleep_us) {
     std::lock_guard<std::mutex> g(h_mu);
+    h_srcs.clear();
     h_sizes.clear();
     h_ops.clear();
     h_modes.clear();
@@ -164,6 +187,15 @@ int harness_batches(int *sizes, int *ops, int *modes, int cap) {
         modes[i] = h_modes[i];
     }
     return n;
+}
+
+// src pointers of AEAD batch `batch` (issue order); returns how many
+int harness_batch_srcs(int batch, uintptr_t *out, int cap) {
+    std::lock_guard<std::mutex> g(h_mu);
+    if (batch < 0 || batch >= (int)h_srcs.size()) return -1;
+    const std::vector<uintptr_t> &v = h_srcs[batch];
+    for (int i = 0; i < (int)v.size() && i < cap; i++) out[i] = v[i];
+    return (int)v.size();
 }
 
 // ctx_close's hook, for the async queue tests

@@ -43,6 +43,7 @@ def H(tmp_path_factory):
         ("harness_set_ndev", None, [I]),
         ("harness_open_ctx", I, []),
         ("harness_batch_devs", I, [P, P, I]),
+        ("harness_batch_srcs", I, [I, P, I]),
         ("jfsx_mctx_open", I, [U64, U32, ctypes.POINTER(P)]),
         ("jfsx_mctx_close", I, [P]),
         ("jfsx_mctx_ndev", I, [P]),
@@ -284,13 +285,14 @@ def test_mctx_open_mask_and_close(H):
     H.harness_set_ndev(4)
 
 
+@pytest.mark.parametrize("ndev", [4, 8])
 @pytest.mark.parametrize("lens", [[4 << 20] * 64, [1000 * (i % 7 + 1) for i in range(37)], [5, 0, 0, 9], [1 << 30]])
-def test_mctx_batch_splits_runs_by_bytes(H, lens):
+def test_mctx_batch_splits_runs_by_bytes(H, lens, ndev):
     """A host batch is cut into contiguous per-device runs balanced by bytes;
     every block is processed exactly once, by one device, and gets its own
-    result."""
+    result (4 and 8 fake devices: the 8-GPU node's split)."""
     H.harness_reset(0)
-    m = mctx(H)
+    m = mctx(H, ndev=ndev)
     n = len(lens)
     arr = (E.jfsx_blk * n)()
     keys = []
@@ -304,9 +306,9 @@ def test_mctx_batch_splits_runs_by_bytes(H, lens):
         assert bytes(arr[i].tag) == fake_tag(keys[i], ln, 1), i
     bd = batch_devs(H)
     sizes = [s for s, _, _ in batches(H)]
-    assert sum(sizes) == n and len(bd) == min(4, n) and len({d for d, _ in bd}) == len(bd)
-    if len(set(lens)) == 1 and n % 4 == 0:
-        assert sizes == [n // 4] * 4  # equal blocks: equal runs
+    assert sum(sizes) == n and len(bd) == min(ndev, n) and len({d for d, _ in bd}) == len(bd)
+    if len(set(lens)) == 1 and n % ndev == 0:
+        assert sizes == [n // ndev] * ndev  # equal blocks: equal runs
     # runs are contiguous and in order: device d's first block follows device d-1's run
     order = sorted(zip([d for d, _ in bd], sizes))
     start = 0
@@ -323,8 +325,9 @@ def test_mctx_batch_splits_runs_by_bytes(H, lens):
         for d, sz in order:
             per[d] = sum(lens[i:i + sz]) + sz
             i += sz
-        assert max(per.values()) <= total / 4 + max(lens) + 1
+        assert max(per.values()) <= total / ndev + max(lens) + 1
     H.jfsx_mctx_close(m)
+    H.harness_set_ndev(4)
 
 
 def test_mctx_errors(H):
@@ -333,8 +336,9 @@ def test_mctx_errors(H):
     arr = (E.jfsx_blk * 8)()
     for i in range(8):
         arr[i].len = 100
-    # device pointers belong to one GPU: a 4-device context refuses MEM_DEVICE
+    # device batches route by ownership: host pointers (here null) have no device
     assert H.jfsx_mctx_seal_batch(m, 0, 8, arr, 0, E.MEM_DEVICE) == E.EINVAL
+    assert batches(H) == []
     assert H.jfsx_mctx_seal_batch(m, 0, 0, arr, 0, E.MEM_HOST) == 0
     # an engine error on one device reaches the caller
     arr[5].reserved = 1
@@ -462,3 +466,133 @@ def test_agg_over_devices_rejects_device_memory(H):
     assert H.jfsx_agg_seal(h, 0, ctypes.byref(b), E.CRC_GEN, E.MEM_DEVICE) == 0
     H.jfsx_agg_free(h)
     H.jfsx_mctx_close(one)
+
+
+def dev_ptr(d, off):
+    """A fake device pointer of device d (tests/harness/agg_host.cpp device_of)."""
+    return ((d + 1) << 40) + off
+
+
+@pytest.mark.parametrize("order", ["grouped", "interleaved"])
+def test_mctx_device_batch_routes_by_owner(H, order):
+    """A device-memory batch on an 8-device context: every block runs on the
+    GPU that owns its buffers (BASELINE configs[1] at 8 GPUs from one process),
+    each device's blocks in the caller's order, in place when they are one run
+    of the array and gathered otherwise; every block gets its own result."""
+    H.harness_reset(0)
+    m = mctx(H, ndev=8)
+    per = 6
+    n = 8 * per
+    arr = (E.jfsx_blk * n)()
+    owner = {}
+    for i in range(n):
+        d = i // per if order == "grouped" else i % 8
+        j = i % per if order == "grouped" else i // 8
+        ctypes.memmove(arr[i].key, bytes([(i * 5 + k) & 255 for k in range(32)]), 32)
+        arr[i].len = 4096 + i
+        arr[i].src = dev_ptr(d, j << 23)
+        arr[i].dst = dev_ptr(d, (j << 23) + (1 << 22))
+        arr[i].crc = dev_ptr(d, (1 << 34) + 512 * j)
+        owner[arr[i].src] = (d, i)
+    assert H.jfsx_mctx_seal_batch(m, 0, n, arr, E.CRC_GEN, E.MEM_DEVICE) == 0
+    for i in range(n):
+        assert bytes(arr[i].tag) == fake_tag(bytes([(i * 5 + k) & 255 for k in range(32)]), 4096 + i, 0), i
+        assert arr[i].src == owner[arr[i].src][1] * 0 + arr[i].src  # the caller's records stay in place
+    bd = batch_devs(H)
+    assert sorted(d for d, _ in bd) == list(range(8))  # one batch per device
+    buf = (ctypes.c_uint64 * 64)()
+    for b, (d, _) in enumerate(bd):
+        k = H.harness_batch_srcs(b, buf, 64)
+        srcs = list(buf[:k])
+        assert k == per and all(owner[p][0] == d for p in srcs)
+        assert [owner[p][1] for p in srcs] == sorted(owner[p][1] for p in srcs)  # caller's order kept
+    H.jfsx_mctx_close(m)
+    H.harness_set_ndev(4)
+
+
+def test_mctx_device_batch_rejects_mixed_or_foreign_buffers(H):
+    H.harness_reset(0)
+    m = mctx(H, mask=0b0110, ndev=8)  # devices 1 and 2
+    arr = (E.jfsx_blk * 2)()
+    for i in range(2):
+        arr[i].len = 64
+        arr[i].src = arr[i].dst = dev_ptr(1 + i, 0)
+    assert H.jfsx_mctx_seal_batch(m, 0, 2, arr, 0, E.MEM_DEVICE) == 0
+    assert sorted(d for d, _ in batch_devs(H)) == [1, 2]
+    arr[1].dst = dev_ptr(1, 4096)  # src on device 2, dst on device 1
+    assert H.jfsx_mctx_seal_batch(m, 0, 2, arr, 0, E.MEM_DEVICE) == E.EINVAL
+    arr[1].dst = arr[1].src = dev_ptr(5, 0)  # device 5 is not in the context
+    assert H.jfsx_mctx_seal_batch(m, 0, 2, arr, 0, E.MEM_DEVICE) == E.EINVAL
+    arr[1].src = arr[1].dst = dev_ptr(2, 0)
+    arr[1].crc = 0x1000  # a host CRC array beside device data
+    assert H.jfsx_mctx_seal_batch(m, 0, 2, arr, E.CRC_GEN, E.MEM_DEVICE) == E.EINVAL
+    # a zero-length block with no buffers runs on the first device
+    H.harness_reset(0)
+    z = (E.jfsx_blk * 1)()
+    assert H.jfsx_mctx_seal_batch(m, 0, 1, z, 0, E.MEM_DEVICE) == 0
+    assert [d for d, _ in batch_devs(H)] == [1]
+    # device ranges route the same way
+    r = (E.jfsx_range * 3)()
+    for i, d in enumerate((2, 1, 2)):
+        r[i].data, r[i].len, r[i].crc = dev_ptr(d, 65536 * i), 32768, dev_ptr(d, 1 << 30)
+    H.harness_reset(0)
+    assert H.jfsx_mctx_crc32c_segments(m, 3, r, E.CRC_GEN, E.MEM_DEVICE) == 0
+    assert sorted(d for d, _ in batch_devs(H)) == [1, 2]
+    H.jfsx_mctx_close(m)
+    H.harness_set_ndev(4)
+
+
+def test_pipelined_seals_run_several_batches_at_once(H):
+    """Host-memory Seal requests pipeline (jfsx_seal_batch keeps several
+    batches in flight): with the engine busy, free dispatchers take what is
+    queued at once, so a 20-caller closed loop (max-uploads,
+    cmd/flags.go:124-128) has several batches running together instead of one
+    batch all callers wait for."""
+    H.harness_reset(5000)
+    h = new_agg(H, max_bytes=4 * 4096, window_us=2000)
+    live, peak = [0], [0]
+    lock = threading.Lock()
+
+    def worker(t):
+        for j in range(6):
+            b, key = mkblk(t * 6 + j, 4096)
+            with lock:
+                live[0] += 1
+            assert H.jfsx_agg_seal(h, 0, ctypes.byref(b), E.CRC_GEN, E.MEM_HOST) == 0
+            with lock:
+                live[0] -= 1
+            assert bytes(b.tag) == fake_tag(key, 4096, 0)
+
+    import time
+    t0 = time.perf_counter()
+    run_threads(20, worker)
+    el = time.perf_counter() - t0
+    calls, nb, blocks = stats(H, h)
+    assert calls == blocks == 120
+    assert max(s for s, _, _ in batches(H)) <= 4
+    # 120 blocks in batches of <= 4 at 5 ms each: >= 30 batches, 150 ms one at a
+    # time; several dispatchers overlap them
+    assert nb >= 30 and el < 0.6 * nb * 0.005, (nb, el)
+    H.jfsx_agg_free(h)
+
+
+def test_serial_ops_keep_one_batch_per_device(H):
+    """Codec and CRC requests hold their context for the whole call, so a
+    device runs one such batch at a time and the requests that arrive
+    meanwhile join the next batch (one wave per object: bigger batches)."""
+    H.harness_reset(20000)
+    h = new_agg(H, window_us=1000)
+    zs = [E.jfsx_zblk() for _ in range(40)]
+    for z in zs:
+        z.src_len, z.dst_cap = 1000, 5000
+
+    def worker(i):
+        if i >= 8:
+            import time
+            time.sleep(0.005)  # arrive while the first batch runs
+        assert H.jfsx_agg_lz4_compress(h, ctypes.byref(zs[i]), E.MEM_HOST) == 0
+
+    run_threads(40, worker)
+    sizes = [s for s, _, _ in batches(H)]
+    assert sum(sizes) == 40 and len(sizes) <= 3, sizes
+    H.jfsx_agg_free(h)

@@ -82,3 +82,40 @@ def test_bench_gpus_2_launches_two_ranks():
     assert rec["n_gpus"] == 2 and rec["dry_run"] is True
     assert rec["last_rank_first_block"] == 5  # rank 1 owns blocks [5, 10)
     assert rec["ms_per_step"] >= 1.0  # rank 1's extra 1 ms: the max over ranks is reported
+
+
+def _bench_dry(args):
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run"] + args, env=env,
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_strong_split_two_ranks():
+    """configs[3] as BASELINE states it: a fixed 2 TiB scan split across the
+    GPUs (--total-gib 2048).  At world 2 (gloo) the ranks' shards are
+    contiguous, disjoint and cover all 524,288 blocks; each rank loops 16x over
+    its 16,384-block resident batch; the line says "strong"."""
+    rec = _bench_dry(["--gpus", "2", "--total-gib", "2048", "--mode", "open"])
+    assert rec["n_gpus"] == 2 and rec["scaling"] == "strong"
+    assert rec["blocks_total"] == 524288 and rec["block_range"] == [0, 524288]
+    assert rec["per_gpu_blocks_max"] == 262144 and rec["last_rank_first_block"] == 262144
+    assert rec["resident_blocks"] == 16384 and rec["loops_per_step"] == 16
+    # an uneven split: 3 ranks would not divide 1000 blocks, 2 do; odd totals still cover every block
+    rec = _bench_dry(["--gpus", "2", "--total-gib", str(1001 * 4 / 1024), "--blocks", "300"])
+    assert rec["blocks_total"] == 1001 and rec["per_gpu_blocks_max"] == 501
+    assert rec["resident_blocks"] == 300 and rec["loops_per_step"] == 2
+
+
+def test_bench_host_pool_is_capped():
+    """Host ingest pins at most --host-pool-gib per GPU (twice: in and out) and
+    loops over it: 64 GiB per GPU through an 8 GiB pool is 8 passes."""
+    rec = _bench_dry(["--mem", "host", "--blocks", "16384", "--host-pool-gib", "8"])
+    assert rec["resident_blocks"] == 2048 and rec["loops_per_step"] == 8
+    rec = _bench_dry(["--gpus", "2", "--mem", "host", "--total-gib", "256", "--host-pool-gib", "8"])
+    assert rec["blocks_total"] == 65536 and rec["resident_blocks"] == 2048 and rec["loops_per_step"] == 16

@@ -260,3 +260,131 @@ def test_lz4_per_block_calls_through_the_aggregator():
         assert calls == 2 * T and batches < calls
     finally:
         eng.close()
+
+
+def _host_block(seed, i, n):
+    p = orc.gen_block(seed, i, n)
+    key, nonce = orc.gen_key(seed, i)
+    c = np.zeros(max(n, 1), np.uint8)
+    cs = np.zeros(4 * max(1, -(-n // E.SEG)), np.uint8)
+    return p, key, nonce, c, cs
+
+
+@pytest.mark.parametrize("algo", [E.AES256GCM, E.CHACHA20P1305])
+def test_host_pipeline_shared_by_concurrent_callers(algo):
+    """jfsx_seal_batch / jfsx_open_batch on host memory share one pipeline of
+    staging slots per context and wait only for their own groups: two callers
+    whose batches each span more groups than there are slots (2 MiB slots),
+    plus 16 one-block callers, all at once, every block bit-exact to the oracle
+    and every CRC array right; then the same through Open."""
+    eng = E.Engine(0)
+    try:
+        eng.set_slot_bytes(2 << 20)
+        rng = np.random.default_rng(algo + 11)
+        big = [[int(x) for x in rng.integers(1, 3 << 20, 24)] for _ in range(2)]
+        small = [int(x) for x in rng.integers(0, 5 << 20, 16)]
+        jobs = [(0, ln) for ln in big] + [(1, [ln]) for ln in small]
+        res = [None] * len(jobs)
+
+        def work(j):
+            _, lens = jobs[j]
+            blocks = [_host_block(900 + j, i, n) for i, n in enumerate(lens)]
+            arr, nb = eng.make_blocks([{"key": k, "nonce": nn, "src": p.ctypes.data if p.size else None,
+                                        "dst": c.ctypes.data, "len": p.size, "crc": cs.ctypes.data}
+                                       for p, k, nn, c, cs in blocks])
+            eng.seal_batch(algo, arr, nb, E.CRC_GEN, E.MEM_HOST)
+            tags = [bytes(arr[i].tag) for i in range(nb)]
+            # and back through Open, in place, verifying the CRCs
+            for i, (p, k, nn, c, cs) in enumerate(blocks):
+                arr[i].src = arr[i].dst = c.ctypes.data
+                ctypes.memmove(arr[i].tag, tags[i], 16)
+            eng.open_batch(algo, arr, nb, E.CRC_VERIFY, E.MEM_HOST)
+            res[j] = (blocks, tags, [arr[i].status for i in range(nb)])
+
+        run_threads(len(jobs), work)
+        for blocks, tags, st in res:
+            for (p, k, nn, c, cs), tag, s in zip(blocks, tags, st):
+                ct, etag = orc.seal(ORC[algo], k, nn, p, fast=True)
+                assert tag == etag and s == E.OK
+                assert c[:p.size].tobytes() == p.tobytes()  # opened in place: the plaintext again
+                assert cs.tobytes() == orc.checksum(p, hw=True)
+    finally:
+        eng.close()
+
+
+def test_agg_data_encrypt_equals_data_encrypt(eng):
+    """jfsx_agg_data_encrypt / _decrypt (dataEncryptor.Encrypt / Decrypt through
+    the aggregator, encrypt.go:164-216) write the same object bytes and object
+    checksum as the one-call form, from 20 threads."""
+    wrapped = bytes(range(256))
+    lens = [0, 1, 4 << 20, 100003, 32768] + [(i * 98765) % (1 << 20) for i in range(15)]
+    got = [None] * len(lens)
+    with E.Aggregator(eng, window_us=500, max_bytes=16 << 20) as agg:
+        def work(i):
+            p = orc.gen_block(71, i, lens[i]).tobytes()
+            key, nonce = orc.gen_key(71, i)
+            obj, crc = agg.data_encrypt(E.AES256GCM, key, nonce, wrapped, p, obj_crc=True)
+            back = agg.data_decrypt(E.AES256GCM, key, obj)
+            got[i] = (p, key, nonce, obj, crc, back)
+        run_threads(len(lens), work)
+    for p, key, nonce, obj, crc, back in got:
+        assert (obj, crc) == eng.data_encrypt(E.AES256GCM, key, nonce, wrapped, p, obj_crc=True)
+        assert back == p
+
+
+def test_multi_device_context_device_batch():
+    """A device-memory batch on a multi-device context runs each block on the
+    GPU that owns its buffers (here every visible GPU's own blocks), bit-exact
+    to the oracle; device memory of another process-local context routes too."""
+    m = E.MultiEngine(0)
+    try:
+        specs, keep = [], []
+        for d in range(m.ndev):
+            mem = m.member(d)
+            for i, n in enumerate([4 << 20, 12345, 0, 65536]):
+                gi = 10 * d + i
+                p = orc.gen_block(77, gi, n)
+                src, dst = mem.alloc(max(n, 16)), mem.alloc(max(n, 16))
+                if n:
+                    src.upload(p)
+                crc = mem.alloc(4 * max(1, -(-n // E.SEG)))
+                key, nonce = orc.gen_key(77, gi)
+                specs.append({"key": key, "nonce": nonce, "src": src.ptr, "dst": dst.ptr, "len": n, "crc": crc.ptr})
+                keep.append((p, key, nonce, src, dst, crc, mem))
+        arr, nb = E.Engine.make_blocks(specs)
+        m.seal_batch(E.AES256GCM, arr, nb, E.CRC_GEN, E.MEM_DEVICE)
+        for i, (p, key, nonce, src, dst, crc, mem) in enumerate(keep):
+            c, tag = orc.seal(orc.AES256GCM, key, nonce, p, fast=True)
+            assert bytes(arr[i].tag) == tag and dst.download(p.size).tobytes() == c, i
+            assert crc.download().tobytes()[:len(orc.checksum(p))] == orc.checksum(p)
+        for k in keep:
+            for b in k[3:6]:
+                b.free()
+    finally:
+        m.close()
+
+
+def test_pinned_staging_on_the_gpu_numa_node(eng):
+    """jfsx_alloc_pinned_node places the staging pages on the GPU's NUMA node
+    (when the process may use that node), and the placement is reported."""
+    node = eng.numa_node()
+    nbytes = 256 << 20
+    p = eng.alloc_pinned_node(nbytes)
+    try:
+        got = E.host_numa_node(p, nbytes)
+        assert got != -2  # one node for the whole pool
+        allowed = ""
+        for line in open("/proc/self/status"):
+            if line.startswith("Mems_allowed_list"):
+                allowed = line.split(":", 1)[1].strip()
+        nodes = set()
+        for part in allowed.split(","):
+            if "-" in part:
+                a, b = part.split("-")
+                nodes |= set(range(int(a), int(b) + 1))
+            elif part:
+                nodes.add(int(part))
+        if node >= 0 and node in nodes and got >= 0:
+            assert got == node, (got, node, allowed)
+    finally:
+        eng.free_pinned(p)
