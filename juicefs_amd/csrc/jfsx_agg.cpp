@@ -181,7 +181,12 @@ struct Req {
     uint64_t bytes;
     Clock::time_point t0;
     int rc = 0;
-    bool done = false;
+    // completion: each caller sleeps on its own condition variable, so a
+    // finished batch wakes only its own callers (not every waiting caller,
+    // which would contend on the queue lock the dispatchers need)
+    std::mutex m;
+    std::condition_variable cv;
+    bool fin = false;
     bool same(const Req &o) const { return op == o.op && algo == o.algo && mode == o.mode && mem == o.mem; }
 };
 
@@ -203,7 +208,7 @@ struct jfsx_agg {
     uint64_t max_bytes;
     std::chrono::microseconds window;
     std::mutex mu;
-    std::condition_variable cv_work, cv_done;
+    std::condition_variable cv_work;
     std::deque<Req *> q;
     bool stop = false;
     int busy = 0;             // dispatchers running a pipelined batch
@@ -295,9 +300,9 @@ struct jfsx_agg {
             }
             std::vector<Req *> b;
             bytes = 0;
-            const Req h = *head;
+            const Req *h = head;  // still alive: its caller waits until the batch is done
             for (auto it = q.begin(); it != q.end() && (int)b.size() < max_blocks;) {
-                if ((*it)->same(h) && (b.empty() || bytes + (*it)->bytes <= max_bytes)) {
+                if ((*it)->same(*h) && (b.empty() || bytes + (*it)->bytes <= max_bytes)) {
                     bytes += (*it)->bytes;
                     b.push_back(*it);
                     it = q.erase(it);
@@ -310,25 +315,31 @@ struct jfsx_agg {
             if (!q.empty()) cv_work.notify_all();  // the rest may go to an idle dispatcher now
             lk.unlock();
             execute(cs[k], b);
+            for (Req *r : b) {
+                std::lock_guard<std::mutex> g(r->m);  // r may be gone once fin is seen: notify under its lock
+                r->fin = true;
+                r->cv.notify_one();
+            }
             lk.lock();
             held--;
             batches++;
             dev_batches[dev[k]]++;
             blocks += b.size();
-            for (Req *r : b) r->done = true;
-            cv_done.notify_all();
             if (!q.empty()) cv_work.notify_all();
         }
     }
 
     int submit(Req &r) {
-        std::unique_lock<std::mutex> lk(mu);
-        if (stop) return JFSX_EINVAL;
-        r.t0 = Clock::now();
-        q.push_back(&r);
-        calls++;
-        cv_work.notify_one();
-        cv_done.wait(lk, [&] { return r.done; });
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            if (stop) return JFSX_EINVAL;
+            r.t0 = Clock::now();
+            q.push_back(&r);
+            calls++;
+            cv_work.notify_one();
+        }
+        std::unique_lock<std::mutex> l2(r.m);
+        r.cv.wait(l2, [&] { return r.fin; });
         return r.rc;
     }
 };

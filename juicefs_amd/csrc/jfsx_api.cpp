@@ -251,6 +251,10 @@ struct jfsx_ctx {
     hipEvent_t ev_k0[kRing] = {}, ev_k1[kRing] = {};  // main-kernel timing of the synchronous paths
     PipeSlot pipe[kPipe];
     int pipe_next = 0;  // next pipeline slot (under mu)
+    // JFSX_PIPE_STATS=1: where host batches spend their time, printed at close
+    // (groups, us enqueueing under mu, us waiting for a busy slot, us waiting
+    // for one's own groups)
+    std::atomic<uint64_t> ps_groups{0}, ps_enq_us{0}, ps_slot_us{0}, ps_own_us{0};
     std::mutex stat_mu; // met, ms_total, launches
     std::atomic<size_t> slot_bytes{(size_t)256 << 20};
     int ncu = 256;  // compute units: persistent transform kernels launch one workgroup per CU
@@ -769,14 +773,23 @@ int run_aead_host(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int c
     std::vector<jfsx_blk> dv(blks, blks + n);
     std::vector<PipeGroup> recs(groups.size());
     size_t issued = 0;
+    using SClock = std::chrono::steady_clock;
+    auto us = [](SClock::time_point a, SClock::time_point b) {
+        return (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(b - a).count();
+    };
     for (size_t g = 0; g < groups.size() && !rc; g++) {
         std::lock_guard<std::mutex> lk(c->mu);
         PipeSlot &s = c->pipe[c->pipe_next];
         c->pipe_next = (c->pipe_next + 1) % kPipe;
         std::lock_guard<std::mutex> sl(s.mu);
+        const SClock::time_point t0 = SClock::now();
         pipe_collect(c, s);
+        const SClock::time_point t1 = SClock::now();
         const int b0 = groups[g].first, b1 = groups[g].second;
         rc = pipe_enqueue(c, s, algo, open, b1 - b0, blks + b0, dv.data() + b0, crc_mode);
+        c->ps_slot_us += us(t0, t1);
+        c->ps_enq_us += us(t1, SClock::now());
+        c->ps_groups++;
         if (rc) {
             (void)hipStreamSynchronize(c->s_in);
             (void)hipStreamSynchronize(c->stream);
@@ -792,12 +805,14 @@ int run_aead_host(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int c
         s.owner = &recs[g];
         issued++;
     }
+    const SClock::time_point tw = SClock::now();
     for (size_t g = 0; g < issued; g++) {
         PipeSlot &s = *recs[g].slot;
         std::lock_guard<std::mutex> sl(s.mu);
         if (s.owner == &recs[g]) pipe_collect(c, s);
         if (recs[g].rc && !rc) rc = recs[g].rc;
     }
+    c->ps_own_us += us(tw, SClock::now());
     if (rc) return rc;
     for (int i = 0; i < n; i++) {
         blks[i].status = dv[i].status;
@@ -947,6 +962,11 @@ int run_codec(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, CodecOp op) {
     int zd_waves = op == kZstdDecomp && !zd_serial ? zstd_par_waves(n, c->ncu) : 0;
     if (zd_waves) zd_waves = (int)std::min<size_t>((size_t)zd_waves, std::max<size_t>(c->zstd_arena_budget / kZstdArena, 1));
     const size_t o_out = align256(sizeof(ZDev) * n), o_tab = o_out + align256(sizeof(ZOut) * n);
+    ErrRec before;  // a hipMalloc failure the arena fallback recovers from is not recorded
+    {
+        std::lock_guard<std::mutex> g(c->err_mu);
+        before = c->err;
+    }
     for (;;) {
         size_t extra = 0;
         if (op == kLz4Comp) extra = kLz4TabBytes * (size_t)n;
@@ -956,6 +976,10 @@ int run_codec(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, CodecOp op) {
         if (rc != JFSX_ENOMEM || op != kZstdDecomp || zd_waves == 0) break;
         zd_waves = zd_waves > c->ncu ? std::max(zd_waves / 2, c->ncu) : 0;  // fewer waves, then serial
         (void)hipGetLastError();  // the failed hipMalloc is not this batch's error
+        {
+            std::lock_guard<std::mutex> g(c->err_mu);
+            c->err = before;
+        }
     }
     if (rc) return rc;
     if ((rc = ensure_host(&w.h, &w.hcap, o_tab))) return rc;  // descriptors and results only
@@ -1158,6 +1182,11 @@ int jfsx_ctx_open(int device, uint32_t flags, jfsx_ctx **out) {
 
 int jfsx_ctx_close(jfsx_ctx *c) {
     if (!c) return JFSX_EINVAL;
+    if (getenv("JFSX_PIPE_STATS") && c->ps_groups)
+        fprintf(stderr, "jfsx pipe stats (device %d): %llu groups, enqueue %.1f us/group, slot wait %.1f us/group, "
+                "own wait %.1f us/group\n", c->device, (unsigned long long)c->ps_groups.load(),
+                c->ps_enq_us.load() / (double)c->ps_groups, c->ps_slot_us.load() / (double)c->ps_groups,
+                c->ps_own_us.load() / (double)c->ps_groups);
     async_detach(c);  // queued _async batches run first (jfsx_agg.cpp)
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();

@@ -12,8 +12,24 @@
 //
 // Host/device portable: the includer defines JFSX_HD.  Every function is
 // pinned on the CPU by tests/test_rsa.py against libcrypto's RSA-OAEP.
+//
+// Constant time with respect to the private key and the decrypted message,
+// as Go's rsa.DecryptOAEP is (crypto/internal/bigmod, subtle.ConstantTime*):
+// the exponentiation runs a fixed 4-bit window over the full 1024-bit
+// exponent length, always multiplies (digit 0 multiplies by the Montgomery
+// one), and reads its window table by a masked scan of all 16 entries; the
+// modular corrections, the CRT recombination and the OAEP checks select with
+// masks instead of branching.  Branches remain only on public values: the
+// ciphertext length and c >= n (Go rejects both before the private
+// operation), and the final valid / invalid outcome.
 #pragma once
 #include <stdint.h>
+
+// test hook: the host harness records every Montgomery product and every
+// window-table read to check that the sequence does not depend on the exponent
+#ifndef JFSX_RSA_TRACE
+#define JFSX_RSA_TRACE(tag, v) ((void)0)
+#endif
 
 namespace jfsx_rsa {
 
@@ -60,8 +76,40 @@ JFSX_HD uint32_t add_in(uint32_t *a, const uint32_t *b, int n) {
     return (uint32_t)c;
 }
 
+// all-ones if x != 0, else 0 (no branch)
+JFSX_HD uint32_t ct_nz(uint32_t x) { return 0u - ((x | (0u - x)) >> 31); }
+
+// a >= b as an all-ones / zero mask, over all n limbs (no early exit)
+JFSX_HD uint32_t ct_geq(const uint32_t *a, const uint32_t *b, int n) {
+    uint64_t br = 0;
+    for (int i = 0; i < n; i++) br = (((uint64_t)a[i] - b[i] - br) >> 32) & 1u;
+    return (uint32_t)br - 1u;  // no borrow: a >= b
+}
+
+// a = mask ? a - b : a, over n limbs; returns the borrow of a - b
+JFSX_HD uint32_t ct_sub_if(uint32_t *a, const uint32_t *b, int n, uint32_t mask) {
+    uint64_t br = 0;
+    for (int i = 0; i < n; i++) {
+        const uint64_t d = (uint64_t)a[i] - b[i] - br;
+        br = (d >> 32) & 1u;
+        a[i] = (a[i] & ~mask) | ((uint32_t)d & mask);
+    }
+    return (uint32_t)br;
+}
+
+// a += mask & b over n limbs
+JFSX_HD void ct_add_if(uint32_t *a, const uint32_t *b, int n, uint32_t mask) {
+    uint64_t c = 0;
+    for (int i = 0; i < n; i++) {
+        c += (uint64_t)a[i] + (b[i] & mask);
+        a[i] = (uint32_t)c;
+        c >>= 32;
+    }
+}
+
 // out = a b R^-1 mod m (R = 2^1024), a, b < m; CIOS with one final subtract
 JFSX_HD void mont_mul(const uint32_t *a, const uint32_t *b, const uint32_t *m, uint32_t minv, uint32_t *out) {
+    JFSX_RSA_TRACE('M', 0);
     uint32_t t[kLimbs + 2];
 #pragma unroll
     for (int j = 0; j < kLimbs + 2; j++) t[j] = 0;
@@ -214,21 +262,27 @@ JFSX_HD void mgf1_xor(const uint8_t *seed, int slen, uint8_t *dst, int len) {
 
 // EME-OAEP decode (RFC 8017 7.1.2 step 3) of em[0..k), lhash = SHA-256(label).
 // Returns the message length and moves the message to em[0..len), or -1
-// ("crypto/rsa: decryption error").  Branches depend on the data; the GPU
-// batch is not a constant-time implementation (documented in DESIGN.md).
+// ("crypto/rsa: decryption error").  As Go's decryptOAEP: the leading zero
+// byte, the label hash and the 0x01 separator are checked without branching
+// on the data (the separator by a masked scan of the whole of DB), and one
+// combined valid / invalid outcome is branched on at the end.
 JFSX_HD int oaep_decode(uint8_t *em, int k, const uint8_t lhash[32]) {
     uint8_t *seed = em + 1, *db = em + 1 + kHash;
     const int dblen = k - kHash - 1;
     mgf1_xor(db, dblen, seed, kHash);
     mgf1_xor(seed, kHash, db, dblen);
-    int bad = em[0] != 0;
-    for (int i = 0; i < kHash; i++) bad |= db[i] != lhash[i];
-    int i = kHash;
-    while (i < dblen && db[i] == 0) i++;
-    if (i >= dblen || db[i] != 1) bad = 1;
-    if (bad) return -1;
-    const int mlen = dblen - i - 1;
-    for (int j = 0; j < mlen; j++) em[j] = db[i + 1 + j];
+    uint32_t bad = ct_nz(em[0]);
+    for (int i = 0; i < kHash; i++) bad |= ct_nz((uint32_t)(db[i] ^ lhash[i]));
+    uint32_t looking = ~0u, index = 0, invalid = 0;
+    for (int i = kHash; i < dblen; i++) {
+        const uint32_t is0 = ~ct_nz(db[i]), is1 = ~ct_nz((uint32_t)db[i] ^ 1u);
+        index = (index & ~(looking & is1)) | ((uint32_t)i & looking & is1);
+        invalid |= looking & ~is0 & ~is1;
+        looking &= ~is1;
+    }
+    if (bad | invalid | looking) return -1;
+    const int mlen = dblen - (int)index - 1;
+    for (int j = 0; j < mlen; j++) em[j] = db[index + 1 + j];
     return mlen;
 }
 
@@ -291,22 +345,46 @@ JFSX_HD void reduce_2048(const uint32_t *c, const uint32_t *m, uint32_t minv, co
     uint32_t t[kLimbs + 1];
     mont_mul(c + kLimbs, r2, m, minv, t);  // hi R mod m (hi < R, r2 < m: CIOS bound holds)
     t[kLimbs] = add_in(t, c, kLimbs);      // + lo: < 3m since lo < R < 2m
-    for (int rep = 0; rep < 2; rep++)
-        if (t[kLimbs] || geq(t, m, kLimbs)) t[kLimbs] -= sub_in(t, m, kLimbs);
+    for (int rep = 0; rep < 2; rep++) {     // two masked corrections, always both
+        const uint32_t ge = ct_nz(t[kLimbs]) | ct_geq(t, m, kLimbs);
+        t[kLimbs] -= ct_sub_if(t, m, kLimbs, ge) & ge;
+    }
     for (int j = 0; j < kLimbs; j++) out[j] = t[j];
 }
 
-// x^e mod m, left to right over the e_bits bits of e (x < m)
+// The fixed-window schedule both exponentiations follow: kDigits 4-bit
+// digits of the exponent zero-extended to the prime's length, top first; per
+// digit four squarings and one multiply by tab[digit] (tab[0] = the
+// Montgomery one), whatever the digit.
+constexpr int kDigits = 8 * kLimbs;
+JFSX_HD uint32_t exp_digit(const uint32_t *e, int d) { return (e[d >> 3] >> (4 * (d & 7))) & 15u; }
+
+// b = tab[idx] by reading every entry and keeping the one whose index matches
+// (mask), so the addresses touched do not depend on idx
+JFSX_HD void ct_select16(const uint32_t (*tab)[kLimbs], uint32_t idx, uint32_t *b) {
+    for (int j = 0; j < kLimbs; j++) b[j] = 0;
+    for (uint32_t w = 0; w < 16; w++) {
+        const uint32_t m = ~ct_nz(w ^ idx);
+        JFSX_RSA_TRACE('S', w);
+        for (int j = 0; j < kLimbs; j++) b[j] |= tab[w][j] & m;
+    }
+}
+
+// x^e mod m (x < m) on the fixed schedule above; constant time in e
 JFSX_HD void mod_exp(const uint32_t *x, const uint32_t *e, int e_bits, const uint32_t *m, uint32_t minv,
                      const uint32_t *r2, uint32_t *out) {
-    uint32_t xm[kLimbs], acc[kLimbs], one[kLimbs];
-    mont_mul(x, r2, m, minv, xm);  // x R mod m
-    for (int j = 0; j < kLimbs; j++) acc[j] = xm[j];
-    for (int b = e_bits - 2; b >= 0; b--) {
-        mont_mul(acc, acc, m, minv, acc);
-        if ((e[b >> 5] >> (b & 31)) & 1u) mont_mul(acc, xm, m, minv, acc);
-    }
+    (void)e_bits;  // the schedule covers the full length whatever the exponent's bit length
+    uint32_t tab[16][kLimbs], acc[kLimbs], b[kLimbs], one[kLimbs];
     for (int j = 0; j < kLimbs; j++) one[j] = j == 0;
+    mont_mul(r2, one, m, minv, tab[0]);  // R mod m: the Montgomery one
+    mont_mul(x, r2, m, minv, tab[1]);    // x R mod m
+    for (int w = 2; w < 16; w++) mont_mul(tab[w - 1], tab[1], m, minv, tab[w]);
+    for (int j = 0; j < kLimbs; j++) acc[j] = tab[0][j];
+    for (int d = kDigits - 1; d >= 0; d--) {
+        for (int sq = 0; sq < 4; sq++) mont_mul(acc, acc, m, minv, acc);
+        ct_select16(tab, exp_digit(e, d), b);
+        mont_mul(acc, b, m, minv, acc);
+    }
     mont_mul(acc, one, m, minv, out);  // leave the Montgomery domain
 }
 
@@ -315,20 +393,21 @@ JFSX_HD void crt(const Key &k, const uint32_t *m1, const uint32_t *m2, uint32_t 
     uint32_t t[kLimbs + 1], h[kLimbs], u[kLimbs];
     for (int j = 0; j < kLimbs; j++) t[j] = m2[j];
     t[kLimbs] = 0;
-    if (geq(t, k.p, kLimbs)) sub_in(t, k.p, kLimbs);  // m2 < q < 2p
+    ct_sub_if(t, k.p, kLimbs, ct_geq(t, k.p, kLimbs));  // m2 < q < 2p
     for (int j = 0; j < kLimbs; j++) u[j] = m1[j];
-    if (sub_in(u, t, kLimbs)) add_in(u, k.p, kLimbs);  // (m1 - m2) mod p
+    const uint32_t neg = 0u - sub_in(u, t, kLimbs);     // (m1 - m2) mod p
+    ct_add_if(u, k.p, kLimbs, neg);
     mont_mul(u, k.qinv, k.p, k.pinv, h);               // u qinv R^-1
     mont_mul(h, k.r2p, k.p, k.pinv, h);                // u qinv
     for (int j = 0; j < 2 * kLimbs; j++) m[j] = j < kLimbs ? m2[j] : 0;
-    for (int i = 0; i < kLimbs; i++) {  // m += h q
+    for (int i = 0; i < kLimbs; i++) {  // m += h q, carries run to the top every time
         uint64_t c = 0;
         for (int j = 0; j < kLimbs; j++) {
             c = (uint64_t)h[i] * k.q[j] + (c + m[i + j]);
             m[i + j] = (uint32_t)c;
             c >>= 32;
         }
-        for (int j = i + kLimbs; j < 2 * kLimbs && c; j++) {
+        for (int j = i + kLimbs; j < 2 * kLimbs; j++) {
             c += m[j];
             m[j] = (uint32_t)c;
             c >>= 32;

@@ -5,14 +5,15 @@
 // ~0.35 ms per core, which caps end-to-end Decrypt far below the Open kernel.
 // Here one batch unwraps every object key of a read window on the GPU:
 //   * rsa_half_k: one thread per (object, CRT half): c mod p_h, then
-//     c^d_h mod p_h by left-to-right Montgomery exponentiation (32-limb CIOS,
-//     jfsx_rsa.h).  The key is wave-uniform (scalar loads); the exponent bits
-//     are uniform branches.
+//     c^d_h mod p_h by a fixed-window Montgomery exponentiation (32-limb CIOS,
+//     jfsx_rsa.h), constant time in the exponent.
 //   * rsa_finish_k: one thread per object: c < n check, CRT recombination,
 //     EME-OAEP decoding (SHA-256, MGF1, label hash), message out.
-// Bit-exact to rsa.DecryptOAEP(sha256, ..., "keys"); not constant-time (the
-// data-dependent OAEP checks branch) -- the batch runs on the GPU the key
-// owner controls, as the host path does.
+// Bit-exact to rsa.DecryptOAEP(sha256, ..., "keys") and, like it, constant
+// time with respect to the private key and the decrypted data (jfsx_rsa.h):
+// no branch and no memory address depends on the exponent, the CRT values or
+// the OAEP checks; the one branch on secret-derived data is the final valid /
+// invalid outcome, which Go's decryptOAEP also returns as an error.
 #include "jfsx_internal.h"
 
 #define JFSX_HD __device__ __forceinline__
@@ -23,84 +24,65 @@ namespace jfsx {
 using jfsx_rsa::kLimbs;
 using jfsx_rsa::kModBytes;
 
-// x^e mod m, left to right with a fixed 4-bit window: x^1..x^15 (Montgomery
-// domain) in private memory, then per digit four squarings and one multiply
-// by the digit's power (none for a zero digit) -- about 1275 products for a
-// 1024-bit exponent instead of 1535 bit by bit.  One Montgomery multiply site
-// in the loop: the unrolled CIOS is ~6K instructions, and one copy keeps the
-// loop inside the instruction cache.  The exponent (the key's) is wave-uniform,
-// so every branch is.
-#ifndef JFSX_RSA_WIN
-#define JFSX_RSA_WIN 1  // 0: bit by bit (A/B)
-#endif
-__device__ __forceinline__ uint32_t exp_digit(const uint32_t *e, int d) { return (e[d >> 3] >> (4 * (d & 7))) & 15u; }
-
-__device__ __forceinline__ void mod_exp_1site(const uint32_t *x, const uint32_t *e, int e_bits, const uint32_t *m,
-                                              uint32_t minv, const uint32_t *r2, uint32_t *out) {
-#if JFSX_RSA_WIN
-    uint32_t tab[16][kLimbs];  // tab[j] = x^j R mod m, j >= 1
+// x^e mod m on jfsx_rsa.h's constant-time schedule (kDigits fixed 4-bit
+// digits over the full prime length, four squarings and one multiply per
+// digit, the window entry picked by a masked scan of all 16), with one
+// Montgomery multiply site: the unrolled CIOS is ~6K instructions, and one
+// copy keeps the loop inside the instruction cache.  The step sequence is a
+// function of the step counter alone; the exponent only feeds the masks,
+// which pass through a register barrier so the compiler cannot turn them
+// back into a secret-dependent branch or a secret-indexed load.
+__device__ __forceinline__ void mod_exp_ct(const uint32_t *x, const uint32_t *e, const uint32_t *m, uint32_t minv,
+                                           const uint32_t *r2, uint32_t *out) {
+    using jfsx_rsa::kDigits;
+    uint32_t tab[16][kLimbs];  // tab[j] = x^j R mod m
     uint32_t acc[kLimbs], b[kLimbs];
-    jfsx_rsa::mont_mul(x, r2, m, minv, acc);  // to the Montgomery domain
+    constexpr int kTab = 16, kMain = kTab + 5 * kDigits;  // steps: table, digits, leave the domain
+#pragma unroll 1
+    for (int st = 0; st <= kMain; st++) {
+        if (st == 0) {  // R mod m = r2 * 1
 #pragma unroll
-    for (int j = 0; j < kLimbs; j++) tab[1][j] = acc[j];
-    const int ndig = (e_bits + 3) / 4;  // the top digit holds the top set bit: nonzero
-    int k = 2;                          // phase 0: tab[k] = tab[k - 1] * x
-    int d = ndig - 1, phase = 0, nsq = 0;
-    for (;;) {
-        const uint32_t bi = phase == 0 ? 1u : phase == 2 ? exp_digit(e, d) : 0u;
-        if (phase == 1) {
+            for (int j = 0; j < kLimbs; j++) acc[j] = r2[j], b[j] = j == 0;
+        } else if (st == 1) {  // x R mod m
 #pragma unroll
-            for (int j = 0; j < kLimbs; j++) b[j] = acc[j];
-        } else {
+            for (int j = 0; j < kLimbs; j++) acc[j] = x[j], b[j] = r2[j];
+        } else if (st < kTab) {  // tab[st] = tab[st - 1] * x R
 #pragma unroll
-            for (int j = 0; j < kLimbs; j++) b[j] = tab[bi][j];
-        }
-        jfsx_rsa::mont_mul(acc, b, m, minv, acc);
-        if (phase == 0) {
+            for (int j = 0; j < kLimbs; j++) b[j] = tab[1][j];
+        } else if (st < kMain) {
+            const int r = st - kTab;
+            if (r % 5 < 4) {
 #pragma unroll
-            for (int j = 0; j < kLimbs; j++) tab[k][j] = acc[j];
-            if (++k < 16) continue;
-            const uint32_t top = exp_digit(e, ndig - 1);
-#pragma unroll
-            for (int j = 0; j < kLimbs; j++) acc[j] = tab[top][j];
-            if (--d < 0) break;
-            phase = 1, nsq = 4;
-        } else if (phase == 1) {
-            if (--nsq) continue;
-            if (exp_digit(e, d)) {
-                phase = 2;
+                for (int j = 0; j < kLimbs; j++) b[j] = acc[j];
             } else {
-                if (--d < 0) break;
-                nsq = 4;
+                uint32_t idx = jfsx_rsa::exp_digit(e, kDigits - 1 - r / 5);
+                asm volatile("" : "+v"(idx));
+#pragma unroll
+                for (int j = 0; j < kLimbs; j++) b[j] = 0;
+#pragma unroll
+                for (uint32_t w = 0; w < 16; w++) {
+                    uint32_t msk = ~jfsx_rsa::ct_nz(w ^ idx);
+                    asm volatile("" : "+v"(msk));
+#pragma unroll
+                    for (int j = 0; j < kLimbs; j++) b[j] |= tab[w][j] & msk;
+                }
             }
-        } else {
-            if (--d < 0) break;
-            phase = 1, nsq = 4;
+        } else {  // out of the Montgomery domain
+#pragma unroll
+            for (int j = 0; j < kLimbs; j++) b[j] = j == 0;
         }
-    }
-#else
-    uint32_t xm[kLimbs], acc[kLimbs], b[kLimbs];
-    jfsx_rsa::mont_mul(x, r2, m, minv, xm);  // to the Montgomery domain
-#pragma unroll
-    for (int j = 0; j < kLimbs; j++) acc[j] = xm[j];
-    int bit = e_bits - 2;
-    bool mul = false;  // a multiply by x is pending for the bit just squared in
-    while (bit >= 0 || mul) {
-        const bool do_mul = mul;  // wave-uniform
-#pragma unroll
-        for (int j = 0; j < kLimbs; j++) b[j] = do_mul ? xm[j] : acc[j];
         jfsx_rsa::mont_mul(acc, b, m, minv, acc);
-        if (do_mul) {
-            mul = false;
-        } else {
-            mul = (e[bit >> 5] >> (bit & 31)) & 1u;
-            bit--;
+        if (st < kTab) {
+#pragma unroll
+            for (int j = 0; j < kLimbs; j++) tab[st][j] = acc[j];
+            if (st == kTab - 1) {
+#pragma unroll
+                for (int j = 0; j < kLimbs; j++) acc[j] = tab[0][j];
+            }
         }
     }
-#endif
 #pragma unroll
-    for (int j = 0; j < kLimbs; j++) b[j] = j == 0;
-    jfsx_rsa::mont_mul(acc, b, m, minv, out);  // out of the Montgomery domain
+    for (int j = 0; j < kLimbs; j++) out[j] = acc[j];
 }
 
 __global__ __launch_bounds__(64) void rsa_half_k(const jfsx_rsa::Key *__restrict__ key, int n,
@@ -113,10 +95,10 @@ __global__ __launch_bounds__(64) void rsa_half_k(const jfsx_rsa::Key *__restrict
     jfsx_rsa::from_be(ct + (size_t)kModBytes * i, kModBytes, c, 2 * kLimbs);
     if (half == 0) {
         jfsx_rsa::reduce_2048(c, k.p, k.pinv, k.r2p, x);
-        mod_exp_1site(x, k.dp, k.dp_bits, k.p, k.pinv, k.r2p, r);
+        mod_exp_ct(x, k.dp, k.p, k.pinv, k.r2p, r);
     } else {
         jfsx_rsa::reduce_2048(c, k.q, k.qinv32, k.r2q, x);
-        mod_exp_1site(x, k.dq, k.dq_bits, k.q, k.qinv32, k.r2q, r);
+        mod_exp_ct(x, k.dq, k.q, k.qinv32, k.r2q, r);
     }
     uint32_t *o = mh + ((size_t)half * n + i) * kLimbs;
 #pragma unroll

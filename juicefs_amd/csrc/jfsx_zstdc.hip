@@ -242,9 +242,15 @@ struct ZExt {
 __device__ __forceinline__ void zx_load(ZExt &X, const ZImg &I, int32_t m) {
     const int32_t o = ((m + (int32_t)I.sh) & ~3) - 4;
     X.in = o >= 0 && o + 24 <= (int32_t)(I.n + I.sh);
-    const uint8_t *a = I.al + (X.in ? o : 0);
-    const zv4u v = *(__attribute__((address_space(1))) const zv4u *)a;
-    const zv2u w = *(__attribute__((address_space(1))) const zv2u *)(a + 16);
+    // lanes whose 24 bytes are not inside the image load nothing (an object
+    // shorter than 24 bytes has no in-bounds 24-byte window at all)
+    zv4u v = {0u, 0u, 0u, 0u};
+    zv2u w = {0u, 0u};
+    if (X.in) {
+        const uint8_t *a = I.al + o;
+        v = *(__attribute__((address_space(1))) const zv4u *)a;
+        w = *(__attribute__((address_space(1))) const zv2u *)(a + 16);
+    }
     X.e[0] = v.x, X.e[1] = v.y, X.e[2] = v.z, X.e[3] = v.w, X.e[4] = w.x, X.e[5] = w.y;
 }
 

@@ -726,43 +726,57 @@ class MultiEngine:
         except Exception:
             pass
 
-    def _check(self, rc, what):
-        """A failed mctx call raises with the HIP error of every member
-        context that recorded one (each device's part runs on its own
-        thread and records its failure on its own context), or the calling
-        thread's record when none did."""
+    def _errs(self):
+        return [last_error(self.L.jfsx_mctx_ctx(self.m, i)) for i in range(self.ndev)]
+
+    def _call(self, what, fn, *args):
+        """Run one mctx entry point; a failure raises with the HIP error of
+        every member context whose record this call changed (each device's
+        part runs on its own worker and records on its own context; records
+        left by earlier calls are not reported), or the calling thread's
+        record when none did."""
+        before = self._errs()
+        rc = fn(self.m, *args)
         if not rc:
             return
         if rc in (EIO, ENOMEM):
-            recs = []
-            for i in range(self.ndev):
-                he, txt = last_error(self.L.jfsx_mctx_ctx(self.m, i))
-                if he or txt:
-                    recs.append((i, he, txt))
+            recs = [(i, he, txt) for i, ((he, txt), old) in enumerate(zip(self._errs(), before))
+                    if (he or txt) and (he, txt) != old]
+            if recs:
+                raise EngineError(rc, what, recs[0][1], "; ".join("device %d: %s" % (i, t) for i, _, t in recs))
+        _raise(None, rc, what)
+
+    def _check(self, rc, what):
+        """For calls made outside _call (the aggregator's): every member
+        context's record."""
+        if not rc:
+            return
+        if rc in (EIO, ENOMEM):
+            recs = [(i, he, txt) for i, (he, txt) in enumerate(self._errs()) if he or txt]
             if recs:
                 raise EngineError(rc, what, recs[0][1], "; ".join("device %d: %s" % (i, t) for i, _, t in recs))
         _raise(None, rc, what)
 
     def seal_batch(self, algo, blks, n, crc_mode=CRC_GEN, mem=MEM_HOST):
-        self._check(self.L.jfsx_mctx_seal_batch(self.m, algo, n, blks, crc_mode, mem), "jfsx_mctx_seal_batch")
+        self._call("jfsx_mctx_seal_batch", self.L.jfsx_mctx_seal_batch, algo, n, blks, crc_mode, mem)
 
     def open_batch(self, algo, blks, n, crc_mode=CRC_NONE, mem=MEM_HOST):
-        self._check(self.L.jfsx_mctx_open_batch(self.m, algo, n, blks, crc_mode, mem), "jfsx_mctx_open_batch")
+        self._call("jfsx_mctx_open_batch", self.L.jfsx_mctx_open_batch, algo, n, blks, crc_mode, mem)
 
     def crc32c_segments(self, ranges, n, mode=CRC_GEN, mem=MEM_HOST):
-        self._check(self.L.jfsx_mctx_crc32c_segments(self.m, n, ranges, mode, mem), "jfsx_mctx_crc32c_segments")
+        self._call("jfsx_mctx_crc32c_segments", self.L.jfsx_mctx_crc32c_segments, n, ranges, mode, mem)
 
     def lz4_compress_batch(self, zblks, n, mem=MEM_HOST):
-        self._check(self.L.jfsx_mctx_lz4_compress_batch(self.m, n, zblks, mem), "jfsx_mctx_lz4_compress_batch")
+        self._call("jfsx_mctx_lz4_compress_batch", self.L.jfsx_mctx_lz4_compress_batch, n, zblks, mem)
 
     def lz4_decompress_batch(self, zblks, n, mem=MEM_HOST):
-        self._check(self.L.jfsx_mctx_lz4_decompress_batch(self.m, n, zblks, mem), "jfsx_mctx_lz4_decompress_batch")
+        self._call("jfsx_mctx_lz4_decompress_batch", self.L.jfsx_mctx_lz4_decompress_batch, n, zblks, mem)
 
     def zstd_decompress_batch(self, zblks, n, mem=MEM_HOST):
-        self._check(self.L.jfsx_mctx_zstd_decompress_batch(self.m, n, zblks, mem), "jfsx_mctx_zstd_decompress_batch")
+        self._call("jfsx_mctx_zstd_decompress_batch", self.L.jfsx_mctx_zstd_decompress_batch, n, zblks, mem)
 
     def zstd_compress_batch(self, zblks, n, mem=MEM_HOST):
-        self._check(self.L.jfsx_mctx_zstd_compress_batch(self.m, n, zblks, mem), "jfsx_mctx_zstd_compress_batch")
+        self._call("jfsx_mctx_zstd_compress_batch", self.L.jfsx_mctx_zstd_compress_batch, n, zblks, mem)
 
 
 class Aggregator:

@@ -122,3 +122,25 @@ def test_more_objects_than_waves_round_trip(eng):
         assert g == zstd_lib.compress_simple(s, 1), i
     back = eng.zstd_decompress(got, lens)
     assert all(st == E.OK and d == s for (st, d), s in zip(back, srcs))
+
+
+def test_tiny_objects_at_the_end_of_their_buffer(eng):
+    """objects of 8-24 bytes (too short for the parser's 24-byte
+    candidate window) compressed from the very end of a device buffer: the
+    frames equal libzstd's and decode back (the window loads stay inside the
+    object)."""
+    for kind in ("zeros", "text", "random"):
+        for n in range(8, 25):
+            s = lz4_data.sample(kind, n, seed=n + 5) if kind in lz4_data.KINDS else bytes(n)
+            inb = eng.alloc(n)
+            inb.upload(np.frombuffer(s, np.uint8), 0)
+            cap = int(E.zstd_bound(n))
+            outb = eng.alloc(cap)
+            arr, k = eng.make_zblocks([(inb.ptr, n, outb.ptr, cap)])
+            eng.zstd_compress_batch(arr, k, E.MEM_DEVICE)
+            assert arr[0].status == E.OK
+            f = outb.download(arr[0].out_len).tobytes()
+            assert f == zstd_lib.compress_simple(s, 1), (kind, n)
+            assert eng.zstd_decompress([f], [n]) == [(E.OK, s)]
+            inb.free()
+            outb.free()

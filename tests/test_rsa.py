@@ -73,3 +73,71 @@ def test_unwrap_errors(rsa, keypair):
     good = rsae.Encrypt(os.urandom(32))
     assert unwrap(rsa, comps, good, label=b"other") is None  # wrong label -> lHash mismatch
     assert unwrap(rsa, comps, b"\xff" * 256) is None         # c >= n
+
+
+def test_exponentiation_schedule_is_independent_of_the_exponent(rsa, keypair):
+    """Constant time in the private exponent (as Go's crypto/internal/bigmod
+    Exp, which rsa.DecryptOAEP uses; encrypt.go:132-134): the sequence of
+    Montgomery products and window-table reads is the same for the key's real
+    CRT exponent, a tiny one, an all-ones one and zero -- 1024-bit fixed
+    window, one multiply per digit, every table entry read for every digit --
+    and every result equals pow()."""
+    _, _, comps = keypair
+    p = comps[0]
+    pi = int.from_bytes(p, "big")
+    x = int.from_bytes(os.urandom(127), "big") % pi
+    traces = set()
+    for e in (int.from_bytes(comps[2], "big"), 3, (1 << 1024) - 1, 0, 1 << 1023, 0x10001):
+        out = ctypes.create_string_buffer(128)
+        ops = ctypes.c_uint64()
+        rsa.rsa_exp_trace.restype = ctypes.c_uint64
+        h = rsa.rsa_exp_trace(p, e.to_bytes(128, "big"), x.to_bytes(128, "big"), out, ctypes.byref(ops))
+        assert int.from_bytes(out.raw, "big") == pow(x, e, pi)
+        traces.add((h, ops.value))
+    assert len(traces) == 1, traces
+    (_, nops), = traces
+    assert nops == 2 + 14 + 256 * 5 + 1 + 256 * 16  # table, 256 digits x (4 sq + 1 mul), exit; 16 reads per digit
+
+
+def _oaep_encode(msg, seed, label=b"keys", k=256, db_patch=None):
+    import hashlib as h
+    lh = h.sha256(label).digest()
+    ps = b"\0" * (k - len(msg) - 2 * 32 - 2)
+    db = bytearray(lh + ps + b"\x01" + msg)
+    if db_patch:
+        db_patch(db)
+
+    def mgf(s, n):
+        out = b""
+        c = 0
+        while len(out) < n:
+            out += h.sha256(s + c.to_bytes(4, "big")).digest()
+            c += 1
+        return out[:n]
+    mdb = bytes(a ^ b for a, b in zip(db, mgf(seed, len(db))))
+    ms = bytes(a ^ b for a, b in zip(seed, mgf(mdb, 32)))
+    return bytearray(b"\0" + ms + mdb)
+
+
+def test_oaep_decode_checks_without_branching_on_the_data(rsa):
+    """The decode's outcomes, each reached by the masked scan (RFC 8017
+    7.1.2 step 3g, Go's decryptOAEP): good messages of every length decode;
+    a nonzero first byte, a wrong label hash, a missing 0x01 separator, or a
+    nonzero byte in the padding all give the one decryption error."""
+    seed = os.urandom(32)
+    for n in (0, 1, 32, 190):
+        m = os.urandom(n)
+        em = _oaep_encode(m, seed)
+        buf = ctypes.create_string_buffer(bytes(em), 256)
+        assert rsa.oaep(buf, b"keys", 4) == n and buf.raw[:n] == m
+    bad = []
+    em = _oaep_encode(b"k" * 32, seed)
+    em[0] = 1
+    bad.append(em)
+    bad.append(_oaep_encode(b"k" * 32, seed, label=b"other"))
+    bad.append(_oaep_encode(b"", seed, db_patch=lambda db: db.__setitem__(len(db) - 1, 0)))  # no 0x01 at all
+    bad.append(_oaep_encode(b"k" * 32, seed, db_patch=lambda db: db.__setitem__(40, 7)))  # junk in the padding
+    bad.append(_oaep_encode(b"k" * 32, seed, db_patch=lambda db: db.__setitem__(40, 2)))
+    for em in bad:
+        buf = ctypes.create_string_buffer(bytes(em), 256)
+        assert rsa.oaep(buf, b"keys", 4) == -1
