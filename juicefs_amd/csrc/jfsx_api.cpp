@@ -79,6 +79,31 @@ struct CtxScope {
 std::shared_mutex g_alloc_mu;
 std::map<uintptr_t, std::pair<uintptr_t, int>> g_allocs;  // base -> (end, device)
 
+// Pinned host allocations made by the engine (jfsx_alloc_pinned*): the host
+// pipeline lets a kernel write straight into them.  Memory the engine did not
+// pin (pageable caller buffers) is never written by a kernel: the GPU cannot
+// fault in pageable pages.
+std::shared_mutex g_pin_mu;
+std::map<uintptr_t, uintptr_t> g_pins;  // base -> end
+
+void note_pinned(void *p, size_t bytes) {
+    std::unique_lock<std::shared_mutex> g(g_pin_mu);
+    g_pins[(uintptr_t)p] = (uintptr_t)p + bytes;
+}
+void forget_pinned(void *p) {
+    std::unique_lock<std::shared_mutex> g(g_pin_mu);
+    g_pins.erase((uintptr_t)p);
+}
+// [p, p + n) lies inside one engine-pinned allocation
+bool in_pinned(const void *p, uint64_t n) {
+    const uintptr_t a = (uintptr_t)p;
+    std::shared_lock<std::shared_mutex> g(g_pin_mu);
+    auto it = g_pins.upper_bound(a);
+    if (it == g_pins.begin()) return false;
+    --it;
+    return a >= it->first && a + n <= it->second && a + n >= a;
+}
+
 void note_alloc(void *p, size_t bytes, int device) {
     std::unique_lock<std::shared_mutex> g(g_alloc_mu);
     g_allocs[(uintptr_t)p] = {(uintptr_t)p + bytes, device};
@@ -372,11 +397,13 @@ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // Split each block into <= max_bytes tasks (a multiple of waves segments), one
 // workgroup each; `slots` partial slots per task.
 Plan plan_tasks(const std::vector<uint64_t> &lens, uint64_t max_bytes, uint32_t waves, uint32_t slots,
-                uint64_t want) {
+                uint64_t want, uint64_t min_task = 0) {
     Plan p;
     uint64_t total = 0;
     for (uint64_t l : lens) total += l;
-    const uint64_t unit = (uint64_t)waves * kSeg;
+    // tasks are whole segments; min_task (GCM: its row split keeps all 16
+    // waves busy on any task) or else one segment per wave
+    const uint64_t unit = min_task ? min_task : (uint64_t)waves * kSeg;
     uint64_t ch = max_bytes;
     // enough workgroups to fill the 256 CUs when the batch is small
     if (total / ch < want) {
@@ -412,6 +439,7 @@ void order_largest_first(Task *t, size_t n, size_t max_units) {
 }
 
 constexpr uint64_t kGcmMaxLen = (((uint64_t)1 << 32) - 2) * 16;
+constexpr uint64_t kGcmMinTask = 2 * (uint64_t)kSeg;  // 64 KiB
 constexpr uint64_t kCpMaxLen = ((uint64_t)1 << 38) - 64;
 
 int check_aead_args(int algo, int n, const jfsx_blk *blks, int crc_mode, bool device) {
@@ -453,7 +481,10 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
         if ((crc_mode & 3) == JFSX_CRC_VERIFY) crc_calc_words += nseg_of(blks[i].len);
     }
     const uint32_t slots = gcm ? kSlotsPerTask : kCpWaves;
-    Plan plan = gcm ? plan_tasks(lens, kMaxTaskBytes, kWaves, slots, 512)
+    // a small batch (the per-object path) is cut into tasks down to 64 KiB so
+    // that it still spreads over the CUs (2 tasks per CU); a 64 GiB batch keeps
+    // 4 MiB tasks
+    Plan plan = gcm ? plan_tasks(lens, kMaxTaskBytes, kWaves, slots, 512, kGcmMinTask)
                     : plan_tasks(lens, kCpTaskBytes, kCpWaves, slots, 2048);
     const size_t nt = plan.tasks.size();
     // device workspace layout
@@ -495,10 +526,12 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
         hb[i].tag_in = open ? (const uint8_t *)(d + o_tagin + 16 * (size_t)i) : nullptr;
         memcpy(h + o_tagin + 16 * (size_t)i, b.tag, 16);
     }
+    uint32_t max_slots = 0;
     for (size_t t = 0; t < nt; t++) {
         BlkDev &bd = hb[plan.tasks[t].blk];
         if (bd.nslots == 0) bd.slot0 = plan.tasks[t].slot0;
         bd.nslots += slots;
+        max_slots = std::max(max_slots, bd.nslots);
     }
     if (nt) {
         Task *ht = (Task *)(h + o_task);
@@ -536,7 +569,7 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
         launch_gcm_main(s, (int)nt, c->ncu, (uint32_t *)(d + o_queue), open, crc_mode, c->bitslice, dt, db, dsch, dpart,
                         dpexp, c->tabs);
         if (c->timing) HIP_OK(hipEventRecord(k1, s));
-        launch_gcm_finalize(s, n, open, crc_mode, db, dsch, dpart, dpexp, dout);
+        launch_gcm_finalize(s, n, open, crc_mode, db, dsch, dpart, dpexp, dout, max_slots);
     } else {
         CpSched *dsch = (CpSched *)(d + o_sched);
         launch_begin();
@@ -670,9 +703,41 @@ void pipe_collect(jfsx_ctx *c, PipeSlot &s) {
 // finalize on the transform stream, and the outputs, CRC arrays and BlkOut
 // records down on s_out, chained by the slot's events.  dv[i] (the call's copy
 // of blks[i]) is pointed at the staging copy.
+// Small groups (the per-object path) whose outputs lie in engine-pinned
+// memory have the transform kernel write them straight into the caller's
+// buffers (ciphertext rows and CRC words over PCIe, zero-copy), so the group's
+// only D2H is its BlkOut records: SDMA runs device-to-host copies of a few MiB at ~20 GB/s
+// (tools/copy_probe.hip: 4 MiB in 203 us) while a kernel's stores reach
+// ~40 GB/s beside SDMA H2D.  Large groups (host ingest's 256 MiB slots) keep
+// staged SDMA copies, which reach the full duplex rate at that size.
+// JFSX_DIRECT_MAX_MB sets the largest direct group (0: never).
+size_t direct_max_bytes() {
+    static const size_t v = [] {
+        const char *e = getenv("JFSX_DIRECT_MAX_MB");
+        return (e ? (size_t)atoll(e) : (size_t)48) << 20;
+    }();
+    return v;
+}
+
+// a group goes direct when it is small and every output lies, aligned, in
+// engine-pinned memory (a kernel cannot write pageable host memory)
+bool group_direct(int nb, const jfsx_blk *blks, int crc_mode) {
+    size_t bytes = 0;
+    for (int i = 0; i < nb; i++) bytes += blks[i].len;
+    if (bytes > direct_max_bytes()) return false;
+    for (int i = 0; i < nb; i++) {
+        const jfsx_blk &b = blks[i];
+        if (!b.len || ((uintptr_t)b.dst & 15) || !in_pinned(b.dst, b.len)) return false;
+        if ((crc_mode & 3) == JFSX_CRC_GEN && (((uintptr_t)b.crc & 3) || !in_pinned(b.crc, 4 * nseg_of(b.len))))
+            return false;
+    }
+    return true;
+}
+
 int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, int algo, bool open, int nb, const jfsx_blk *blks, jfsx_blk *dv,
                  int crc_mode) {
     Workspace &w = s.w;
+    const bool direct = group_direct(nb, blks, crc_mode);
     size_t need = 0;
     for (int i = 0; i < nb; i++) need += host_need(blks[i], crc_mode);
     int rc;
@@ -701,18 +766,24 @@ int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, int algo, bool open, int nb, const jf
             if (align256(blks[i].len) != blks[i].len && (rc = flush_in())) return rc;
         }
         dv[i].src = buf;
-        dv[i].dst = buf;
+        dv[i].dst = direct ? blks[i].dst : buf;
         if (crc_mode) {
             char *cb = w.stage + coff;
             coff += align256(4 * nseg_of(blks[i].len));
             if ((crc_mode & 3) == JFSX_CRC_VERIFY)
                 HIP_OK(hipMemcpyAsync(cb, blks[i].crc, 4 * nseg_of(blks[i].len), hipMemcpyHostToDevice, c->s_in));
-            dv[i].crc = (uint8_t *)cb;
+            dv[i].crc = direct && (crc_mode & 3) == JFSX_CRC_GEN ? blks[i].crc : (uint8_t *)cb;
         }
     }
     if ((rc = flush_in())) return rc;
     if ((rc = enqueue_aead(c, w, c->stream, s.ev_k0, s.ev_k1, algo, open, nb, dv, crc_mode, c->s_in, s.ev_in, false)))
         return rc;
+    if (direct) {
+        // outputs already in place: only the per-block results come down
+        HIP_OK(hipMemcpyAsync(w.h, w.dout, sizeof(BlkOut) * nb, hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(hipEventRecord(s.ev_out, c->stream));
+        return 0;
+    }
     HIP_OK(hipEventRecord(s.ev_comp, c->stream));
     HIP_OK(hipStreamWaitEvent(c->s_out, s.ev_comp, 0));
     char *oh = nullptr;
@@ -1342,7 +1413,10 @@ int jfsx_alloc_pinned(jfsx_ctx *c, size_t bytes, void **p) {
     HIP_OK(hipSetDevice(c->device));
     // portable: the multi-device context's other GPUs DMA from it as well
     const hipError_t e = hipHostMalloc(p, bytes, hipHostMallocPortable);
-    if (e == hipSuccess) return 0;
+    if (e == hipSuccess) {
+        note_pinned(*p, bytes);
+        return 0;
+    }
     note_hip_error(e, __FILE__, __LINE__, "hipHostMalloc(pinned)");
     return JFSX_ENOMEM;
 }
@@ -1394,7 +1468,10 @@ int jfsx_alloc_pinned_node(jfsx_ctx *c, size_t bytes, int node, void **p) {
     }
     const hipError_t e = hipHostMalloc(p, bytes, hipHostMallocPortable | (bound ? hipHostMallocNumaUser : 0));
     if (bound) (void)syscall(SYS_set_mempolicy, old_mode, old_mode == kMpolDefault ? nullptr : old_mask, kMaxNodes);
-    if (e == hipSuccess) return 0;
+    if (e == hipSuccess) {
+        note_pinned(*p, bytes);
+        return 0;
+    }
     note_hip_error(e, __FILE__, __LINE__, "hipHostMalloc(pinned, NUMA node)");
     return JFSX_ENOMEM;
 }
@@ -1418,6 +1495,7 @@ int jfsx_host_numa_node(const void *p, size_t bytes, int *node) {
 
 int jfsx_free_pinned(jfsx_ctx *c, void *p) {
     if (!c) return JFSX_EINVAL;
+    forget_pinned(p);
     HIP_OK(hipHostFree(p));
     return 0;
 }

@@ -961,9 +961,12 @@ __global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *
 // ---------------------------------------------------------------------------
 // keysetup: one wave per block; AES via the (global) T-table image
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t gT0(const uint32_t *aes, uint32_t x) { return aes[x * 64]; }
-__device__ __forceinline__ uint32_t gT2(const uint32_t *aes, uint32_t x) { return aes[x * 64 + 32]; }
-__device__ __forceinline__ uint32_t gS(const uint32_t *aes, uint32_t x) { return (aes[x * 64] >> 8) & 0xffu; }
+// keysetup's lookups go to a compact copy of T0 | T2 staged in LDS (entry x
+// at 2x, 2x + 1): every lane looks up the same index (a broadcast), and a
+// dependent chain of LDS reads costs a fraction of the same chain through L2
+__device__ __forceinline__ uint32_t gT0(const uint32_t *aes, uint32_t x) { return aes[2 * x]; }
+__device__ __forceinline__ uint32_t gT2(const uint32_t *aes, uint32_t x) { return aes[2 * x + 1]; }
+__device__ __forceinline__ uint32_t gS(const uint32_t *aes, uint32_t x) { return (aes[2 * x] >> 8) & 0xffu; }
 
 __device__ uint32_t gcol(const uint32_t *aes, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     return gT0(aes, a & 0xff) ^ rotl8(gT0(aes, (b >> 8) & 0xff)) ^ gT2(aes, (c >> 16) & 0xff) ^
@@ -1022,10 +1025,16 @@ __device__ __forceinline__ g128 g_mul_uy(const g128 &x, const g128 &y, uint4 *M,
 }
 
 __global__ __launch_bounds__(64) void gcm_keysetup_k(const KeyIn *__restrict__ keys, const BlkDev *__restrict__ blks,
-                                                    GcmSched *__restrict__ sched, const uint32_t *__restrict__ aes) {
+                                                    GcmSched *__restrict__ sched, const uint32_t *__restrict__ gtab) {
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
     GcmSched *sc = sched + b;
     const KeyIn k = keys[b];
+    __shared__ uint32_t aes[512];  // T0 | T2, compact (gT0 / gT2 / gS)
+    for (uint32_t x = lane; x < 256; x += 64) {
+        aes[2 * x] = gtab[x * 64];
+        aes[2 * x + 1] = gtab[x * 64 + 32];
+    }
+    __syncthreads();
     // AES-256 key expansion (FIPS-197 5.2), little-endian dwords
     uint32_t w[60];
     for (int i = 0; i < 8; i++) w[i] = k.key[i];
@@ -1146,32 +1155,62 @@ __global__ __launch_bounds__(64) void gcm_keysetup_k(const KeyIn *__restrict__ k
 }
 
 // ---------------------------------------------------------------------------
-// finalize: one wave per block
+// finalize: one workgroup per block, one thread per partial slot
 // ---------------------------------------------------------------------------
+// Each slot's partial is lifted by H^e (e = pexp) as products by the powers
+// H^(2^k) the block's exponents use: per k, 16 threads build the 4-bit table
+// of that (block-uniform) power in LDS and every thread whose e has bit k set
+// takes the table product (g_mul_uy) -- 32 lookups instead of a bit-serial
+// 128-step product per set bit.  A small batch (the per-object path) has
+// blocks of many short tasks and so many slots: the workgroup grows to one
+// thread per slot (up to 1024) instead of one wave looping over them.
 template <bool OPEN, int CRCMODE>
-__global__ __launch_bounds__(64) void gcm_finalize_k(const BlkDev *__restrict__ blks, const GcmSched *__restrict__ sched,
-                                                    const uint32_t *__restrict__ partial,
-                                                    const uint32_t *__restrict__ pexp, BlkOut *__restrict__ out) {
-    const uint32_t b = blockIdx.x, lane = threadIdx.x;
+__global__ __launch_bounds__(1024) void gcm_finalize_k(const BlkDev *__restrict__ blks, const GcmSched *__restrict__ sched,
+                                                      const uint32_t *__restrict__ partial,
+                                                      const uint32_t *__restrict__ pexp, BlkOut *__restrict__ out) {
+    const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nthr = blockDim.x;
+    const uint32_t nw = nthr >> 6;
+    __shared__ uint4 M[16];
+    __shared__ uint32_t sor[16];
+    __shared__ uint32_t sred[16][4];
     const BlkDev blk = blks[b];
     const GcmSched *sc = sched + b;
     uint32_t acc[4] = {0, 0, 0, 0};
-    for (uint32_t base = 0; base < blk.nslots; base += 64) {
-        const uint32_t s = base + lane;
+    for (uint32_t base = 0; base < blk.nslots; base += nthr) {
+        const uint32_t s = base + tid;
+        uint32_t m[4] = {0, 0, 0, 0}, e = 0;
         if (s < blk.nslots) {
             const uint32_t slot = blk.slot0 + s;
-            uint32_t m[4] = {partial[4 * slot], partial[4 * slot + 1], partial[4 * slot + 2], partial[4 * slot + 3]};
-            if (m[0] | m[1] | m[2] | m[3]) {
-                g128 z = g_from_mem(m);
-                uint32_t e = pexp[slot];
-                for (int k = 0; e; k++, e >>= 1)
-                    if (e & 1) z = g_mul(z, g_from_mem(sc->h2k[k]));
-                g_to_mem(z, m);
-                for (int q = 0; q < 4; q++) acc[q] ^= m[q];
-            }
+            for (int q = 0; q < 4; q++) m[q] = partial[4 * slot + q];
+            if (m[0] | m[1] | m[2] | m[3]) e = pexp[slot];
         }
+        // the powers any slot of the block needs (block-uniform loop below)
+        uint32_t eo = e;
+        for (int off = 32; off > 0; off >>= 1) eo |= __shfl_xor(eo, off, 64);
+        if (lane == 0) sor[wave] = eo;
+        __syncthreads();
+        eo = 0;
+        for (uint32_t w = 0; w < nw; w++) eo |= sor[w];
+        g128 z = g_from_mem(m);
+        for (int k = 0; k < 32 && (eo >> k); k++) {
+            if (!((eo >> k) & 1u)) continue;
+            const g128 zk = g_mul_uy(z, g_from_mem(sc->h2k[k]), M, tid);
+            if ((e >> k) & 1u) z = zk;
+        }
+        g_to_mem(z, m);
+        for (int q = 0; q < 4; q++) acc[q] ^= m[q];
+        __syncthreads();  // sor is rewritten by the next round
     }
-    for (int q = 0; q < 4; q++) acc[q] = wave_xor(acc[q]) ^ sc->init[q];
+    for (int q = 0; q < 4; q++) acc[q] = wave_xor(acc[q]);
+    if (lane == 0)
+        for (int q = 0; q < 4; q++) sred[wave][q] = acc[q];
+    __syncthreads();
+    if (wave) return;
+    for (int q = 0; q < 4; q++) {
+        uint32_t t = sc->init[q];
+        for (uint32_t w = 0; w < nw; w++) t ^= sred[w][q];
+        acc[q] = t;
+    }
     BlkOut o;
     o.status = JFSX_OK;
     o.bad_seg = -1;
@@ -1239,9 +1278,11 @@ void launch_gcm_main(hipStream_t s, int ntasks, int ncu, uint32_t *queue, bool o
 }
 
 void launch_gcm_finalize(hipStream_t s, int n, bool open, int crc_mode, const BlkDev *blks, const GcmSched *sched,
-                         const uint32_t *partial, const uint32_t *pexp, BlkOut *out) {
+                         const uint32_t *partial, const uint32_t *pexp, BlkOut *out, uint32_t max_slots) {
     if (n <= 0) return;
-#define L(O, C) hipLaunchKernelGGL((gcm_finalize_k<O, C>), dim3(n), dim3(64), 0, s, blks, sched, partial, pexp, out)
+    // one thread per slot of the block with the most slots, 64..1024
+    const uint32_t th = max_slots <= 64 ? 64u : max_slots >= 1024 ? 1024u : (max_slots + 63) / 64 * 64;
+#define L(O, C) hipLaunchKernelGGL((gcm_finalize_k<O, C>), dim3(n), dim3(th), 0, s, blks, sched, partial, pexp, out)
     if (open) {
         if ((crc_mode & 3) == 2) L(true, 2); else L(true, 0);
     } else {

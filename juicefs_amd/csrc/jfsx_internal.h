@@ -288,8 +288,9 @@ void launch_gcm_keysetup(hipStream_t s, int n, const KeyIn *keys, const BlkDev *
 void launch_gcm_main(hipStream_t s, int ntasks, int ncu, uint32_t *queue, bool open, int crc_mode, bool bitslice,
                      const Task *tasks, const BlkDev *blks, const GcmSched *sched, uint32_t *partial, uint32_t *pexp,
                      DevTables t);
+// max_slots: the most partial slots any block of the batch has (sizes the workgroup)
 void launch_gcm_finalize(hipStream_t s, int n, bool open, int crc_mode, const BlkDev *blks, const GcmSched *sched,
-                         const uint32_t *partial, const uint32_t *pexp, BlkOut *out);
+                         const uint32_t *partial, const uint32_t *pexp, BlkOut *out, uint32_t max_slots);
 void launch_cp_keysetup(hipStream_t s, int n, const KeyIn *keys, const BlkDev *blks, CpSched *sched);
 void launch_cp_main(hipStream_t s, int ntasks, int ncu, uint32_t *queue, bool open, int crc_mode, const Task *tasks,
                     const BlkDev *blks, const CpSched *sched, uint32_t *partial, uint32_t *pexp, DevTables t);

@@ -1,8 +1,11 @@
 /* The cgo shim's call sequence, made from C through
  * the C-ABI exactly as the Go side makes it, checked against the CPU oracle.
  *
- *   §2 gpuEncryptor.Encrypt  -> jfsx_data_encrypt (12 args, obj_crc NULL / set)
- *      gpuEncryptor.Decrypt  -> jfsx_parse_header, [key unwrap], jfsx_data_decrypt (10 args)
+ *   §2 gpuEncryptor.Encrypt  -> jfsx_agg_data_encrypt over the multi-device
+ *                               aggregator, from many threads (and the one-call
+ *                               jfsx_data_encrypt, obj_crc NULL / set)
+ *      gpuEncryptor.Decrypt  -> jfsx_parse_header, [key unwrap], jfsx_agg_data_decrypt
+ *                               (and jfsx_data_decrypt)
  *   §3 upload goroutines     -> jfsx_agg_seal / jfsx_agg_open on descriptors in
  *                               C memory whose src/dst/crc point into the pinned
  *                               pool (jfsx_alloc_pinned), from many threads;
@@ -73,6 +76,56 @@ static void encrypt_decrypt(jfsx_ctx *ctx, int algo) {
         CHECK(jfsx_parse_header(obj, 271, &klen, &nlen) == JFSX_EMISFORMED);
         free(p), free(obj), free(ref), free(back);
     }
+}
+
+/* --- §2 as the shim runs it: per-object Encrypt / Decrypt from many
+ * goroutines (max-uploads, cmd/flags.go:124-128) through the aggregator ---- */
+typedef struct {
+    jfsx_agg *agg;
+    int algo, t, bad;
+} obj_arg;
+
+static void *obj_worker(void *vp) {
+    obj_arg *a = (obj_arg *)vp;
+    uint8_t wrapped[256];
+    for (int k = 0; k < 256; k++) wrapped[k] = (uint8_t)(k * 5 + a->t);
+    for (int j = 0; j < PER_THREAD; j++) {
+        const int i = a->t * PER_THREAD + j;
+        const uint64_t n = kLens[i];
+        uint8_t key[32], nonce[12];
+        orc_gen_key(SEED, 3000 + i, key, nonce);
+        uint8_t *p = malloc(n + 1), *obj = malloc(n + 287), *ref = malloc(n + 287), *back = malloc(n + 287);
+        orc_gen_block(SEED, 3000 + i, p, n);
+        uint64_t olen = 0, pl = 0;
+        uint32_t ocrc = 0, got = 0;
+        if (jfsx_agg_data_encrypt(a->agg, a->algo, key, nonce, wrapped, 256, p, n, obj, n + 287, &olen, &ocrc) ||
+            olen != n + 287 || orc_data_encrypt(a->algo, key, nonce, wrapped, 256, p, n, ref) != (int64_t)olen ||
+            memcmp(obj, ref, olen) != 0 || ocrc != orc_crc32c_update(0, obj, olen))
+            a->bad++;
+        else if (jfsx_agg_data_decrypt(a->agg, a->algo, key, obj, olen, back, olen, &pl, &ocrc, &got) || pl != n ||
+                 got != ocrc || memcmp(back, p, n) != 0)
+            a->bad++;
+        free(p), free(obj), free(ref), free(back);
+    }
+    return NULL;
+}
+
+static void agg_encrypt_decrypt(jfsx_mctx *m, int algo) {
+    jfsx_agg *agg = NULL;
+    CHECK(jfsx_agg_new_mctx(m, 0, 16u << 20, 500, &agg) == 0);
+    pthread_t th[NTHREADS];
+    obj_arg a[NTHREADS];
+    for (int t = 0; t < NTHREADS; t++) {
+        a[t] = (obj_arg){agg, algo, t, 0};
+        CHECK(pthread_create(&th[t], NULL, obj_worker, &a[t]) == 0);
+    }
+    for (int t = 0; t < NTHREADS; t++) {
+        CHECK(pthread_join(th[t], NULL) == 0);
+        CHECK(a[t].bad == 0);
+    }
+    uint64_t calls = 0, batches = 0, blocks = 0;
+    CHECK(jfsx_agg_stats(agg, &calls, &batches, &blocks) == 0 && calls == 2 * NTHREADS * PER_THREAD);
+    CHECK(jfsx_agg_free(agg) == 0);
 }
 
 /* --- §3: per-block calls through the aggregator, descriptors in C memory -- */
@@ -365,6 +418,7 @@ int main(void) {
     CHECK(jfsx_mctx_open(0, 0, &m) == 0 && jfsx_mctx_ndev(m) == nd);
     for (int algo = 0; algo < 2; algo++) {
         encrypt_decrypt(ctx, algo);
+        agg_encrypt_decrypt(m, algo);
         aggregated(ctx, NULL, algo);
         aggregated(ctx, m, algo);
     }
