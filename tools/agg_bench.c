@@ -1,0 +1,97 @@
+/* agg_bench.c -- the per-object call shape from C threads (no Python): T
+ * threads each seal one 4 MiB block of pinned host memory per call through
+ * the aggregator (jfsx_agg_seal), as the Go shim's upload goroutines do
+ * (pkg/chunk/cached_store.go:415-472, max-uploads at cmd/flags.go:124-128).
+ * Reports GB/s of plaintext for the aggregator and for direct one-block
+ * jfsx_seal_batch calls, to separate the engine from the Python harness.
+ *
+ * usage: agg_bench [threads=20] [blocks=512] [passes=4] [max_mb=16] [window_us=500]
+ * build: cc -O2 -o tools/agg_bench tools/agg_bench.c -Iinclude -Ljuicefs_amd -ljfsx -lpthread \
+ *        -Wl,-rpath,'$ORIGIN/../juicefs_amd' */
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "jfsx.h"
+
+static int T = 20, NB = 512, PASSES = 4;
+static const uint64_t L = 4 << 20;
+static uint8_t *hin, *hout, *hcrc;
+static jfsx_ctx *ctx;
+static jfsx_agg *agg;
+static int use_agg;
+
+static double now(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+static void *worker(void *vp) {
+    const int t = (int)(intptr_t)vp;
+    jfsx_blk *b = calloc(1, sizeof(jfsx_blk));
+    for (int pass = 0; pass < PASSES; pass++)
+        for (int i = t; i < NB; i += T) {
+            memset(b, 0, sizeof(*b));
+            jfsx_gen_key(7, (uint64_t)i, b->key, b->nonce);
+            b->src = hin + (uint64_t)i * L;
+            b->dst = hout + (uint64_t)i * L;
+            b->len = L;
+            b->crc = hcrc + (uint64_t)i * 512;
+            const int rc = use_agg ? jfsx_agg_seal(agg, JFSX_AES256GCM, b, JFSX_CRC_GEN, JFSX_MEM_HOST)
+                                   : jfsx_seal_batch(ctx, JFSX_AES256GCM, 1, b, JFSX_CRC_GEN, JFSX_MEM_HOST);
+            if (rc || b->status) {
+                fprintf(stderr, "seal failed: rc %d status %d\n", rc, b->status);
+                exit(1);
+            }
+        }
+    free(b);
+    return NULL;
+}
+
+static double run(void) {
+    pthread_t th[256];
+    const double t0 = now();
+    for (int t = 0; t < T; t++) pthread_create(&th[t], NULL, worker, (void *)(intptr_t)t);
+    for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
+    return (double)NB * L * PASSES / (now() - t0) / 1e9;
+}
+
+int main(int argc, char **argv) {
+    if (argc > 1) T = atoi(argv[1]);
+    if (argc > 2) NB = atoi(argv[2]);
+    if (argc > 3) PASSES = atoi(argv[3]);
+    const uint64_t max_mb = argc > 4 ? strtoull(argv[4], 0, 10) : 16;
+    const uint32_t window = argc > 5 ? (uint32_t)atoi(argv[5]) : 500;
+    if (jfsx_ctx_open(0, 0, &ctx)) return 1;
+    if (jfsx_alloc_pinned(ctx, NB * L, (void **)&hin) || jfsx_alloc_pinned(ctx, NB * L, (void **)&hout) ||
+        jfsx_alloc_pinned(ctx, NB * 512, (void **)&hcrc))
+        return 1;
+    for (uint64_t i = 0; i < NB * L; i += 8) *(uint64_t *)(hin + i) = i * 0x9E3779B97F4A7C15ull;
+    use_agg = 0;
+    PASSES = 1;
+    run();
+    const int passes = argc > 3 ? atoi(argv[3]) : 4;
+    PASSES = passes;
+    const double direct = run();
+    if (jfsx_agg_new(ctx, 0, max_mb << 20, window, &agg)) return 1;
+    use_agg = 1;
+    PASSES = 1;
+    run();
+    PASSES = passes;
+    const double aggr = run();
+    uint64_t calls, batches, blocks;
+    jfsx_agg_stats(agg, &calls, &batches, &blocks);
+    printf("{\"threads\": %d, \"blocks\": %d, \"passes\": %d, \"max_mb\": %llu, \"window_us\": %u, "
+           "\"direct_GBs\": %.2f, \"agg_GBs\": %.2f, \"agg_batches\": %llu, \"agg_calls\": %llu}\n",
+           T, NB, passes, (unsigned long long)max_mb, window, direct, aggr, (unsigned long long)batches,
+           (unsigned long long)calls);
+    jfsx_agg_free(agg);
+    jfsx_free_pinned(ctx, hin);
+    jfsx_free_pinned(ctx, hout);
+    jfsx_free_pinned(ctx, hcrc);
+    jfsx_ctx_close(ctx);
+    return 0;
+}
