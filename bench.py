@@ -46,7 +46,7 @@ def parse():
                     help="aggcodec: the Compress / Decompress call of cachedStore.upload / load measured in the "
                          "reference's call shape")
     ap.add_argument("--agg-window-us", type=int, default=500, help="agg: aggregation window")
-    ap.add_argument("--agg-max-mb", type=int, default=16,
+    ap.add_argument("--agg-max-mb", type=int, default=12,
                     help="agg: byte cap of one aggregated batch (several batches pipeline at once)")
     ap.add_argument("--algo", choices=["aes256gcm", "chacha20poly1305"], default="aes256gcm")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")

@@ -470,9 +470,15 @@ int check_aead_args(int algo, int n, const jfsx_blk *blks, int crc_mode, bool de
 // collect = false the caller downloads the BlkOut results on its own stream.
 // The compute stream then carries kernels only, so the H2D and D2H DMA of
 // neighbouring slots run concurrently (full duplex).
+// With fin = (s_out, ev) the keysetup kernel also rides the upload stream
+// (after the data and descriptors) and the finalize kernel runs on fin after
+// ev marks the main kernel's end: the compute stream then carries only the
+// main kernels, so a small batch's keysetup and finalize -- a few waves each,
+// latency-bound -- overlap the neighbouring batches' main kernels instead of
+// running between them.
 int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEvent_t k1, int algo, bool open, int n,
                  const jfsx_blk *blks, int crc_mode, hipStream_t up = nullptr, hipEvent_t up_ev = nullptr,
-                 bool collect = true) {
+                 bool collect = true, hipStream_t fin = nullptr, hipEvent_t main_ev = nullptr) {
     const bool gcm = algo == JFSX_AES256GCM;
     std::vector<uint64_t> lens(n);
     uint64_t crc_calc_words = 0;
@@ -493,19 +499,20 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
     const size_t o_blk = off; off = align256(off + sizeof(BlkDev) * n);
     const size_t o_task = off; off = align256(off + sizeof(Task) * std::max<size_t>(nt, 1));
     const size_t o_tagin = off; off = align256(off + 16 * (size_t)n);
+    const size_t o_queue = off; off = align256(off + 4);  // persistent kernel's task counter (uploaded as 0)
     const size_t h_bytes = off;  // everything above is uploaded from the pinned mirror
     const size_t o_out = off; off = align256(off + sizeof(BlkOut) * n);
     const size_t o_sched = off; off = align256(off + (gcm ? sizeof(GcmSched) : sizeof(CpSched)) * n);
     const size_t o_part = off; off = align256(off + 32 * std::max<uint64_t>(plan.nslots, 1));
     const size_t o_pexp = off; off = align256(off + 4 * std::max<uint64_t>(plan.nslots, 1));
     const size_t o_calc = off; off = align256(off + 4 * std::max<uint64_t>(crc_calc_words, 1));
-    const size_t o_queue = off; off = align256(off + 4);  // persistent kernel's task counter
     int rc;
     if ((rc = ensure_dev(c, &w.d, &w.dcap, off))) return rc;
     if ((rc = ensure_host(&w.h, &w.hcap, std::max(h_bytes, sizeof(BlkOut) * n)))) return rc;
     char *h = w.h, *d = w.d;
     KeyIn *hk = (KeyIn *)(h + o_keys);
     BlkDev *hb = (BlkDev *)(h + o_blk);
+    *(uint32_t *)(h + o_queue) = 0;
     uint64_t calc = 0;
     for (int i = 0; i < n; i++) {
         const jfsx_blk &b = blks[i];
@@ -545,44 +552,51 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
         // critical path for every batch
         order_largest_first(ht, nt, (size_t)(gcm ? kMaxTaskBytes : kCpTaskBytes) >> 12);
     }
-    if (up) {
-        HIP_OK(hipMemcpyAsync(d, h, h_bytes, hipMemcpyHostToDevice, up));
-        HIP_OK(hipEventRecord(up_ev, up));
-        HIP_OK(hipStreamWaitEvent(s, up_ev, 0));
-    } else {
-        HIP_OK(hipMemcpyAsync(d, h, h_bytes, hipMemcpyHostToDevice, s));
-    }
-    if ((crc_mode & 3) == JFSX_CRC_GEN)
-        for (int i = 0; i < n; i++)
-            if (blks[i].len == 0) HIP_OK(hipMemsetAsync(blks[i].crc, 0, 4, s));
     const KeyIn *dk = (const KeyIn *)(d + o_keys);
     const BlkDev *db = (const BlkDev *)(d + o_blk);
     const Task *dt = (const Task *)(d + o_task);
     uint32_t *dpart = (uint32_t *)(d + o_part);
     uint32_t *dpexp = (uint32_t *)(d + o_pexp);
+    uint32_t *dq = (uint32_t *)(d + o_queue);
     BlkOut *dout = (BlkOut *)(d + o_out);
-    if (gcm) {
-        GcmSched *dsch = (GcmSched *)(d + o_sched);
-        launch_begin();
-        launch_gcm_keysetup(s, n, dk, db, dsch, c->tabs);
-        if (c->timing) HIP_OK(hipEventRecord(k0, s));
-        launch_gcm_main(s, (int)nt, c->ncu, (uint32_t *)(d + o_queue), open, crc_mode, c->bitslice, dt, db, dsch, dpart,
-                        dpexp, c->tabs);
-        if (c->timing) HIP_OK(hipEventRecord(k1, s));
-        launch_gcm_finalize(s, n, open, crc_mode, db, dsch, dpart, dpexp, dout, max_slots);
-    } else {
-        CpSched *dsch = (CpSched *)(d + o_sched);
-        launch_begin();
-        launch_cp_keysetup(s, n, dk, db, dsch);
-        if (c->timing) HIP_OK(hipEventRecord(k0, s));
-        launch_cp_main(s, (int)nt, c->ncu, (uint32_t *)(d + o_queue), open, crc_mode, dt, db, dsch, dpart, dpexp,
-                       c->tabs);
-        if (c->timing) HIP_OK(hipEventRecord(k1, s));
-        launch_cp_finalize(s, n, open, crc_mode, db, dsch, dpart, dpexp, dout);
+    // keysetup on the upload stream when one is given (fin set), else on s
+    hipStream_t ks = (up && fin) ? up : s, fs = fin ? fin : s;
+    HIP_OK(hipMemcpyAsync(d, h, h_bytes, hipMemcpyHostToDevice, up ? up : s));
+    // the compute stream waits for the upload before the first kernel that
+    // reads the descriptors: keysetup when it runs on s, else main
+    if (up && ks == s) {
+        HIP_OK(hipEventRecord(up_ev, up));
+        HIP_OK(hipStreamWaitEvent(s, up_ev, 0));
     }
+    launch_begin();
+    if (gcm) launch_gcm_keysetup(ks, n, dk, db, (GcmSched *)(d + o_sched), c->tabs);
+    else launch_cp_keysetup(ks, n, dk, db, (CpSched *)(d + o_sched));
+    if (up && ks != s) {
+        HIP_OK(hipEventRecord(up_ev, up));
+        HIP_OK(hipStreamWaitEvent(s, up_ev, 0));
+    }
+    if ((crc_mode & 3) == JFSX_CRC_GEN)
+        for (int i = 0; i < n; i++)
+            if (blks[i].len == 0) HIP_OK(hipMemsetAsync(blks[i].crc, 0, 4, s));
+    if (c->timing) HIP_OK(hipEventRecord(k0, s));
+    if (gcm)
+        launch_gcm_main(s, (int)nt, c->ncu, dq, open, crc_mode, c->bitslice, dt, db, (const GcmSched *)(d + o_sched),
+                        dpart, dpexp, c->tabs);
+    else
+        launch_cp_main(s, (int)nt, c->ncu, dq, open, crc_mode, dt, db, (const CpSched *)(d + o_sched), dpart, dpexp,
+                       c->tabs);
+    if (c->timing) HIP_OK(hipEventRecord(k1, s));
+    if (fin) {
+        HIP_OK(hipEventRecord(main_ev, s));
+        HIP_OK(hipStreamWaitEvent(fs, main_ev, 0));
+    }
+    if (gcm)
+        launch_gcm_finalize(fs, n, open, crc_mode, db, (const GcmSched *)(d + o_sched), dpart, dpexp, dout, max_slots);
+    else
+        launch_cp_finalize(fs, n, open, crc_mode, db, (const CpSched *)(d + o_sched), dpart, dpexp, dout);
     HIP_OK(hipGetLastError());
     w.dout = dout;
-    if (collect) HIP_OK(hipMemcpyAsync(h, dout, sizeof(BlkOut) * n, hipMemcpyDeviceToHost, s));
+    if (collect) HIP_OK(hipMemcpyAsync(h, dout, sizeof(BlkOut) * n, hipMemcpyDeviceToHost, fs));
     w.n = n;
     w.nt = nt;
     w.timed = c->timing;
@@ -714,7 +728,7 @@ void pipe_collect(jfsx_ctx *c, PipeSlot &s) {
 size_t direct_max_bytes() {
     static const size_t v = [] {
         const char *e = getenv("JFSX_DIRECT_MAX_MB");
-        return (e ? (size_t)atoll(e) : (size_t)48) << 20;
+        return (e ? (size_t)atoll(e) : (size_t)0) << 20;
     }();
     return v;
 }
@@ -776,6 +790,10 @@ int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, int algo, bool open, int nb, const jf
         }
     }
     if ((rc = flush_in())) return rc;
+    // keysetup, main and finalize on the compute stream.  (Moving keysetup onto
+    // s_in and finalize onto s_out, to overlap them with neighbouring groups'
+    // main kernels, measured 30-33 GB/s against 38-40 at 20 per-object callers:
+    // the copy engines then wait behind those kernels.)
     if ((rc = enqueue_aead(c, w, c->stream, s.ev_k0, s.ev_k1, algo, open, nb, dv, crc_mode, c->s_in, s.ev_in, false)))
         return rc;
     if (direct) {

@@ -572,7 +572,7 @@ void launch_cp_main(hipStream_t s, int ntasks, int ncu, uint32_t *queue, bool op
     if (ntasks <= 0) return;
     const int groups = ncu * kCpGroupsPerCu;
     dim3 g(ntasks < groups ? ntasks : groups), bl(kCpWaves * 64);
-    (void)hipMemsetAsync(queue, 0, 4, s);
+    // queue: zeroed by the caller (uploaded with the batch descriptors)
 #define L(O, C) hipLaunchKernelGGL((cp_main_k<O, C>), g, bl, 0, s, tasks, (uint32_t)ntasks, queue, blks, sched, \
                                    partial, pexp, t)
     switch ((open ? 8 : 0) | crc_mode) {

@@ -973,13 +973,18 @@ __device__ uint32_t gcol(const uint32_t *aes, uint32_t a, uint32_t b, uint32_t c
            rotl8(gT2(aes, d >> 24));
 }
 
+// rk: the schedule in LDS (broadcast reads); the state stays in registers
 __device__ void aes_enc_global(const uint32_t *aes, const uint32_t *rk, const uint32_t in[4], uint32_t out[4]) {
     uint32_t s[4], t[4];
+#pragma unroll
     for (int c = 0; c < 4; c++) s[c] = in[c] ^ rk[c];
     for (int r = 1; r < 14; r++) {
+#pragma unroll
         for (int c = 0; c < 4; c++) t[c] = gcol(aes, s[c], s[(c + 1) & 3], s[(c + 2) & 3], s[(c + 3) & 3]) ^ rk[4 * r + c];
+#pragma unroll
         for (int c = 0; c < 4; c++) s[c] = t[c];
     }
+#pragma unroll
     for (int c = 0; c < 4; c++) {
         uint32_t a = s[c], b = s[(c + 1) & 3], cc = s[(c + 2) & 3], d = s[(c + 3) & 3];
         out[c] = (gS(aes, a & 0xff) | (gS(aes, (b >> 8) & 0xff) << 8) | (gS(aes, (cc >> 16) & 0xff) << 16) |
@@ -1035,28 +1040,36 @@ __global__ __launch_bounds__(64) void gcm_keysetup_k(const KeyIn *__restrict__ k
         aes[2 * x + 1] = gtab[x * 64 + 32];
     }
     __syncthreads();
-    // AES-256 key expansion (FIPS-197 5.2), little-endian dwords
-    uint32_t w[60];
-    for (int i = 0; i < 8; i++) w[i] = k.key[i];
-    uint32_t rcon = 1;
-    for (int i = 8; i < 60; i++) {
-        uint32_t t = w[i - 1];
-        if ((i & 7) == 0) {
-            t = (t >> 8) | (t << 24);  // RotWord
-            t = gS(aes, t & 0xff) | (gS(aes, (t >> 8) & 0xff) << 8) | (gS(aes, (t >> 16) & 0xff) << 16) |
-                (gS(aes, t >> 24) << 24);
-            t ^= rcon;
-            rcon <<= 1;
-        } else if ((i & 7) == 4) {
-            t = gS(aes, t & 0xff) | (gS(aes, (t >> 8) & 0xff) << 8) | (gS(aes, (t >> 16) & 0xff) << 16) |
-                (gS(aes, t >> 24) << 24);
+    // AES-256 key expansion (FIPS-197 5.2), little-endian dwords, kept in LDS:
+    // one lane expands, every lane reads the words it needs by index (a
+    // lane-indexed register array would live in scratch, whose every access is
+    // a memory round trip)
+    __shared__ uint32_t sw[60];
+    if (lane < 8) sw[lane] = keys[b].key[lane];
+    __syncthreads();
+    if (lane == 0) {
+        uint32_t rcon = 1;
+        for (int i = 8; i < 60; i++) {
+            uint32_t t = sw[i - 1];
+            if ((i & 7) == 0) {
+                t = (t >> 8) | (t << 24);  // RotWord
+                t = gS(aes, t & 0xff) | (gS(aes, (t >> 8) & 0xff) << 8) | (gS(aes, (t >> 16) & 0xff) << 16) |
+                    (gS(aes, t >> 24) << 24);
+                t ^= rcon;
+                rcon <<= 1;
+            } else if ((i & 7) == 4) {
+                t = gS(aes, t & 0xff) | (gS(aes, (t >> 8) & 0xff) << 8) | (gS(aes, (t >> 16) & 0xff) << 16) |
+                    (gS(aes, t >> 24) << 24);
+            }
+            sw[i] = sw[i - 8] ^ t;
         }
-        w[i] = w[i - 8] ^ t;
     }
-    if (lane < 60) sc->rk[lane] = w[lane];
+    __syncthreads();
+    const uint32_t *w = sw;
+    if (lane < 60) sc->rk[lane] = sw[lane];
     {
         // bitsliced-AES masks: lane 4(r-1) + w computes dword w of u_r
-        const uint32_t my = lane < 56 ? jfsx_bs::round_mask_word(w, 1 + (int)(lane >> 2), (int)(lane & 3)) : 0u;
+        const uint32_t my = lane < 56 ? jfsx_bs::round_mask_word(sw, 1 + (int)(lane >> 2), (int)(lane & 3)) : 0u;
         if (lane < 56) sc->bsu[1 + (lane >> 2)][lane & 3] = my;
         // round-1 constants: S-boxes of the 12 nonce bytes (lanes 0..11), then
         // MixColumns of each column's uniform part (lanes 0..3)
@@ -1084,10 +1097,10 @@ __global__ __launch_bounds__(64) void gcm_keysetup_k(const KeyIn *__restrict__ k
     aes_enc_global(aes, w, J0, EJ0);
     const g128 H = g_from_mem(Hm);
     // H^(2^k)
-    g128 hs[8];
+    __shared__ g128 hs[8];  // H^(2^k), k < 8: uniform values read by index (LDS, not scratch)
     g128 g = H;
     for (int i = 0; i < 32; i++) {
-        if (i < 8) hs[i] = g;
+        if (i < 8 && lane == 0) hs[i] = g;
         if ((int)lane == i) {
             uint32_t m[4];
             g_to_mem(g, m);
@@ -1095,6 +1108,7 @@ __global__ __launch_bounds__(64) void gcm_keysetup_k(const KeyIn *__restrict__ k
         }
         g = g_sqr(g);
     }
+    __syncthreads();
 #if JFSX_KS_NIB
     // H^e for e = lane (bits 0..5: six products by the uniform H^(2^q), each
     // kept where the lane's bit is set), then H^(64 + e) = H^e H^64, e < 4
@@ -1173,8 +1187,11 @@ __global__ __launch_bounds__(1024) void gcm_finalize_k(const BlkDev *__restrict_
     __shared__ uint4 M[16];
     __shared__ uint32_t sor[16];
     __shared__ uint32_t sred[16][4];
+    __shared__ uint32_t h2k[32][4];  // the block's H^(2^k), staged once (not a global load per product)
     const BlkDev blk = blks[b];
     const GcmSched *sc = sched + b;
+    if (tid < 128) h2k[tid >> 2][tid & 3] = sc->h2k[tid >> 2][tid & 3];
+    __syncthreads();
     uint32_t acc[4] = {0, 0, 0, 0};
     for (uint32_t base = 0; base < blk.nslots; base += nthr) {
         const uint32_t s = base + tid;
@@ -1194,7 +1211,7 @@ __global__ __launch_bounds__(1024) void gcm_finalize_k(const BlkDev *__restrict_
         g128 z = g_from_mem(m);
         for (int k = 0; k < 32 && (eo >> k); k++) {
             if (!((eo >> k) & 1u)) continue;
-            const g128 zk = g_mul_uy(z, g_from_mem(sc->h2k[k]), M, tid);
+            const g128 zk = g_mul_uy(z, g_from_mem(h2k[k]), M, tid);
             if ((e >> k) & 1u) z = zk;
         }
         g_to_mem(z, m);
@@ -1241,7 +1258,7 @@ void launch_gcm_main(hipStream_t s, int ntasks, int ncu, uint32_t *queue, bool o
                      DevTables t) {
     if (ntasks <= 0) return;
     const unsigned grid = (unsigned)(ntasks < ncu ? ntasks : ncu);  // persistent: one workgroup per CU
-    (void)hipMemsetAsync(queue, 0, 4, s);
+    // queue: zeroed by the caller (uploaded with the batch descriptors)
     // JFSX_GCM_HYBRID="nbs,rho,prio" selects the hybrid shape (BS = 2) for the
     // T-table context (an A/B switch; see GcmShape)
     static const uint32_t hyb = [] {
