@@ -232,12 +232,17 @@ def dry_run(args, world, rank, local, dist):
     lo = -max_over_ranks(dist, -float(base), local)
     hi = max_over_ranks(dist, float(base + count), local)
     per_max = max_over_ranks(dist, float(count), local)
+    # host mode pins the resident pool twice (in, out) plus its CRC arrays
+    L = args.block_bytes
+    pinned = resident * (2 * L + 4 * -(-L // (32 << 10))) if args.mem == "host" else 0
+    pinned_max = max_over_ranks(dist, float(pinned), local)
     if rank == 0:
         print(json.dumps({"metric": "dry run (no engine)", "value": None, "unit": "GB/s", "n_gpus": world,
                           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3, 3),
                           "dry_run": True, "last_rank_first_block": int(first), "scaling": scaling(args),
                           "blocks_total": int(total), "block_range": [int(lo), int(hi)],
                           "per_gpu_blocks_max": int(per_max), "resident_blocks": resident, "loops_per_step": len(loops),
+                          "pinned_bytes_per_rank_max": int(pinned_max),
                           "config": {"blocks_per_gpu": args.blocks, "total_gib": args.total_gib or None,
                                      "parallelism": "block-sharded x%d, no collective" % world}}), flush=True)
     if dist is not None:
@@ -730,7 +735,7 @@ def full_check(args, E, blks, got, lens, base):
 PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
 # labelled PMC summaries (scripts/pmc_r3.py), newest first; the round-2 file
 # (FETCH / WRITE only, keyed by kernel) is the last resort for traffic
-PMC_FILES = ("r4/pmc_r4.json", "r3/pmc_r3.json")
+PMC_FILES = ("r5/pmc_r5.json", "r4/pmc_r4.json", "r3/pmc_r3.json")
 PMC_R2 = "r2/pmc_traffic.json"
 R2_KEYS = {"seal_gcm": "gcm_ttable", "open_gcm": "gcm_ttable", "seal_gcm_bitslice": "gcm_bitslice",
            "seal_chacha": "chacha", "open_chacha": "chacha", "crc_verify": "crc_verify",
@@ -1005,7 +1010,13 @@ def agg_bench(args, world, rank, local, dist, eng):
     nb, L = min(args.blocks, 1024), args.block_bytes
     nseg = -(-L // E.SEG)
     algo = E.AES256GCM if args.algo == "aes256gcm" else E.CHACHA20P1305
-    hin, hout, hcrc = eng.alloc_pinned(nb * L), eng.alloc_pinned(nb * L), eng.alloc_pinned(nb * 4 * nseg)
+    # the blocks live on the GPU's NUMA node and the callers run there (an
+    # unbound pool that lands on the far socket measured 19 GB/s against 41)
+    node = eng.numa_node()
+    cpus = numa_pin(node) if node >= 0 else 0
+    hin, hout = eng.alloc_pinned_node(nb * L, node), eng.alloc_pinned_node(nb * L, node)
+    hcrc = eng.alloc_pinned_node(nb * 4 * nseg, node)
+    pool_node = E.host_numa_node(hin, nb * L)
     tmp = eng.alloc(L)
     base = rank * nb
     for b in range(nb):
@@ -1085,7 +1096,8 @@ def agg_bench(args, world, rank, local, dist, eng):
             "config": {"workload": "%d one-block Seal calls per step from %d threads, %s + CRC32C full, JFSX_MEM_HOST"
                                    % (nb, T, args.algo), "blocks_per_gpu": nb, "block_bytes": L, "algo": args.algo,
                        "mode": "agg", "window_us": args.agg_window_us, "max_batch_bytes": args.agg_max_mb << 20,
-                       "dispatchers_per_gpu": int(os.environ.get("JFSX_AGG_DISPATCHERS", "4"))},
+                       "dispatchers_per_gpu": int(os.environ.get("JFSX_AGG_DISPATCHERS", "4")),
+                       "numa": {"gpu_node": node, "pool_node": pool_node, "cpus_on_node": cpus}},
             "aggregator": {"calls": c1 - c0, "batches": b1 - b0,
                            "mean_batch_blocks": round((k1 - k0) / max(b1 - b0, 1), 2)},
             "direct_one_block_calls_GBs": round(nb * L * d_steps / d_el / 1e9, 2),
@@ -1371,13 +1383,22 @@ def lz4_bench(args, world, rank, local, dist, eng):
                          "frac": round(algo_bytes / (k_avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if k_n else None,
                          "traffic": pmc_traffic(args, nb * L)[0], "traffic_source": pmc_traffic(args, nb * L)[1],
                          "traffic_note": CODEC_TRAFFIC_NOTE, "binding": pmc_traffic(args, nb * L)[2],
-                         "kernel": "lz4_compress_k" if args.mode == "lz4" else "lz4_decompress_k",
+                         "kernel": lz4_kernel_name(args.mode, nb),
                          "kernel_avg_ms": round(k_avg, 3), "algorithmic_bytes_per_launch": algo_bytes,
                          "plain_bytes_per_launch": nb * L},
             "cpu_baseline": cpu, "verified_blocks": verified}), flush=True)
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def lz4_kernel_name(mode, nb, cus=256):
+    """The LZ4 kernel a batch of nb blocks runs (launch_lz4_compress: the LDS
+    table while the batch fits 16 blocks per CU, JFSX_LZ4_TABLE overrides)."""
+    if mode != "lz4":
+        return "lz4_decompress_k"
+    env = os.environ.get("JFSX_LZ4_TABLE")
+    return "lz4_compress_lds_k" if env == "lds" or (env != "global" and nb <= 16 * cus) else "lz4_compress_k"
 
 
 def zstd_cpu_baseline(frames, L):

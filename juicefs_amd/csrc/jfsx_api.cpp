@@ -230,6 +230,9 @@ struct Workspace {
     int n = 0;              // blocks of the batch in flight
     uint64_t nt = 0;        // tasks of the batch in flight
     const void *dout = nullptr;  // device BlkOut[n] of the batch in flight
+    size_t down = 0;        // bytes of the result download (BlkOut[n], then the CRC words with host_crc)
+    size_t crc_off = 0;     // host_crc GEN: offset of the CRC words in that download
+    bool crc_back = false;  // host_crc GEN: finish_aead copies the CRC words to the callers' arrays
     bool timed = false;     // the batch's main kernel is bracketed by timing events
 };
 
@@ -470,6 +473,10 @@ int check_aead_args(int algo, int n, const jfsx_blk *blks, int crc_mode, bool de
 // collect = false the caller downloads the BlkOut results on its own stream.
 // The compute stream then carries kernels only, so the H2D and D2H DMA of
 // neighbouring slots run concurrently (full duplex).
+// host_crc: the blocks' CRC pointers are host arrays.  VERIFY arrays ride the
+// descriptor upload (copied into the pinned mirror) and GEN arrays come back
+// behind the BlkOut records in the same download, so a group of per-object
+// blocks costs one small copy each way instead of one per block.
 // With fin = (s_out, ev) the keysetup kernel also rides the upload stream
 // (after the data and descriptors) and the finalize kernel runs on fin after
 // ev marks the main kernel's end: the compute stream then carries only the
@@ -478,14 +485,18 @@ int check_aead_args(int algo, int n, const jfsx_blk *blks, int crc_mode, bool de
 // running between them.
 int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEvent_t k1, int algo, bool open, int n,
                  const jfsx_blk *blks, int crc_mode, hipStream_t up = nullptr, hipEvent_t up_ev = nullptr,
-                 bool collect = true, hipStream_t fin = nullptr, hipEvent_t main_ev = nullptr) {
+                 bool collect = true, hipStream_t fin = nullptr, hipEvent_t main_ev = nullptr,
+                 bool host_crc = false) {
     const bool gcm = algo == JFSX_AES256GCM;
     std::vector<uint64_t> lens(n);
-    uint64_t crc_calc_words = 0;
+    uint64_t crc_calc_words = 0, crc_words = 0;
     for (int i = 0; i < n; i++) {
         lens[i] = blks[i].len;
         if ((crc_mode & 3) == JFSX_CRC_VERIFY) crc_calc_words += nseg_of(blks[i].len);
+        crc_words += nseg_of(blks[i].len);
     }
+    const bool hc_in = host_crc && (crc_mode & 3) == JFSX_CRC_VERIFY;
+    const bool hc_out = host_crc && (crc_mode & 3) == JFSX_CRC_GEN;
     const uint32_t slots = gcm ? kSlotsPerTask : kCpWaves;
     // a small batch (the per-object path) is cut into tasks down to 64 KiB so
     // that it still spreads over the CUs (2 tasks per CU); a 64 GiB batch keeps
@@ -500,20 +511,23 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
     const size_t o_task = off; off = align256(off + sizeof(Task) * std::max<size_t>(nt, 1));
     const size_t o_tagin = off; off = align256(off + 16 * (size_t)n);
     const size_t o_queue = off; off = align256(off + 4);  // persistent kernel's task counter (uploaded as 0)
+    const size_t o_crcin = off; if (hc_in) off = align256(off + 4 * crc_words);
     const size_t h_bytes = off;  // everything above is uploaded from the pinned mirror
     const size_t o_out = off; off = align256(off + sizeof(BlkOut) * n);
+    const size_t o_crcout = off; if (hc_out) off = align256(off + 4 * crc_words);
+    const size_t down = hc_out ? o_crcout + 4 * crc_words - o_out : sizeof(BlkOut) * n;
     const size_t o_sched = off; off = align256(off + (gcm ? sizeof(GcmSched) : sizeof(CpSched)) * n);
     const size_t o_part = off; off = align256(off + 32 * std::max<uint64_t>(plan.nslots, 1));
     const size_t o_pexp = off; off = align256(off + 4 * std::max<uint64_t>(plan.nslots, 1));
     const size_t o_calc = off; off = align256(off + 4 * std::max<uint64_t>(crc_calc_words, 1));
     int rc;
     if ((rc = ensure_dev(c, &w.d, &w.dcap, off))) return rc;
-    if ((rc = ensure_host(&w.h, &w.hcap, std::max(h_bytes, sizeof(BlkOut) * n)))) return rc;
+    if ((rc = ensure_host(&w.h, &w.hcap, std::max(h_bytes, down)))) return rc;
     char *h = w.h, *d = w.d;
     KeyIn *hk = (KeyIn *)(h + o_keys);
     BlkDev *hb = (BlkDev *)(h + o_blk);
     *(uint32_t *)(h + o_queue) = 0;
-    uint64_t calc = 0;
+    uint64_t calc = 0, cw = 0;
     for (int i = 0; i < n; i++) {
         const jfsx_blk &b = blks[i];
         memcpy(hk[i].key, b.key, 32);
@@ -523,6 +537,13 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
         hb[i].dst = (uint8_t *)b.dst;
         hb[i].len = b.len;
         hb[i].crc = b.crc;
+        if (hc_in) {
+            memcpy(h + o_crcin + 4 * cw, b.crc, 4 * nseg_of(b.len));
+            hb[i].crc = (uint8_t *)(d + o_crcin + 4 * cw);
+        } else if (hc_out) {
+            hb[i].crc = (uint8_t *)(d + o_crcout + 4 * cw);
+        }
+        cw += nseg_of(b.len);
         hb[i].crc_calc = nullptr;
         if ((crc_mode & 3) == JFSX_CRC_VERIFY) {
             hb[i].crc_calc = (uint32_t *)(d + o_calc) + calc;
@@ -577,7 +598,7 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
     }
     if ((crc_mode & 3) == JFSX_CRC_GEN)
         for (int i = 0; i < n; i++)
-            if (blks[i].len == 0) HIP_OK(hipMemsetAsync(blks[i].crc, 0, 4, s));
+            if (blks[i].len == 0) HIP_OK(hipMemsetAsync(hb[i].crc, 0, 4, s));
     if (c->timing) HIP_OK(hipEventRecord(k0, s));
     if (gcm)
         launch_gcm_main(s, (int)nt, c->ncu, dq, open, crc_mode, c->bitslice, dt, db, (const GcmSched *)(d + o_sched),
@@ -596,7 +617,10 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
         launch_cp_finalize(fs, n, open, crc_mode, db, (const CpSched *)(d + o_sched), dpart, dpexp, dout);
     HIP_OK(hipGetLastError());
     w.dout = dout;
-    if (collect) HIP_OK(hipMemcpyAsync(h, dout, sizeof(BlkOut) * n, hipMemcpyDeviceToHost, fs));
+    w.down = down;
+    w.crc_off = o_crcout - o_out;
+    w.crc_back = hc_out;
+    if (collect) HIP_OK(hipMemcpyAsync(h, dout, down, hipMemcpyDeviceToHost, fs));
     w.n = n;
     w.nt = nt;
     w.timed = c->timing;
@@ -619,6 +643,15 @@ int finish_aead(jfsx_ctx *c, Workspace &w, hipEvent_t k0, hipEvent_t k1, bool op
         b.crc_bad_seg = ho[i].bad_seg;
         b.crc_got = ho[i].got;
         b.crc_expect = ho[i].expect;
+    }
+    if (w.crc_back) {
+        const char *hw = w.h + w.crc_off;
+        for (int i = 0; i < w.n; i++) {
+            const size_t cb = 4 * nseg_of(blks[i].len);
+            memcpy(blks[i].crc, hw, cb);
+            hw += cb;
+        }
+        w.crc_back = false;
     }
     w.n = 0;
     w.nt = 0;
@@ -703,6 +736,7 @@ void pipe_collect(jfsx_ctx *c, PipeSlot &s) {
     if (e != hipSuccess) {
         note_hip_error(e, __FILE__, __LINE__, "hipEventSynchronize(pipeline slot)");
         g->rc = JFSX_EIO;
+        s.w.crc_back = false;
         s.w.n = 0;
         s.w.nt = 0;
         s.w.timed = false;
@@ -781,7 +815,7 @@ int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, int algo, bool open, int nb, const jf
         }
         dv[i].src = buf;
         dv[i].dst = direct ? blks[i].dst : buf;
-        if (crc_mode) {
+        if (crc_mode && direct) {
             char *cb = w.stage + coff;
             coff += align256(4 * nseg_of(blks[i].len));
             if ((crc_mode & 3) == JFSX_CRC_VERIFY)
@@ -794,7 +828,10 @@ int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, int algo, bool open, int nb, const jf
     // s_in and finalize onto s_out, to overlap them with neighbouring groups'
     // main kernels, measured 30-33 GB/s against 38-40 at 20 per-object callers:
     // the copy engines then wait behind those kernels.)
-    if ((rc = enqueue_aead(c, w, c->stream, s.ev_k0, s.ev_k1, algo, open, nb, dv, crc_mode, c->s_in, s.ev_in, false)))
+    // staged groups pass their CRC arrays through the descriptor upload and
+    // the result download (host_crc)
+    if ((rc = enqueue_aead(c, w, c->stream, s.ev_k0, s.ev_k1, algo, open, nb, dv, crc_mode, c->s_in, s.ev_in, false,
+                           nullptr, nullptr, !direct)))
         return rc;
     if (direct) {
         // outputs already in place: only the per-block results come down
@@ -825,23 +862,7 @@ int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, int algo, bool open, int nb, const jf
         if (align256(blks[i].len) != blks[i].len && (rc = flush_out())) return rc;
     }
     if ((rc = flush_out())) return rc;
-    if ((crc_mode & 3) == JFSX_CRC_GEN) {
-        // CRC arrays: one copy per run that is contiguous on both sides
-        for (int i = 0; i < nb; i++) {
-            const size_t cn = 4 * nseg_of(blks[i].len);
-            char *hd = (char *)blks[i].crc;
-            const char *dd = (const char *)dv[i].crc;
-            if (!(on && oh + on == hd && od + on == dd) && (rc = flush_out())) return rc;
-            if (!on) {
-                oh = hd;
-                od = dd;
-            }
-            on += cn;
-            if (align256(cn) != cn && (rc = flush_out())) return rc;
-        }
-        if ((rc = flush_out())) return rc;
-    }
-    HIP_OK(hipMemcpyAsync(w.h, w.dout, sizeof(BlkOut) * nb, hipMemcpyDeviceToHost, c->s_out));
+    HIP_OK(hipMemcpyAsync(w.h, w.dout, w.down, hipMemcpyDeviceToHost, c->s_out));
     HIP_OK(hipEventRecord(s.ev_out, c->s_out));
     return 0;
 }
@@ -1099,7 +1120,7 @@ int run_codec(jfsx_ctx *c, int n, jfsx_zblk *z, int mem, CodecOp op) {
     launch_begin();
     switch (op) {
     case kLz4Comp:
-        launch_lz4_compress(s, n, dz, dout, (uint32_t *)(w.d + o_tab));
+        launch_lz4_compress(s, n, c->ncu, dz, dout, (uint32_t *)(w.d + o_tab));
         break;
     case kLz4Decomp:
         launch_lz4_decompress(s, n, dz, dout);

@@ -1190,7 +1190,7 @@ __global__ __launch_bounds__(1024) void gcm_finalize_k(const BlkDev *__restrict_
     __shared__ uint32_t h2k[32][4];  // the block's H^(2^k), staged once (not a global load per product)
     const BlkDev blk = blks[b];
     const GcmSched *sc = sched + b;
-    if (tid < 128) h2k[tid >> 2][tid & 3] = sc->h2k[tid >> 2][tid & 3];
+    for (uint32_t i = tid; i < 128; i += nthr) h2k[i >> 2][i & 3] = sc->h2k[i >> 2][i & 3];  // 64-thread launches too
     __syncthreads();
     uint32_t acc[4] = {0, 0, 0, 0};
     for (uint32_t base = 0; base < blk.nslots; base += nthr) {

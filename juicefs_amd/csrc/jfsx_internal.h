@@ -303,7 +303,7 @@ void launch_gen_synthetic_batch(hipStream_t s, uint8_t *dst, uint64_t stride, in
                                 uint64_t seed, uint64_t block0);
 // tabs: n x 16 KiB of device memory, the blocks' LZ4 hash tables
 constexpr size_t kLz4TabBytes = 16384;
-void launch_lz4_compress(hipStream_t s, int n, const ZDev *blks, ZOut *outs, uint32_t *tabs);
+void launch_lz4_compress(hipStream_t s, int n, int ncu, const ZDev *blks, ZOut *outs, uint32_t *tabs);
 void launch_lz4_decompress(hipStream_t s, int n, const ZDev *blks, ZOut *outs);
 // Zstandard frames (jfsx_zstd.hip): scratch = n x kZstdScratch bytes (literal
 // buffer + the literal window's read-ahead, then a log-12 Huffman table)

@@ -32,6 +32,8 @@
 // only output written before it (overlapping matches are expanded as
 // out[op+i] = out[op-off+i%off]), from the ring, or from global memory once
 // the wave's stores of it have completed (s_waitcnt vmcnt(0)).
+#include <string.h>
+
 #include "jfsx_dev.h"
 
 namespace jfsx {
@@ -274,50 +276,97 @@ __device__ unsigned long long g_lz4_stamps[8];
     } while (0)
 #endif
 
+// The compressor's hash table.  Positions are absolute input offsets; get()
+// takes the reference position p of the probe (every entry was written at a
+// position <= p) and step(lo, hi) is called, wave-uniform, before each step
+// whose table accesses lie at positions in [lo, hi] (steps advance
+// monotonically).
+//
+// TabG: the table in global memory (16 KiB per block: 4096 x u32 for inputs
+// >= 64 KiB + 11 B, else 8192 x u16 as LZ4_compress_default), L2/MALL
+// resident; occupancy is then set by VGPRs (8 waves per SIMD).
+struct TabG {
+    typedef __attribute__((address_space(1))) uint32_t gtu32;
+    typedef __attribute__((address_space(1))) uint16_t gtu16;
+    gtu32 *T;
+    bool small;
+    __device__ __forceinline__ uint32_t get(uint32_t h, uint32_t) const {
+        return small ? (uint32_t)((gtu16 *)T)[h] : T[h];
+    }
+    __device__ __forceinline__ void put(uint32_t h, uint32_t v) const {
+        if (small) ((gtu16 *)T)[h] = (uint16_t)v;
+        else T[h] = v;
+    }
+    __device__ __forceinline__ void step(uint32_t, uint32_t, uint32_t) {}
+};
+
+// TabL: the 4096-entry table of inputs >= 64 KiB + 11 B in 9 KiB of LDS, each
+// entry the low 18 bits of its position (u16 + a 2-bit field), so 16 blocks
+// fit a CU (the 16 GiB / 4096-block batch is one wave per block on 16 waves per
+// CU: the global table's L2/MALL round trips are then the parse's latency).
+// A position is recovered relative to the probe, x = p - ((p - v) mod 2^18);
+// that is exact while every entry is younger than 2^18.  The only thing LZ4
+// asks of an entry older than 65535 bytes is that it fails the distance test
+// (LZ4_compress_generic: match + LZ4_DISTANCE_MAX < ip), so step() sweeps the
+// table whenever the parse has moved 64 KiB past the last sweep point and
+// rewrites every entry older than 65535 bytes as s - 65536 (still too far from
+// any later probe, and young enough to stay unambiguous until the next sweep).
+// Bounds (s_k sweep points, hi the highest position of the previous steps):
+// a live entry is <= 65535 + 96 KiB old at any read, a rewritten one between
+// 64 KiB and 160 KiB, both below 2^18.
+struct TabL {
+    uint16_t *lo;  // [4096]
+    uint32_t *hb;  // [256]: bits 16-17 of entry h at 2 * (h & 15) of word h >> 4
+    uint32_t sw, whi;  // last sweep point, highest position of the previous steps (wave-uniform)
+    __device__ __forceinline__ uint32_t get(uint32_t h, uint32_t p) const {
+        const uint32_t v = (uint32_t)lo[h] | (((hb[h >> 4] >> (2 * (h & 15))) & 3u) << 16);
+        return p - ((p - v) & 0x3FFFFu);
+    }
+    __device__ __forceinline__ void put(uint32_t h, uint32_t v) const {
+        lo[h] = (uint16_t)v;
+        const uint32_t sh = 2 * (h & 15);
+        atomicAnd(&hb[h >> 4], ~(3u << sh));
+        atomicOr(&hb[h >> 4], ((v >> 16) & 3u) << sh);
+    }
+    __device__ void sweep(uint32_t s, uint32_t lane) {
+        // lane owns words 4 lane .. 4 lane + 3 and their 64 entries
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t w = 4 * lane + k;
+            const uint32_t hw = hb[w];
+            uint32_t nw = 0;
+            for (uint32_t e = 0; e < 16; e++) {
+                const uint32_t i = 16 * w + e;
+                uint32_t v = (uint32_t)lo[i] | (((hw >> (2 * e)) & 3u) << 16);
+                if (((s - v) & 0x3FFFFu) > 65535u) v = (s - 65536u) & 0x3FFFFu;
+                lo[i] = (uint16_t)v;
+                nw |= ((v >> 16) & 3u) << (2 * e);
+            }
+            hb[w] = nw;
+        }
+    }
+    __device__ __forceinline__ void step(uint32_t lo_pos, uint32_t hi_pos, uint32_t lane) {
+        while (lo_pos - sw >= 65536u) {
+            const uint32_t s = min(lo_pos, max(sw + 65536u, whi));
+            sweep(s, lane);
+            sw = s;
+        }
+        whi = max(whi, hi_pos);
+    }
+};
+
 // One wave per block.  ZDev.len = input bytes, ZDev.cap >= LZ4_compressBound
 // (checked on the host); ZOut.out_len = compressed bytes.
 #ifndef JFSX_LZ4_K0
 #define JFSX_LZ4_K0 4
 #endif
-__global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ blks, ZOut *__restrict__ outs,
-                                                     uint32_t *__restrict__ tabs) {
-#ifdef JFSX_LZ4_LDS_TABLE
-    __shared__ uint32_t T[4096];
-    uint16_t *T16 = reinterpret_cast<uint16_t *>(T);
-#else
-    // The hash table in global memory (16 KiB per block, L2/MALL resident):
-    // occupancy is then set by VGPRs (8 waves per SIMD) instead of 16 KiB of
-    // LDS per wave (10 waves per CU).  A wave's own table reads and writes
-    // reach memory in program order, as LDS ones do.
-    typedef __attribute__((address_space(1))) uint32_t gtu32;
-    typedef __attribute__((address_space(1))) uint16_t gtu16;
-    gtu32 *T = (gtu32 *)(tabs + (size_t)blockIdx.x * 4096);
-    gtu16 *T16 = (gtu16 *)T;
-#endif
-    const uint32_t lane = threadIdx.x;
-    const ZDev b = blks[blockIdx.x];
-    const uint8_t *src = b.src;
-    uint8_t *dst = b.dst;
-    const uint32_t n = uni((uint32_t)b.len);
-    const Img I{(const uint8_t *)((uintptr_t)src & ~(uintptr_t)3), (uint32_t)((uintptr_t)src & 3), n};
-    const bool small = n < kLimit64K;
-#ifdef JFSX_LZ4_LDS_TABLE
-    for (uint32_t i = lane; i < 4096; i += 64) T[i] = 0;
-    __syncthreads();
-#else
-    for (uint32_t i = 4 * lane; i < 4096; i += 256) *(__attribute__((address_space(1))) v4u *)(T + i) = v4u{0, 0, 0, 0};
-#endif
-#define TGET(h) (small ? (uint32_t)T16[(h)] : T[(h)])
-#define TPUT(h, v)                            \
-    do {                                      \
-        if (small) T16[(h)] = (uint16_t)(v); \
-        else T[(h)] = (v);                   \
-    } while (0)
-
+template <class Tab>
+__device__ __forceinline__ void lz4c_block(Tab &T, const uint8_t *src, uint8_t *dst, const uint32_t n,
+                                           const Img &I, const bool small, const uint32_t lane, ZOut *out) {
     uint32_t op = 0, anchor = 0;
     if (n >= kMfLimit + 1) {
         const uint32_t mflimit1 = n - kMfLimit + 1, matchlimit = n - kLastLit;
-        if (lane == 0) TPUT(lz_hash(src, small), 0u);
+        T.step(0u, 0u, lane);
+        if (lane == 0) T.put(lz_hash(src, small), 0u);
         uint32_t ip = 1;
 #ifdef JFSX_LZ4_STAMP
         unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last;
@@ -356,8 +405,9 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
                     }
                     const uint32_t h = hash_of(cur, b4, small);
                     const uint64_t vmask = ballot(valid);  // a prefix of the lanes
+                    T.step(pf, pl, lane);
                     // probes against the table as it stood before this step
-                    const uint32_t mi0 = TGET(h);
+                    const uint32_t mi0 = T.get(h, pc);
                     const bool ok0 = valid && (small || mi0 + 65535u >= p) && ld32u(src + mi0) == cur;
                     const uint64_t okm0 = ballot(ok0);
                     uint32_t mi = mi0;
@@ -401,7 +451,7 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
                         const uint64_t ex = okm ? ((okm & (0ull - okm)) << 1) - 1ull : vmask;  // probes that ran
                         writer = ((ex >> lane) & 1ull) && !(eq & ex & ~below & ~(1ull << lane));
                     }
-                    if (writer) TPUT(h, p);
+                    if (writer) T.put(h, p);
                     if (okm) {
                         const int j = __builtin_ctzll(okm);
                         ip = uni(__builtin_amdgcn_readlane(p, j));
@@ -492,9 +542,10 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
                 }
                 const uint32_t hm2 = uni(hash_of(wm2, bm2, small));
                 const uint32_t h = uni(hash_of(w0, b0, small));
-                if (lane == 0) TPUT(hm2, ip - 2);
-                const uint32_t mi = uni(TGET(h));
-                if (lane == 0) TPUT(h, ip);
+                T.step(ip - 2, ip, lane);
+                if (lane == 0) T.put(hm2, ip - 2);
+                const uint32_t mi = uni(T.get(h, ip));
+                if (lane == 0) T.put(h, ip);
                 if (small || mi + 65535u >= ip) {
                     // the 4-byte test and the match length in one round of loads
                     uint32_t nb;
@@ -534,13 +585,46 @@ __global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ bl
         wave_copy(dst + op, src + anchor, run, lane);
         op += run;
     }
-#undef TGET
-#undef TPUT
     if (lane == 0) {
-        outs[blockIdx.x].out_len = op;
-        outs[blockIdx.x].status = JFSX_OK;
+        out->out_len = op;
+        out->status = JFSX_OK;
     }
 }
+
+__global__ __launch_bounds__(64) void lz4_compress_k(const ZDev *__restrict__ blks, ZOut *__restrict__ outs,
+                                                     uint32_t *__restrict__ tabs) {
+    const uint32_t lane = threadIdx.x;
+    const ZDev b = blks[blockIdx.x];
+    const uint32_t n = uni((uint32_t)b.len);
+    const Img I{(const uint8_t *)((uintptr_t)b.src & ~(uintptr_t)3), (uint32_t)((uintptr_t)b.src & 3), n};
+    TabG T{(TabG::gtu32 *)(tabs + (size_t)blockIdx.x * 4096), n < kLimit64K};
+    for (uint32_t i = 4 * lane; i < 4096; i += 256) *(__attribute__((address_space(1))) v4u *)(T.T + i) = v4u{0, 0, 0, 0};
+    lz4c_block(T, b.src, b.dst, n, I, T.small, lane, outs + blockIdx.x);
+}
+
+// the same with the large-input table in LDS (TabL); inputs below 64 KiB + 11 B
+// keep the u16 table in global memory
+__global__ __launch_bounds__(64) void lz4_compress_lds_k(const ZDev *__restrict__ blks, ZOut *__restrict__ outs,
+                                                         uint32_t *__restrict__ tabs) {
+    __shared__ uint16_t tlo[4096];
+    __shared__ uint32_t thb[256];
+    const uint32_t lane = threadIdx.x;
+    const ZDev b = blks[blockIdx.x];
+    const uint32_t n = uni((uint32_t)b.len);
+    const Img I{(const uint8_t *)((uintptr_t)b.src & ~(uintptr_t)3), (uint32_t)((uintptr_t)b.src & 3), n};
+    if (n < kLimit64K) {
+        TabG T{(TabG::gtu32 *)(tabs + (size_t)blockIdx.x * 4096), true};
+        for (uint32_t i = 4 * lane; i < 4096; i += 256)
+            *(__attribute__((address_space(1))) v4u *)(T.T + i) = v4u{0, 0, 0, 0};
+        lz4c_block(T, b.src, b.dst, n, I, true, lane, outs + blockIdx.x);
+        return;
+    }
+    for (uint32_t i = lane; i < 2048; i += 64) reinterpret_cast<uint32_t *>(tlo)[i] = 0u;
+    for (uint32_t i = lane; i < 256; i += 64) thb[i] = 0u;
+    TabL T{tlo, thb, 0u, 0u};
+    lz4c_block(T, b.src, b.dst, n, I, false, lane, outs + blockIdx.x);
+}
+
 
 namespace {
 
@@ -956,8 +1040,16 @@ extern "C" int jfsx_debug_lz4_stamps(unsigned long long *out, int reset) {
 namespace jfsx {
 #endif
 
-void launch_lz4_compress(hipStream_t s, int n, const ZDev *blks, ZOut *outs, uint32_t *tabs) {
-    if (n > 0) hipLaunchKernelGGL(lz4_compress_k, dim3(n), dim3(64), 0, s, blks, outs, tabs);
+// LDS table while every block of the batch is resident at once (up to 16
+// blocks per CU: the parse is then latency-bound), global-memory table for
+// bigger batches (32 waves per CU).  JFSX_LZ4_TABLE=lds|global overrides.
+void launch_lz4_compress(hipStream_t s, int n, int ncu, const ZDev *blks, ZOut *outs, uint32_t *tabs) {
+    if (n <= 0) return;
+    const char *e = getenv("JFSX_LZ4_TABLE");  // read per launch (tests switch it)
+    const int mode = !e ? 0 : !strcmp(e, "lds") ? 1 : !strcmp(e, "global") ? 2 : 0;
+    const bool lds = mode == 1 || (mode == 0 && n <= 16 * ncu);
+    if (lds) hipLaunchKernelGGL(lz4_compress_lds_k, dim3(n), dim3(64), 0, s, blks, outs, tabs);
+    else hipLaunchKernelGGL(lz4_compress_k, dim3(n), dim3(64), 0, s, blks, outs, tabs);
 }
 
 void launch_lz4_decompress(hipStream_t s, int n, const ZDev *blks, ZOut *outs) {

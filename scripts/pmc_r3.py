@@ -32,7 +32,7 @@ KERNELS = {  # variant -> kernel-name prefix of the dominant kernel
     "seal_chacha": "void jfsx::cp_main_k<false", "open_chacha": "void jfsx::cp_main_k<true",
     "seal_chacha_ragged": "void jfsx::cp_main_k<false", "open_chacha_ragged": "void jfsx::cp_main_k<true",
     "crc_verify": "jfsx::crc_segments_k", "zstd_text": "jfsx::zstd_compress_k",
-    "unzstd_text": "jfsx::zstd_decompress", "lz4_text": "jfsx::lz4_compress_k",
+    "unzstd_text": "jfsx::zstd_decompress", "lz4_text": "jfsx::lz4_compress_",  # _k (global table) or _lds_k
     "unlz4_text": "void jfsx::lz4_decompress_k",
 }
 CUS, XCDS = 256, 8

@@ -119,3 +119,16 @@ def test_bench_host_pool_is_capped():
     assert rec["resident_blocks"] == 2048 and rec["loops_per_step"] == 8
     rec = _bench_dry(["--gpus", "2", "--mem", "host", "--total-gib", "256", "--host-pool-gib", "8"])
     assert rec["blocks_total"] == 65536 and rec["resident_blocks"] == 2048 and rec["loops_per_step"] == 16
+
+
+def test_bench_host_pool_cap_holds_at_eight_ranks():
+    """The 8-GPU node's host ingest (gloo stand-in for the 8 ranks): each rank
+    pins at most the cap (--host-pool-gib in and out, plus CRC arrays) while
+    the ranks together cover the whole strong total."""
+    cap = 8
+    rec = _bench_dry(["--gpus", "8", "--mem", "host", "--total-gib", "2048", "--host-pool-gib", str(cap)])
+    assert rec["n_gpus"] == 8 and rec["blocks_total"] == 524288 and rec["block_range"] == [0, 524288]
+    assert rec["per_gpu_blocks_max"] == 65536 and rec["resident_blocks"] == 2048
+    assert rec["pinned_bytes_per_rank_max"] <= 2 * cap * 2**30 + 2048 * 512
+    assert rec["pinned_bytes_per_rank_max"] >= 2 * cap * 2**30
+

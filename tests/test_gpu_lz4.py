@@ -47,6 +47,42 @@ def test_large_blocks(eng, n):
         assert st == E.OK and d == src
 
 
+def _stale_entry_block(n, seed):
+    """Random bytes with 16-byte phrases repeated at distances around the
+    LZ4 window (65535 / 65536) and the LDS table's 2^17 / 2^18 position
+    aliases, plus zero runs longer than 64 KiB (the parse jumps past several
+    sweep points at once)."""
+    rng = np.random.default_rng(seed)
+    b = bytearray(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+    pos = 4096
+    for d in (65531, 65532, 65535, 65536, 65537, 131071, 131072, 131073, 196608, 262143, 262144, 262145,
+              262144 + 65535, 327680):
+        ph = rng.integers(0, 256, 16, dtype=np.uint8).tobytes()
+        if pos + d + 16 < n:
+            b[pos:pos + 16] = ph
+            b[pos + d:pos + d + 16] = ph
+        pos += 1031
+    for z0, zl in ((n // 3, 200000), (n // 2 + 7, 70001), (n - 140000, 131073)):
+        if z0 + zl < n:
+            b[z0:z0 + zl] = bytes(zl)
+    return bytes(b)
+
+
+@pytest.mark.parametrize("table", ["lds", "global"])
+def test_table_kinds_match_oracle(eng, table, monkeypatch):
+    """Both compressor tables (JFSX_LZ4_TABLE: the 18-bit LDS table with its
+    64 KiB sweeps, the u32 global table) give the library's bytes: phrases
+    repeated across the 64 KiB window and the LDS table's position aliases,
+    long zero runs, and 4 MiB text / random / runs blocks."""
+    monkeypatch.setenv("JFSX_LZ4_TABLE", table)
+    srcs = [_stale_entry_block(1 << 20, 11), _stale_entry_block((3 << 20) + 77, 12)]
+    srcs += [lz4_data.sample(k, 4 << 20, seed=21) for k in ("text", "random", "runs")]
+    srcs += [lz4_data.sample("text", 70000, seed=22), lz4_data.sample("text", 65546, seed=23)]
+    outs = eng.lz4_compress(srcs)
+    for i, (src, out) in enumerate(zip(srcs, outs)):
+        assert out == orc.lz4_compress(src), (table, i, len(src))
+
+
 def test_device_batch_ragged_unaligned(eng):
     """Device-resident batch: ragged lengths, src/dst at odd offsets."""
     rng = np.random.default_rng(5)

@@ -240,6 +240,38 @@ def test_large_batch_sample_vs_oracle(eng, algo):
 
 
 @pytest.mark.parametrize("algo", [E.AES256GCM, E.CHACHA20P1305])
+def test_large_tasks_few_slots_vs_oracle(eng, algo):
+    """A batch big enough that each 2 MiB block is cut into only 3 tasks: the
+    finalize kernel then runs 64 threads per block while the slots' lifts
+    reach H^(2^17) (the 64 GiB bench shape; a 64-thread finalize once staged
+    only the first 16 powers).  Every tag and CRC array against the oracle,
+    then Open of every block."""
+    nb, L, seed = 200, 2 << 20, 0x4A465322
+    src, dst, crc = eng.alloc(nb * L), eng.alloc(nb * L), eng.alloc(nb * 256)
+    eng.gen_synthetic_batch(src, L, [L] * nb, seed, 0)
+    specs = []
+    for b in range(nb):
+        key, nonce = orc.gen_key(seed, b)
+        specs.append({"key": key, "nonce": nonce, "src": src.ptr + b * L, "dst": dst.ptr + b * L, "len": L,
+                      "crc": crc.ptr + 256 * b})
+    eng.sync()
+    arr, n = eng.make_blocks(specs)
+    eng.seal_batch(algo, arr, n, E.CRC_GEN, E.MEM_DEVICE)
+    tags, crcs, _ = orc.expect_batch(ORC[algo], 8, [L] * nb, seed, 0, 256)
+    got = np.frombuffer(b"".join(bytes(arr[b].tag) for b in range(nb)), np.uint8).reshape(nb, 16)
+    assert (got == tags).all(axis=1).all(), np.nonzero(~(got == tags).all(axis=1))[0][:5]
+    assert (crc.download().reshape(nb, 256) == crcs).all()
+    for b in (0, nb - 1):
+        key, nonce = orc.gen_key(seed, b)
+        c, _ = orc.seal(ORC[algo], key, nonce, orc.gen_block(seed, b, L), fast=True)
+        assert dst.download(L, offset=b * L).tobytes() == c, b
+    ospecs = [dict(s, src=s["dst"], dst=s["src"], tag=bytes(arr[b].tag)) for b, s in enumerate(specs)]
+    oarr, n = eng.make_blocks(ospecs)
+    eng.open_batch(algo, oarr, n, E.CRC_VERIFY, E.MEM_DEVICE)
+    assert all(oarr[b].status == E.OK for b in range(nb))
+
+
+@pytest.mark.parametrize("algo", [E.AES256GCM, E.CHACHA20P1305])
 def test_host_ingest_pipeline_ring(eng, algo):
     """MEM_HOST batches streamed through the 3-slot ring (1 MiB slots -> many
     groups), seal + CRC and open + verify, one tag failure wiped on Open."""

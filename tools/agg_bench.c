@@ -5,10 +5,14 @@
  * Reports GB/s of plaintext for the aggregator and for direct one-block
  * jfsx_seal_batch calls, to separate the engine from the Python harness.
  *
- * usage: agg_bench [threads=20] [blocks=512] [passes=4] [max_mb=16] [window_us=500]
+ * usage: agg_bench [threads=20] [blocks=512] [passes=4] [max_mb=16] [window_us=500] [numa=0]
+ * numa=1 binds the pinned blocks to the GPU's NUMA node and runs the threads
+ * on that node's CPUs (as bench.py's host ingest does).
  * build: cc -O2 -o tools/agg_bench tools/agg_bench.c -Iinclude -Ljuicefs_amd -ljfsx -lpthread \
  *        -Wl,-rpath,'$ORIGIN/../juicefs_amd' */
+#define _GNU_SOURCE
 #include <pthread.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -65,9 +69,36 @@ int main(int argc, char **argv) {
     if (argc > 3) PASSES = atoi(argv[3]);
     const uint64_t max_mb = argc > 4 ? strtoull(argv[4], 0, 10) : 16;
     const uint32_t window = argc > 5 ? (uint32_t)atoi(argv[5]) : 500;
+    const int numa = argc > 6 ? atoi(argv[6]) : 0;
+    int node = -1;
+    if (numa && jfsx_device_numa_node(0, &node) == 0 && node >= 0) {
+        char path[96], list[4096];
+        snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+        FILE *f = fopen(path, "r");
+        if (f && fgets(list, sizeof list, f)) {
+            cpu_set_t set;
+            CPU_ZERO(&set);
+            for (char *p = list; *p && *p != '\n';) {
+                const long a = strtol(p, &p, 10);
+                const long b = *p == '-' ? strtol(p + 1, &p, 10) : a;
+                for (long c = a; c <= b; c++) CPU_SET((int)c, &set);
+                if (*p == ',') p++;
+            }
+            cpu_set_t cur;
+            sched_getaffinity(0, sizeof cur, &cur);
+            CPU_AND(&set, &set, &cur);
+            if (CPU_COUNT(&set)) sched_setaffinity(0, sizeof set, &set);
+        }
+        if (f) fclose(f);
+    }
     if (jfsx_ctx_open(0, 0, &ctx)) return 1;
-    if (jfsx_alloc_pinned(ctx, NB * L, (void **)&hin) || jfsx_alloc_pinned(ctx, NB * L, (void **)&hout) ||
-        jfsx_alloc_pinned(ctx, NB * 512, (void **)&hcrc))
+    if (node >= 0) {
+        if (jfsx_alloc_pinned_node(ctx, NB * L, node, (void **)&hin) ||
+            jfsx_alloc_pinned_node(ctx, NB * L, node, (void **)&hout) ||
+            jfsx_alloc_pinned_node(ctx, NB * 512, node, (void **)&hcrc))
+            return 1;
+    } else if (jfsx_alloc_pinned(ctx, NB * L, (void **)&hin) || jfsx_alloc_pinned(ctx, NB * L, (void **)&hout) ||
+               jfsx_alloc_pinned(ctx, NB * 512, (void **)&hcrc))
         return 1;
     for (uint64_t i = 0; i < NB * L; i += 8) *(uint64_t *)(hin + i) = i * 0x9E3779B97F4A7C15ull;
     use_agg = 0;
@@ -85,8 +116,8 @@ int main(int argc, char **argv) {
     uint64_t calls, batches, blocks;
     jfsx_agg_stats(agg, &calls, &batches, &blocks);
     printf("{\"threads\": %d, \"blocks\": %d, \"passes\": %d, \"max_mb\": %llu, \"window_us\": %u, "
-           "\"direct_GBs\": %.2f, \"agg_GBs\": %.2f, \"agg_batches\": %llu, \"agg_calls\": %llu}\n",
-           T, NB, passes, (unsigned long long)max_mb, window, direct, aggr, (unsigned long long)batches,
+           "\"numa_node\": %d, \"direct_GBs\": %.2f, \"agg_GBs\": %.2f, \"agg_batches\": %llu, \"agg_calls\": %llu}\n",
+           T, NB, passes, (unsigned long long)max_mb, window, node, direct, aggr, (unsigned long long)batches,
            (unsigned long long)calls);
     jfsx_agg_free(agg);
     jfsx_free_pinned(ctx, hin);
