@@ -1,0 +1,1 @@
+bench.py --engine mctx --steps 10 --warmup 2 --no-cpu

@@ -7,6 +7,8 @@
 //      over PCIe) and host -> device (global loads over PCIe), 4 MiB per block
 // Build: hipcc --offload-arch=gfx950 -O2 -o tools/copy_probe tools/copy_probe.hip
 #include <hip/hip_runtime.h>
+
+#include <chrono>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -237,6 +239,40 @@ int main() {
             }
             printf("SDMA duplex, %3zu MiB copies: %8.2f GB/s per direction\n", c3 >> 20, total / best / 1e6);
         }
+    }
+    // SDMA duplex with 4 MiB copies spread round-robin over k streams per
+    // direction (more copy engines / queues in flight per direction?)
+    for (int k : {1, 2, 4}) {
+        hipStream_t a[4], b[4];
+        for (int j = 0; j < k; j++) {
+            CK(hipStreamCreateWithFlags(&a[j], hipStreamNonBlocking));
+            CK(hipStreamCreateWithFlags(&b[j], hipStreamNonBlocking));
+        }
+        void *h2 = nullptr, *d2 = nullptr;
+        CK(hipHostMalloc(&h2, total, hipHostMallocPortable));
+        CK(hipMalloc(&d2, total));
+        const size_t c2 = 4 << 20;
+        const int m = (int)(total / c2);
+        double best = 1e30;
+        for (int rep = 0; rep < 3; rep++) {
+            CK(hipDeviceSynchronize());
+            const auto t0 = std::chrono::steady_clock::now();
+            for (int i = 0; i < m; i++) {
+                CK(hipMemcpyAsync((char *)d + i * c2, (char *)h + i * c2, c2, hipMemcpyHostToDevice, a[i % k]));
+                CK(hipMemcpyAsync((char *)h2 + i * c2, (char *)d2 + i * c2, c2, hipMemcpyDeviceToHost, b[i % k]));
+            }
+            CK(hipDeviceSynchronize());
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            if (ms < best) best = ms;
+        }
+        printf("SDMA duplex, 4 MiB copies over %d stream(s) per direction: %8.2f GB/s per direction\n", k,
+               total / best / 1e6);
+        for (int j = 0; j < k; j++) {
+            CK(hipStreamDestroy(a[j]));
+            CK(hipStreamDestroy(b[j]));
+        }
+        CK(hipHostFree(h2));
+        CK(hipFree(d2));
     }
     printf("copy probe ok\n");
     return 0;
