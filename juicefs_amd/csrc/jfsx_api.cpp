@@ -283,6 +283,7 @@ struct jfsx_ctx {
     // (groups, us enqueueing under mu, us waiting for a busy slot, us waiting
     // for one's own groups)
     std::atomic<uint64_t> ps_groups{0}, ps_enq_us{0}, ps_slot_us{0}, ps_own_us{0};
+    std::atomic<uint64_t> ps_blocks{0}, ps_h2d{0}, ps_d2h{0};  // blocks, data copies up / down (coalesced runs)
     std::mutex stat_mu; // met, ms_total, launches
     std::atomic<size_t> slot_bytes{(size_t)256 << 20};
     int ncu = 256;  // compute units: persistent transform kernels launch one workgroup per CU
@@ -792,15 +793,28 @@ int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, int algo, bool open, int nb, const jf
     if ((rc = ensure_dev(c, &w.stage, &w.scap, std::max<size_t>(need, 256)))) return rc;
     size_t off = 0, coff = 0;
     for (int i = 0; i < nb; i++) coff += align256(blks[i].len);
+    // staging in the order of the callers' source addresses: blocks that are
+    // neighbours in host memory (pages of one pinned pool) then sit side by
+    // side in staging too, and their copies coalesce both ways whatever order
+    // the callers submitted them in
+    std::vector<int> ord(nb);
+    for (int i = 0; i < nb; i++) ord[i] = i;
+    if (nb > 1)
+        std::stable_sort(ord.begin(), ord.end(),
+                         [&](int a, int b) { return (uintptr_t)blks[a].src < (uintptr_t)blks[b].src; });
     const char *run_h = nullptr;
     char *run_d = nullptr;
     size_t run_n = 0;
     auto flush_in = [&]() -> int {
-        if (run_n) HIP_OK(hipMemcpyAsync(run_d, run_h, run_n, hipMemcpyHostToDevice, c->s_in));
+        if (run_n) {
+            HIP_OK(hipMemcpyAsync(run_d, run_h, run_n, hipMemcpyHostToDevice, c->s_in));
+            c->ps_h2d++;
+        }
         run_n = 0;
         return 0;
     };
-    for (int i = 0; i < nb; i++) {
+    for (int k = 0; k < nb; k++) {
+        const int i = ord[k];
         char *buf = w.stage + off;
         off += align256(blks[i].len);
         if (blks[i].len) {
@@ -845,11 +859,15 @@ int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, int algo, bool open, int nb, const jf
     const char *od = nullptr;
     size_t on = 0;
     auto flush_out = [&]() -> int {
-        if (on) HIP_OK(hipMemcpyAsync(oh, od, on, hipMemcpyDeviceToHost, c->s_out));
+        if (on) {
+            HIP_OK(hipMemcpyAsync(oh, od, on, hipMemcpyDeviceToHost, c->s_out));
+            c->ps_d2h++;
+        }
         on = 0;
         return 0;
     };
-    for (int i = 0; i < nb; i++) {
+    for (int k = 0; k < nb; k++) {
+        const int i = ord[k];
         if (!blks[i].len) continue;
         char *hd = (char *)blks[i].dst;
         const char *dd = (const char *)dv[i].dst;
@@ -900,6 +918,7 @@ int run_aead_host(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int c
         c->ps_slot_us += us(t0, t1);
         c->ps_enq_us += us(t1, SClock::now());
         c->ps_groups++;
+        c->ps_blocks += (uint64_t)(groups[g].second - groups[g].first);
         if (rc) {
             (void)hipStreamSynchronize(c->s_in);
             (void)hipStreamSynchronize(c->stream);
@@ -1293,8 +1312,10 @@ int jfsx_ctx_open(int device, uint32_t flags, jfsx_ctx **out) {
 int jfsx_ctx_close(jfsx_ctx *c) {
     if (!c) return JFSX_EINVAL;
     if (getenv("JFSX_PIPE_STATS") && c->ps_groups)
-        fprintf(stderr, "jfsx pipe stats (device %d): %llu groups, enqueue %.1f us/group, slot wait %.1f us/group, "
-                "own wait %.1f us/group\n", c->device, (unsigned long long)c->ps_groups.load(),
+        fprintf(stderr, "jfsx pipe stats (device %d): %llu groups, %llu blocks, %llu H2D / %llu D2H data copies, "
+                "enqueue %.1f us/group, slot wait %.1f us/group, own wait %.1f us/group\n", c->device,
+                (unsigned long long)c->ps_groups.load(), (unsigned long long)c->ps_blocks.load(),
+                (unsigned long long)c->ps_h2d.load(), (unsigned long long)c->ps_d2h.load(),
                 c->ps_enq_us.load() / (double)c->ps_groups, c->ps_slot_us.load() / (double)c->ps_groups,
                 c->ps_own_us.load() / (double)c->ps_groups);
     async_detach(c);  // queued _async batches run first (jfsx_agg.cpp)

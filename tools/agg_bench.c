@@ -5,9 +5,14 @@
  * Reports GB/s of plaintext for the aggregator and for direct one-block
  * jfsx_seal_batch calls, to separate the engine from the Python harness.
  *
- * usage: agg_bench [threads=20] [blocks=512] [passes=4] [max_mb=16] [window_us=500] [numa=0]
+ * usage: agg_bench [threads=20] [blocks=512] [passes=4] [max_mb=16] [window_us=500] [numa=0] [layout=0]
  * numa=1 binds the pinned blocks to the GPU's NUMA node and runs the threads
  * on that node's CPUs (as bench.py's host ingest does).
+ * layout=0: thread t seals blocks t, t + T, ... of one pinned arena, so the
+ * blocks in flight together are neighbours (a shim that hands out pages of
+ * one pinned pool in order); layout=1: thread t owns a contiguous range of
+ * blocks, so no two blocks in flight are adjacent (every caller with its own
+ * buffers).
  * build: cc -O2 -o tools/agg_bench tools/agg_bench.c -Iinclude -Ljuicefs_amd -ljfsx -lpthread \
  *        -Wl,-rpath,'$ORIGIN/../juicefs_amd' */
 #define _GNU_SOURCE
@@ -25,7 +30,7 @@ static const uint64_t L = 4 << 20;
 static uint8_t *hin, *hout, *hcrc;
 static jfsx_ctx *ctx;
 static jfsx_agg *agg;
-static int use_agg;
+static int use_agg, layout;
 
 static double now(void) {
     struct timespec ts;
@@ -36,8 +41,10 @@ static double now(void) {
 static void *worker(void *vp) {
     const int t = (int)(intptr_t)vp;
     jfsx_blk *b = calloc(1, sizeof(jfsx_blk));
+    const int per = NB / T;
     for (int pass = 0; pass < PASSES; pass++)
-        for (int i = t; i < NB; i += T) {
+        for (int k = 0; layout ? k < per : t + k * T < NB; k++) {
+            const int i = layout ? t * per + k : t + k * T;
             memset(b, 0, sizeof(*b));
             jfsx_gen_key(7, (uint64_t)i, b->key, b->nonce);
             b->src = hin + (uint64_t)i * L;
@@ -60,7 +67,8 @@ static double run(void) {
     const double t0 = now();
     for (int t = 0; t < T; t++) pthread_create(&th[t], NULL, worker, (void *)(intptr_t)t);
     for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
-    return (double)NB * L * PASSES / (now() - t0) / 1e9;
+    const double blocks = layout ? (double)(NB / T) * T : (double)NB;
+    return blocks * L * PASSES / (now() - t0) / 1e9;
 }
 
 int main(int argc, char **argv) {
@@ -70,6 +78,7 @@ int main(int argc, char **argv) {
     const uint64_t max_mb = argc > 4 ? strtoull(argv[4], 0, 10) : 16;
     const uint32_t window = argc > 5 ? (uint32_t)atoi(argv[5]) : 500;
     const int numa = argc > 6 ? atoi(argv[6]) : 0;
+    layout = argc > 7 ? atoi(argv[7]) : 0;
     int node = -1;
     if (numa && jfsx_device_numa_node(0, &node) == 0 && node >= 0) {
         char path[96], list[4096];
@@ -116,8 +125,8 @@ int main(int argc, char **argv) {
     uint64_t calls, batches, blocks;
     jfsx_agg_stats(agg, &calls, &batches, &blocks);
     printf("{\"threads\": %d, \"blocks\": %d, \"passes\": %d, \"max_mb\": %llu, \"window_us\": %u, "
-           "\"numa_node\": %d, \"direct_GBs\": %.2f, \"agg_GBs\": %.2f, \"agg_batches\": %llu, \"agg_calls\": %llu}\n",
-           T, NB, passes, (unsigned long long)max_mb, window, node, direct, aggr, (unsigned long long)batches,
+           "\"numa_node\": %d, \"layout\": %d, \"direct_GBs\": %.2f, \"agg_GBs\": %.2f, \"agg_batches\": %llu, \"agg_calls\": %llu}\n",
+           T, NB, passes, (unsigned long long)max_mb, window, node, layout, direct, aggr, (unsigned long long)batches,
            (unsigned long long)calls);
     jfsx_agg_free(agg);
     jfsx_free_pinned(ctx, hin);
