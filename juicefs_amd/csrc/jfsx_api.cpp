@@ -79,31 +79,6 @@ struct CtxScope {
 std::shared_mutex g_alloc_mu;
 std::map<uintptr_t, std::pair<uintptr_t, int>> g_allocs;  // base -> (end, device)
 
-// Pinned host allocations made by the engine (jfsx_alloc_pinned*): the host
-// pipeline lets a kernel write straight into them.  Memory the engine did not
-// pin (pageable caller buffers) is never written by a kernel: the GPU cannot
-// fault in pageable pages.
-std::shared_mutex g_pin_mu;
-std::map<uintptr_t, uintptr_t> g_pins;  // base -> end
-
-void note_pinned(void *p, size_t bytes) {
-    std::unique_lock<std::shared_mutex> g(g_pin_mu);
-    g_pins[(uintptr_t)p] = (uintptr_t)p + bytes;
-}
-void forget_pinned(void *p) {
-    std::unique_lock<std::shared_mutex> g(g_pin_mu);
-    g_pins.erase((uintptr_t)p);
-}
-// [p, p + n) lies inside one engine-pinned allocation
-bool in_pinned(const void *p, uint64_t n) {
-    const uintptr_t a = (uintptr_t)p;
-    std::shared_lock<std::shared_mutex> g(g_pin_mu);
-    auto it = g_pins.upper_bound(a);
-    if (it == g_pins.begin()) return false;
-    --it;
-    return a >= it->first && a + n <= it->second && a + n >= a;
-}
-
 void note_alloc(void *p, size_t bytes, int device) {
     std::unique_lock<std::shared_mutex> g(g_alloc_mu);
     g_allocs[(uintptr_t)p] = {(uintptr_t)p + bytes, device};
@@ -698,10 +673,9 @@ int run_aead(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mo
     return open ? wipe_failed(c->stream, n, blks, crc_mode, true) : 0;
 }
 
-// staging bytes of one host block in a pipeline slot: data, then its CRC array
-inline size_t host_need(const jfsx_blk &b, int crc_mode) {
-    return align256(b.len) + (crc_mode ? align256(4 * nseg_of(b.len)) : 0);
-}
+// staging bytes of one host block in a pipeline slot (its CRC array rides the
+// slot's descriptor upload / result download instead)
+inline size_t host_need(const jfsx_blk &b, int) { return align256(b.len); }
 
 // The groups of a host batch: runs of blocks of up to slot_bytes; a batch
 // smaller than a few slots is cut into about 6 groups (>= 16 MiB each) so that
@@ -747,52 +721,21 @@ void pipe_collect(jfsx_ctx *c, PipeSlot &s) {
 }
 
 // One group into an empty slot (c->mu and s.mu held): the blocks' data runs up
-// on s_in into the slot's staging (all data first, coalesced where the
-// caller's blocks are adjacent, then the CRC arrays), keysetup / main /
-// finalize on the transform stream, and the outputs, CRC arrays and BlkOut
-// records down on s_out, chained by the slot's events.  dv[i] (the call's copy
-// of blks[i]) is pointed at the staging copy.
-// Small groups (the per-object path) whose outputs lie in engine-pinned
-// memory have the transform kernel write them straight into the caller's
-// buffers (ciphertext rows and CRC words over PCIe, zero-copy), so the group's
-// only D2H is its BlkOut records: SDMA runs device-to-host copies of a few MiB at ~20 GB/s
-// (tools/copy_probe.hip: 4 MiB in 203 us) while a kernel's stores reach
-// ~40 GB/s beside SDMA H2D.  Large groups (host ingest's 256 MiB slots) keep
-// staged SDMA copies, which reach the full duplex rate at that size.
-// JFSX_DIRECT_MAX_MB sets the largest direct group (0: never).
-size_t direct_max_bytes() {
-    static const size_t v = [] {
-        const char *e = getenv("JFSX_DIRECT_MAX_MB");
-        return (e ? (size_t)atoll(e) : (size_t)0) << 20;
-    }();
-    return v;
-}
-
-// a group goes direct when it is small and every output lies, aligned, in
-// engine-pinned memory (a kernel cannot write pageable host memory)
-bool group_direct(int nb, const jfsx_blk *blks, int crc_mode) {
-    size_t bytes = 0;
-    for (int i = 0; i < nb; i++) bytes += blks[i].len;
-    if (bytes > direct_max_bytes()) return false;
-    for (int i = 0; i < nb; i++) {
-        const jfsx_blk &b = blks[i];
-        if (!b.len || ((uintptr_t)b.dst & 15) || !in_pinned(b.dst, b.len)) return false;
-        if ((crc_mode & 3) == JFSX_CRC_GEN && (((uintptr_t)b.crc & 3) || !in_pinned(b.crc, 4 * nseg_of(b.len))))
-            return false;
-    }
-    return true;
-}
-
+// on s_in into the slot's staging (coalesced where the callers' blocks are
+// adjacent), then the descriptors with any VERIFY CRC arrays; keysetup / main
+// / finalize on the transform stream; the outputs, then the BlkOut records
+// with any GEN CRC arrays, down on s_out, chained by the slot's events.  dv[i]
+// (the call's copy of blks[i]) is pointed at the staging copy.  (A variant
+// whose kernel wrote the outputs straight into engine-pinned caller memory
+// over PCIe ran at 25 GB/s against 38.7 staged and was removed.)
 int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, int algo, bool open, int nb, const jfsx_blk *blks, jfsx_blk *dv,
                  int crc_mode) {
     Workspace &w = s.w;
-    const bool direct = group_direct(nb, blks, crc_mode);
     size_t need = 0;
     for (int i = 0; i < nb; i++) need += host_need(blks[i], crc_mode);
     int rc;
     if ((rc = ensure_dev(c, &w.stage, &w.scap, std::max<size_t>(need, 256)))) return rc;
-    size_t off = 0, coff = 0;
-    for (int i = 0; i < nb; i++) coff += align256(blks[i].len);
+    size_t off = 0;
     // staging in the order of the callers' source addresses: blocks that are
     // neighbours in host memory (pages of one pinned pool) then sit side by
     // side in staging too, and their copies coalesce both ways whatever order
@@ -828,31 +771,18 @@ int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, int algo, bool open, int nb, const jf
             if (align256(blks[i].len) != blks[i].len && (rc = flush_in())) return rc;
         }
         dv[i].src = buf;
-        dv[i].dst = direct ? blks[i].dst : buf;
-        if (crc_mode && direct) {
-            char *cb = w.stage + coff;
-            coff += align256(4 * nseg_of(blks[i].len));
-            if ((crc_mode & 3) == JFSX_CRC_VERIFY)
-                HIP_OK(hipMemcpyAsync(cb, blks[i].crc, 4 * nseg_of(blks[i].len), hipMemcpyHostToDevice, c->s_in));
-            dv[i].crc = direct && (crc_mode & 3) == JFSX_CRC_GEN ? blks[i].crc : (uint8_t *)cb;
-        }
+        dv[i].dst = buf;
     }
     if ((rc = flush_in())) return rc;
     // keysetup, main and finalize on the compute stream.  (Moving keysetup onto
     // s_in and finalize onto s_out, to overlap them with neighbouring groups'
     // main kernels, measured 30-33 GB/s against 38-40 at 20 per-object callers:
     // the copy engines then wait behind those kernels.)
-    // staged groups pass their CRC arrays through the descriptor upload and
-    // the result download (host_crc)
+    // the CRC arrays pass through the descriptor upload and the result
+    // download (host_crc)
     if ((rc = enqueue_aead(c, w, c->stream, s.ev_k0, s.ev_k1, algo, open, nb, dv, crc_mode, c->s_in, s.ev_in, false,
-                           nullptr, nullptr, !direct)))
+                           nullptr, nullptr, true)))
         return rc;
-    if (direct) {
-        // outputs already in place: only the per-block results come down
-        HIP_OK(hipMemcpyAsync(w.h, w.dout, sizeof(BlkOut) * nb, hipMemcpyDeviceToHost, c->stream));
-        HIP_OK(hipEventRecord(s.ev_out, c->stream));
-        return 0;
-    }
     HIP_OK(hipEventRecord(s.ev_comp, c->stream));
     HIP_OK(hipStreamWaitEvent(c->s_out, s.ev_comp, 0));
     char *oh = nullptr;
@@ -1474,7 +1404,6 @@ int jfsx_alloc_pinned(jfsx_ctx *c, size_t bytes, void **p) {
     // portable: the multi-device context's other GPUs DMA from it as well
     const hipError_t e = hipHostMalloc(p, bytes, hipHostMallocPortable);
     if (e == hipSuccess) {
-        note_pinned(*p, bytes);
         return 0;
     }
     note_hip_error(e, __FILE__, __LINE__, "hipHostMalloc(pinned)");
@@ -1529,7 +1458,6 @@ int jfsx_alloc_pinned_node(jfsx_ctx *c, size_t bytes, int node, void **p) {
     const hipError_t e = hipHostMalloc(p, bytes, hipHostMallocPortable | (bound ? hipHostMallocNumaUser : 0));
     if (bound) (void)syscall(SYS_set_mempolicy, old_mode, old_mode == kMpolDefault ? nullptr : old_mask, kMaxNodes);
     if (e == hipSuccess) {
-        note_pinned(*p, bytes);
         return 0;
     }
     note_hip_error(e, __FILE__, __LINE__, "hipHostMalloc(pinned, NUMA node)");
@@ -1555,7 +1483,6 @@ int jfsx_host_numa_node(const void *p, size_t bytes, int *node) {
 
 int jfsx_free_pinned(jfsx_ctx *c, void *p) {
     if (!c) return JFSX_EINVAL;
-    forget_pinned(p);
     HIP_OK(hipHostFree(p));
     return 0;
 }
