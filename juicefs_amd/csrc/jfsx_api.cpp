@@ -207,6 +207,7 @@ struct Workspace {
     const void *dout = nullptr;  // device BlkOut[n] of the batch in flight
     size_t down = 0;        // bytes of the result download (BlkOut[n], then the CRC words with host_crc)
     size_t crc_off = 0;     // host_crc GEN: offset of the CRC words in that download
+    size_t res_off = 0;     // offset of the results (BlkOut[n], CRC words) in h
     bool crc_back = false;  // host_crc GEN: finish_aead copies the CRC words to the callers' arrays
     bool timed = false;     // the batch's main kernel is bracketed by timing events
 };
@@ -462,7 +463,7 @@ int check_aead_args(int algo, int n, const jfsx_blk *blks, int crc_mode, bool de
 int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEvent_t k1, int algo, bool open, int n,
                  const jfsx_blk *blks, int crc_mode, hipStream_t up = nullptr, hipEvent_t up_ev = nullptr,
                  bool collect = true, hipStream_t fin = nullptr, hipEvent_t main_ev = nullptr,
-                 bool host_crc = false) {
+                 bool host_crc = false, bool zc = false) {
     const bool gcm = algo == JFSX_AES256GCM;
     std::vector<uint64_t> lens(n);
     uint64_t crc_calc_words = 0, crc_words = 0;
@@ -498,7 +499,9 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
     const size_t o_calc = off; off = align256(off + 4 * std::max<uint64_t>(crc_calc_words, 1));
     int rc;
     if ((rc = ensure_dev(c, &w.d, &w.dcap, off))) return rc;
-    if ((rc = ensure_host(&w.h, &w.hcap, std::max(h_bytes, down)))) return rc;
+    // zc: the results go straight to the pinned mirror, after the descriptors
+    const size_t o_hres = zc ? h_bytes : 0;
+    if ((rc = ensure_host(&w.h, &w.hcap, zc ? h_bytes + down : std::max(h_bytes, down)))) return rc;
     char *h = w.h, *d = w.d;
     KeyIn *hk = (KeyIn *)(h + o_keys);
     BlkDev *hb = (BlkDev *)(h + o_blk);
@@ -517,7 +520,8 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
             memcpy(h + o_crcin + 4 * cw, b.crc, 4 * nseg_of(b.len));
             hb[i].crc = (uint8_t *)(d + o_crcin + 4 * cw);
         } else if (hc_out) {
-            hb[i].crc = (uint8_t *)(d + o_crcout + 4 * cw);
+            hb[i].crc = zc ? (uint8_t *)(h + o_hres + (o_crcout - o_out) + 4 * cw) : (uint8_t *)(d + o_crcout + 4 * cw);
+            if (zc && b.len == 0) *(uint32_t *)hb[i].crc = 0;  // checksum() of nothing: one zero word
         }
         cw += nseg_of(b.len);
         hb[i].crc_calc = nullptr;
@@ -555,24 +559,30 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
     uint32_t *dpart = (uint32_t *)(d + o_part);
     uint32_t *dpexp = (uint32_t *)(d + o_pexp);
     uint32_t *dq = (uint32_t *)(d + o_queue);
-    BlkOut *dout = (BlkOut *)(d + o_out);
+    BlkOut *dout = zc ? (BlkOut *)(h + o_hres) : (BlkOut *)(d + o_out);
     // keysetup on the upload stream when one is given (fin set), else on s
     hipStream_t ks = (up && fin) ? up : s, fs = fin ? fin : s;
-    HIP_OK(hipMemcpyAsync(d, h, h_bytes, hipMemcpyHostToDevice, up ? up : s));
+    launch_begin();
+    if (zc) {
+        // the compute stream pulls the descriptors out of the pinned mirror
+        // itself, so the upload stream carries only the blocks' data
+        launch_pull(s, d, h, h_bytes);
+    } else {
+        HIP_OK(hipMemcpyAsync(d, h, h_bytes, hipMemcpyHostToDevice, up ? up : s));
+    }
     // the compute stream waits for the upload before the first kernel that
-    // reads the descriptors: keysetup when it runs on s, else main
-    if (up && ks == s) {
+    // reads what it carries: keysetup when the descriptors ride it, else main
+    if (up && ks == s && !zc) {
         HIP_OK(hipEventRecord(up_ev, up));
         HIP_OK(hipStreamWaitEvent(s, up_ev, 0));
     }
-    launch_begin();
     if (gcm) launch_gcm_keysetup(ks, n, dk, db, (GcmSched *)(d + o_sched), c->tabs);
     else launch_cp_keysetup(ks, n, dk, db, (CpSched *)(d + o_sched));
-    if (up && ks != s) {
+    if (up && (ks != s || zc)) {
         HIP_OK(hipEventRecord(up_ev, up));
         HIP_OK(hipStreamWaitEvent(s, up_ev, 0));
     }
-    if ((crc_mode & 3) == JFSX_CRC_GEN)
+    if ((crc_mode & 3) == JFSX_CRC_GEN && !(zc && hc_out))
         for (int i = 0; i < n; i++)
             if (blks[i].len == 0) HIP_OK(hipMemsetAsync(hb[i].crc, 0, 4, s));
     if (c->timing) HIP_OK(hipEventRecord(k0, s));
@@ -593,10 +603,11 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
         launch_cp_finalize(fs, n, open, crc_mode, db, (const CpSched *)(d + o_sched), dpart, dpexp, dout);
     HIP_OK(hipGetLastError());
     w.dout = dout;
-    w.down = down;
+    w.down = zc ? 0 : down;
     w.crc_off = o_crcout - o_out;
     w.crc_back = hc_out;
-    if (collect) HIP_OK(hipMemcpyAsync(h, dout, down, hipMemcpyDeviceToHost, fs));
+    w.res_off = o_hres;
+    if (collect && !zc) HIP_OK(hipMemcpyAsync(h, dout, down, hipMemcpyDeviceToHost, fs));
     w.n = n;
     w.nt = nt;
     w.timed = c->timing;
@@ -611,7 +622,7 @@ int finish_aead(jfsx_ctx *c, Workspace &w, hipEvent_t k0, hipEvent_t k1, bool op
         HIP_OK(hipEventElapsedTime(&ms, k0, k1));
         add_kernel_ms(c, ms);
     }
-    const BlkOut *ho = (const BlkOut *)w.h;
+    const BlkOut *ho = (const BlkOut *)(w.h + w.res_off);
     for (int i = 0; i < w.n; i++) {
         jfsx_blk &b = blks[i];
         if (!open) memcpy(b.tag, ho[i].tag, 16);
@@ -621,7 +632,7 @@ int finish_aead(jfsx_ctx *c, Workspace &w, hipEvent_t k0, hipEvent_t k1, bool op
         b.crc_expect = ho[i].expect;
     }
     if (w.crc_back) {
-        const char *hw = w.h + w.crc_off;
+        const char *hw = w.h + w.res_off + w.crc_off;
         for (int i = 0; i < w.n; i++) {
             const size_t cb = 4 * nseg_of(blks[i].len);
             memcpy(blks[i].crc, hw, cb);
@@ -728,6 +739,20 @@ void pipe_collect(jfsx_ctx *c, PipeSlot &s) {
 // (the call's copy of blks[i]) is pointed at the staging copy.  (A variant
 // whose kernel wrote the outputs straight into engine-pinned caller memory
 // over PCIe ran at 25 GB/s against 38.7 staged and was removed.)
+// The host pipeline's metadata path: with it (the default) the compute stream
+// pulls each group's descriptors out of the pinned mirror with a small kernel
+// and finalize writes the per-block results (and GEN CRC words) straight into
+// it, so the copy streams carry only block data -- small copies on them run as
+// blit kernels between the SDMA transfers.  JFSX_PIPE_META=copy restores the
+// metadata copies.
+bool zero_copy_meta() {
+    static const bool v = [] {
+        const char *e = getenv("JFSX_PIPE_META");
+        return !(e && !strcmp(e, "copy"));
+    }();
+    return v;
+}
+
 int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, int algo, bool open, int nb, const jfsx_blk *blks, jfsx_blk *dv,
                  int crc_mode) {
     Workspace &w = s.w;
@@ -781,7 +806,7 @@ int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, int algo, bool open, int nb, const jf
     // the CRC arrays pass through the descriptor upload and the result
     // download (host_crc)
     if ((rc = enqueue_aead(c, w, c->stream, s.ev_k0, s.ev_k1, algo, open, nb, dv, crc_mode, c->s_in, s.ev_in, false,
-                           nullptr, nullptr, true)))
+                           nullptr, nullptr, true, zero_copy_meta())))
         return rc;
     HIP_OK(hipEventRecord(s.ev_comp, c->stream));
     HIP_OK(hipStreamWaitEvent(c->s_out, s.ev_comp, 0));
@@ -810,7 +835,7 @@ int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, int algo, bool open, int nb, const jf
         if (align256(blks[i].len) != blks[i].len && (rc = flush_out())) return rc;
     }
     if ((rc = flush_out())) return rc;
-    HIP_OK(hipMemcpyAsync(w.h, w.dout, w.down, hipMemcpyDeviceToHost, c->s_out));
+    if (w.down) HIP_OK(hipMemcpyAsync(w.h, w.dout, w.down, hipMemcpyDeviceToHost, c->s_out));
     HIP_OK(hipEventRecord(s.ev_out, c->s_out));
     return 0;
 }

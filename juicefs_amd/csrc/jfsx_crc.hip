@@ -446,6 +446,22 @@ __global__ __launch_bounds__(256) void gen_synthetic_batch_k(uint8_t *__restrict
     }
 }
 
+// dst[0, bytes) = src[0, bytes) for a small region (a pipeline group's
+// descriptors) read by the GPU straight out of pinned host memory, which the
+// host rewrote since the previous group: system-scope loads, so no cache level
+// can hand back the previous group's words.  bytes is a multiple of 4.
+__global__ __launch_bounds__(256) void pull_k(uint32_t *__restrict__ dst, uint32_t *__restrict__ src, uint32_t n4) {
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256)
+        dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void launch_pull(hipStream_t s, void *dst, const void *src, size_t bytes) {
+    const uint32_t n4 = (uint32_t)(bytes / 4);
+    if (!n4) return;
+    const uint32_t grid = (n4 + 255) / 256 < 128 ? (n4 + 255) / 256 : 128;
+    hipLaunchKernelGGL(pull_k, dim3(grid), dim3(256), 0, s, (uint32_t *)dst, (uint32_t *)src, n4);
+}
+
 void launch_gen_synthetic_batch(hipStream_t s, uint8_t *dst, uint64_t stride, int n, const uint64_t *lens,
                                 uint64_t seed, uint64_t block0) {
     // y <= 65535 blocks per launch

@@ -299,6 +299,7 @@ void launch_cp_finalize(hipStream_t s, int n, bool open, int crc_mode, const Blk
 void launch_crc_segments(hipStream_t s, int ntasks, const Task *tasks, const BlkDev *blks, DevTables t);
 void launch_crc_finalize(hipStream_t s, int n, int crc_mode, const BlkDev *blks, BlkOut *out);
 void launch_gen_synthetic(hipStream_t s, uint8_t *dst, uint64_t len, uint64_t seed, uint64_t block);
+void launch_pull(hipStream_t s, void *dst, const void *src, size_t bytes);
 void launch_gen_synthetic_batch(hipStream_t s, uint8_t *dst, uint64_t stride, int n, const uint64_t *lens,
                                 uint64_t seed, uint64_t block0);
 // tabs: n x 16 KiB of device memory, the blocks' LZ4 hash tables
