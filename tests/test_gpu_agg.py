@@ -4,6 +4,7 @@ as dataEncryptor.Encrypt/Decrypt (pkg/object/encrypt.go:164-216) and the
 cache-read verify (pkg/chunk/disk_cache.go:1315-1327) are made, get results
 bit-identical to the oracle while the engine sees a few large batches."""
 import ctypes
+import os
 import threading
 
 import numpy as np
@@ -310,6 +311,53 @@ def test_host_pipeline_shared_by_concurrent_callers(algo):
                 assert cs.tobytes() == orc.checksum(p, hw=True)
     finally:
         eng.close()
+
+
+_META_COPY_SCRIPT = r"""
+import sys, numpy as np
+sys.path.insert(0, %r)
+from juicefs_amd import engine as E
+from oracle import oracle as orc
+eng = E.Engine(0)
+eng.set_slot_bytes(2 << 20)
+rng = np.random.default_rng(5)
+lens = [int(x) for x in rng.integers(0, 3 << 20, 12)] + [0, 17]
+specs, keep = [], []
+for i, n in enumerate(lens):
+    p = orc.gen_block(77, i, n)
+    k, nn = orc.gen_key(77, i)
+    c = np.zeros(max(n, 1), np.uint8)
+    cs = np.zeros(4 * max(1, -(-n // E.SEG)), np.uint8)
+    keep.append((p, k, nn, c, cs))
+    specs.append({"key": k, "nonce": nn, "src": p.ctypes.data if n else None, "dst": c.ctypes.data, "len": n,
+                  "crc": cs.ctypes.data})
+arr, nb = eng.make_blocks(specs)
+eng.seal_batch(E.AES256GCM, arr, nb, E.CRC_GEN, E.MEM_HOST)
+for i, (p, k, nn, c, cs) in enumerate(keep):
+    ct, tag = orc.seal(orc.AES256GCM, k, nn, p, fast=True)
+    assert bytes(arr[i].tag) == tag and c[:p.size].tobytes() == ct, i
+    assert cs.tobytes() == orc.checksum(p, hw=True), i
+    arr[i].src = arr[i].dst = c.ctypes.data
+eng.open_batch(E.AES256GCM, arr, nb, E.CRC_VERIFY, E.MEM_HOST)
+assert all(arr[i].status == E.OK for i in range(nb))
+assert all(c[:p.size].tobytes() == p.tobytes() for p, k, nn, c, cs in keep)
+eng.close()
+print("meta copy ok")
+"""
+
+
+def test_host_pipeline_metadata_copy_mode():
+    """JFSX_PIPE_META=copy (descriptors and results as copies on the copy
+    streams instead of the default pull kernel and pinned-mirror results), in
+    a child process since the mode is read once: a host batch across several
+    slots seals and opens bit-exact to the oracle, CRC arrays included."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, JFSX_PIPE_META="copy")
+    out = subprocess.run([sys.executable, "-c", _META_COPY_SCRIPT % root], env=env, capture_output=True, text=True,
+                         timeout=110)
+    assert out.returncode == 0 and "meta copy ok" in out.stdout, out.stderr[-2000:]
 
 
 def test_agg_data_encrypt_equals_data_encrypt(eng):
