@@ -35,6 +35,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--warmup-seconds", type=float, default=None,
+                    help="host-memory modes (--mem host, agg): keep warming up until this much time has passed as "
+                         "well as --warmup steps (default 8 s there, 0 elsewhere): a cold box's D2H path runs at "
+                         "about 20 GB/s for its first seconds of traffic (tools/pin_probe.hip)")
     ap.add_argument("--blocks", type=int, default=16384, help="4 MiB blocks per GPU (16384 = 64 GiB)")
     ap.add_argument("--block-bytes", type=int, default=BLOCK)
     ap.add_argument("--mode", choices=["seal", "open", "crc", "decrypt", "agg", "aggcodec", "lz4", "unlz4", "zstd", "unzstd"], default="seal",
@@ -836,6 +840,21 @@ def numa_pin(node):
 PCIE_GEN5_X16_GBS = 64.0  # per direction, 32 GT/s x 16 lanes (before 128b/130b and TLP overhead)
 
 
+def warm_up(args, step, host=False):
+    """--warmup untimed steps; in the host-memory modes also until
+    --warmup-seconds have passed (default 8 s): the copy engines' D2H rate
+    ramps up over the first seconds of traffic on a cold box (tools/pin_probe.hip
+    measured 19.9 GB/s, then 50.5 later in the same process)."""
+    secs = args.warmup_seconds if args.warmup_seconds is not None else (8.0 if host else 0.0)
+    t0 = time.perf_counter()
+    done = 0
+    while done < args.warmup or time.perf_counter() - t0 < secs:
+        step()
+        done += 1
+    args.warm = {"steps": done, "seconds": round(time.perf_counter() - t0, 1)}
+    return done
+
+
 def host_ingest(args, world, rank, local, dist):
     """BASELINE configs[2]: blocks in pinned host memory, sealed through the
     engine's H2D | transform | D2H pipeline (JFSX_MEM_HOST); value = plaintext
@@ -889,8 +908,7 @@ def host_ingest(args, world, rank, local, dist):
     def step():
         for arr, n, _ in loops:
             front.seal_batch(algo, arr, n, E.CRC_GEN, E.MEM_HOST)
-    for _ in range(args.warmup):
-        step()
+    warm_up(args, step, host=True)
     for e in engs:
         e.sync()
         e.kernel_time(reset=True)
@@ -963,6 +981,7 @@ def host_ingest(args, world, rank, local, dist):
                                        args.algo),
                        "blocks_per_gpu": sh0.count, "pool_blocks_per_gpu": sh0.nb, "block_bytes": L,
                        "algo": args.algo, "mem": "host", "total_gib": args.total_gib or None,
+                       "warmup_run": getattr(args, "warm", None),
                        "engine": "jfsx_mctx (one process, %d GPUs)" % ngpu if m else "one process per GPU",
                        "pinned_bytes_per_process": pinned,
                        "numa": [{"gpu_node": sh.node, "pool_node": sh.pool_node, "cpus_on_node": sh.cpus}
@@ -1065,7 +1084,7 @@ def agg_bench(args, world, rank, local, dist, eng):
     with E.Aggregator(eng, window_us=args.agg_window_us, max_bytes=args.agg_max_mb << 20) as agg:
         def through(b):
             agg.seal(algo, blks[b], E.CRC_GEN, E.MEM_HOST)
-        run(through, args.warmup)
+        warm_up(args, lambda: run(through, 1), host=True)
         c0, b0, k0 = agg.stats()
         barrier(dist)
         el = max_over_ranks(dist, run(through, args.steps), local)
@@ -1101,6 +1120,7 @@ def agg_bench(args, world, rank, local, dist, eng):
                                    "blocks, %s + CRC32C full, JFSX_MEM_HOST" % (nb, T, args.algo), "blocks_per_gpu": nb, "block_bytes": L, "algo": args.algo,
                        "mode": "agg", "window_us": args.agg_window_us, "max_batch_bytes": args.agg_max_mb << 20,
                        "dispatchers_per_gpu": int(os.environ.get("JFSX_AGG_DISPATCHERS", "4")),
+                       "warmup_run": getattr(args, "warm", None),
                        "numa": {"gpu_node": node, "pool_node": pool_node, "cpus_on_node": cpus}},
             "aggregator": {"calls": c1 - c0, "batches": b1 - b0,
                            "mean_batch_blocks": round((k1 - k0) / max(b1 - b0, 1), 2)},

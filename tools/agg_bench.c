@@ -112,7 +112,9 @@ int main(int argc, char **argv) {
     for (uint64_t i = 0; i < NB * L; i += 8) *(uint64_t *)(hin + i) = i * 0x9E3779B97F4A7C15ull;
     use_agg = 0;
     PASSES = 1;
-    run();
+    // warm the copy path up first: a cold box's D2H rate ramps up over the
+    // first seconds of traffic (tools/pin_probe.hip)
+    for (const double w0 = now(); now() - w0 < 8.0;) run();
     const int passes = argc > 3 ? atoi(argv[3]) : 4;
     PASSES = passes;
     const double direct = run();
