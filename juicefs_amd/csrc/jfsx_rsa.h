@@ -30,10 +30,17 @@
 #ifndef JFSX_RSA_TRACE
 #define JFSX_RSA_TRACE(tag, v) ((void)0)
 #endif
+// a register barrier: the compiler cannot see through it, so a mask built from
+// a secret digit cannot become a branch or an address (the GPU includer passes
+// its VGPR form)
+#ifndef JFSX_RSA_OPAQUE
+#define JFSX_RSA_OPAQUE(x) asm volatile("" : "+r"(x))
+#endif
 
 namespace jfsx_rsa {
 
 constexpr int kLimbs = 32;        // 1024-bit prime
+constexpr int kL28 = 37;          // the same in 28-bit limbs (1036 bits), the GPU exponentiation's form
 constexpr int kModBytes = 256;    // RSA-2048 modulus
 constexpr int kHash = 32;         // SHA-256
 
@@ -152,12 +159,12 @@ JFSX_HD void mont_mul(const uint32_t *a, const uint32_t *b, const uint32_t *m, u
     for (int j = 0; j < kLimbs; j++) out[j] = keep ? t[j] : d[j];
 }
 
-// R^2 mod m by doubling (host side, once per key)
-JFSX_HD void mont_r2(const uint32_t *m, uint32_t *r2) {
+// 2^bits mod m by doubling (host side, once per key); R^2 mod m by default
+JFSX_HD void mont_r2(const uint32_t *m, uint32_t *r2, int bits = 2 * 32 * kLimbs) {
     uint32_t x[kLimbs + 1];
     for (int j = 0; j <= kLimbs; j++) x[j] = 0;
     x[0] = 1;
-    for (int k = 0; k < 2 * 32 * kLimbs; k++) {  // x = 2^k mod m
+    for (int k = 0; k < bits; k++) {  // x = 2^k mod m
         uint32_t c = 0;
         for (int j = 0; j <= kLimbs; j++) {
             const uint32_t nc = x[j] >> 31;
@@ -295,6 +302,7 @@ struct Key {
     uint32_t dp[kLimbs], dq[kLimbs];    // CRT exponents
     uint32_t qinv[kLimbs];              // q^-1 mod p
     uint32_t r2p[kLimbs], r2q[kLimbs];  // R^2 mod p, R^2 mod q
+    uint32_t r2p28[kLimbs], r2q28[kLimbs];  // R'^2 mod p, q for the GPU's 28-bit limbs (R' = 2^(28 kL28))
     uint32_t pinv, qinv32;              // -p^-1, -q^-1 mod 2^32
     int32_t dp_bits, dq_bits;           // exponent bit lengths
     uint8_t lhash[32];                  // SHA-256(label)
@@ -323,6 +331,8 @@ JFSX_HD bool key_setup(Key &k, const uint8_t *p, const uint8_t *q, const uint8_t
     k.qinv32 = mont_inv32(k.q[0]);
     mont_r2(k.p, k.r2p);
     mont_r2(k.q, k.r2q);
+    mont_r2(k.p, k.r2p28, 2 * 28 * kL28);
+    mont_r2(k.q, k.r2q28, 2 * 28 * kL28);
     k.dp_bits = bit_length(k.dp, kLimbs);
     k.dq_bits = bit_length(k.dq, kLimbs);
     if (k.dp_bits < 2 || k.dq_bits < 2) return false;
@@ -352,42 +362,6 @@ JFSX_HD void reduce_2048(const uint32_t *c, const uint32_t *m, uint32_t minv, co
     for (int j = 0; j < kLimbs; j++) out[j] = t[j];
 }
 
-// The fixed-window schedule both exponentiations follow: kDigits 4-bit
-// digits of the exponent zero-extended to the prime's length, top first; per
-// digit four squarings and one multiply by tab[digit] (tab[0] = the
-// Montgomery one), whatever the digit.
-constexpr int kDigits = 8 * kLimbs;
-JFSX_HD uint32_t exp_digit(const uint32_t *e, int d) { return (e[d >> 3] >> (4 * (d & 7))) & 15u; }
-
-// b = tab[idx] by reading every entry and keeping the one whose index matches
-// (mask), so the addresses touched do not depend on idx
-JFSX_HD void ct_select16(const uint32_t (*tab)[kLimbs], uint32_t idx, uint32_t *b) {
-    for (int j = 0; j < kLimbs; j++) b[j] = 0;
-    for (uint32_t w = 0; w < 16; w++) {
-        const uint32_t m = ~ct_nz(w ^ idx);
-        JFSX_RSA_TRACE('S', w);
-        for (int j = 0; j < kLimbs; j++) b[j] |= tab[w][j] & m;
-    }
-}
-
-// x^e mod m (x < m) on the fixed schedule above; constant time in e
-JFSX_HD void mod_exp(const uint32_t *x, const uint32_t *e, int e_bits, const uint32_t *m, uint32_t minv,
-                     const uint32_t *r2, uint32_t *out) {
-    (void)e_bits;  // the schedule covers the full length whatever the exponent's bit length
-    uint32_t tab[16][kLimbs], acc[kLimbs], b[kLimbs], one[kLimbs];
-    for (int j = 0; j < kLimbs; j++) one[j] = j == 0;
-    mont_mul(r2, one, m, minv, tab[0]);  // R mod m: the Montgomery one
-    mont_mul(x, r2, m, minv, tab[1]);    // x R mod m
-    for (int w = 2; w < 16; w++) mont_mul(tab[w - 1], tab[1], m, minv, tab[w]);
-    for (int j = 0; j < kLimbs; j++) acc[j] = tab[0][j];
-    for (int d = kDigits - 1; d >= 0; d--) {
-        for (int sq = 0; sq < 4; sq++) mont_mul(acc, acc, m, minv, acc);
-        ct_select16(tab, exp_digit(e, d), b);
-        mont_mul(acc, b, m, minv, acc);
-    }
-    mont_mul(acc, one, m, minv, out);  // leave the Montgomery domain
-}
-
 // m = m2 + q (qinv (m1 - m2) mod p), the 2048-bit CRT recombination
 JFSX_HD void crt(const Key &k, const uint32_t *m1, const uint32_t *m2, uint32_t *m) {
     uint32_t t[kLimbs + 1], h[kLimbs], u[kLimbs];
@@ -415,6 +389,163 @@ JFSX_HD void crt(const Key &k, const uint32_t *m1, const uint32_t *m2, uint32_t 
     }
 }
 
+// ---------------------------------------------------------------------------
+// The exponentiation the unwrap runs, in 28-bit limbs.  With 32-bit limbs every
+// multiply-add of the CIOS carries into the next (a GPU thread spends ~9K
+// instructions per product on the multiply-adds and the moves that build
+// their 64-bit addends).  With 37 limbs of 28 bits a product is < 2^56, so
+// each column's 64-bit accumulator takes every row's two products with no
+// carry at all (37 rows x 2 x 2^56 < 2^63): a row is 74 independent
+// multiply-adds, and carries are resolved once per product.  R' = 2^(28 kL28);
+// R'^2 mod p, q come with the key (Key::r2p28, r2q28).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kM28 = (1u << 28) - 1;
+
+// 32-bit limbs (kLimbs) <-> 28-bit limbs (kL28)
+JFSX_HD void to28(const uint32_t *x, uint32_t *y) {
+#pragma unroll
+    for (int j = 0; j < kL28; j++) {
+        const int bit = 28 * j, l = bit >> 5, o = bit & 31;
+        uint64_t v = x[l];
+        if (l + 1 < kLimbs) v |= (uint64_t)x[l + 1] << 32;
+        y[j] = (uint32_t)(v >> o) & kM28;
+    }
+}
+JFSX_HD void from28(const uint32_t *y, uint32_t *x) {
+#pragma unroll
+    for (int j = 0; j < kLimbs; j++) {
+        const int bit = 32 * j, l = bit / 28, o = bit % 28;  // o <= 24: two limbs cover the word
+        uint64_t v = (uint64_t)y[l] >> o;
+        if (l + 1 < kL28) v |= (uint64_t)y[l + 1] << (28 - o);
+        x[j] = (uint32_t)v;
+    }
+}
+
+// out = a b R'^-1 mod m: a, b < m in normalized 28-bit limbs, minv = -m^-1
+// mod 2^28; out normalized and < m (one masked final subtract)
+JFSX_HD void mont_mul28(const uint32_t *a, const uint32_t *b, const uint32_t *m, uint32_t minv, uint32_t *out) {
+    JFSX_RSA_TRACE('M', 1);
+    uint64_t acc[kL28];
+#pragma unroll
+    for (int j = 0; j < kL28; j++) acc[j] = 0;
+#pragma unroll
+    for (int i = 0; i < kL28; i++) {
+        const uint32_t ai = a[i];
+#pragma unroll
+        for (int j = 0; j < kL28; j++) acc[j] += (uint64_t)ai * b[j];
+        const uint32_t mi = ((uint32_t)acc[0] * minv) & kM28;
+#pragma unroll
+        for (int j = 0; j < kL28; j++) acc[j] += (uint64_t)mi * m[j];
+        const uint64_t c = acc[0] >> 28;  // acc[0] is now a multiple of 2^28
+#pragma unroll
+        for (int j = 0; j < kL28 - 1; j++) acc[j] = acc[j + 1];
+        acc[kL28 - 1] = 0;
+        acc[0] += c;
+    }
+    // normalize (the value is < 2m < 2^1036), then subtract m unless t < m
+    uint32_t t[kL28], d[kL28];
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < kL28; j++) {
+        c += acc[j];
+        t[j] = (uint32_t)c & kM28;
+        c >>= 28;
+    }
+    uint32_t br = 0;
+#pragma unroll
+    for (int j = 0; j < kL28; j++) {
+        const uint32_t x = t[j] - m[j] - br;
+        d[j] = x & kM28;
+        br = x >> 31;
+    }
+    const uint32_t keep = 0u - br;  // t < m
+#pragma unroll
+    for (int j = 0; j < kL28; j++) out[j] = (t[j] & keep) | (d[j] & ~keep);
+}
+
+// The constant-time fixed-window schedule: kWDigits kWBits-bit digits of the
+// exponent zero-extended to the prime's length, top first; per digit kWBits
+// squarings and one multiply by tab[digit] (tab[0] = the Montgomery one),
+// whatever the digit, the entry picked by a masked scan of all kWTab entries.
+// One Montgomery multiply site in a loop over a step counter (the unrolled
+// product is a few thousand instructions; one copy stays in the GPU's
+// instruction cache), table writes at static indices only (so the table can
+// live in registers), and the exponent only feeding masks through a register
+// barrier.  A 3-bit window: the 8-entry table of 37-limb values fits the GPU
+// thread's registers, a 16-entry one spills to scratch memory and the scan
+// then reads it for every digit.
+constexpr int kWBits = 3, kWTab = 1 << kWBits, kWDigits = (32 * kLimbs + kWBits - 1) / kWBits;
+
+// digit d (0 = least significant) of e in kWBits-bit digits
+JFSX_HD uint32_t w_digit(const uint32_t *e, int d) {
+    const int b = kWBits * d, l = b >> 5, o = b & 31;
+    uint64_t v = e[l];
+    if (l + 1 < kLimbs) v |= (uint64_t)e[l + 1] << 32;
+    return (uint32_t)(v >> o) & (kWTab - 1);
+}
+
+// x^e mod m (x < m; 32-bit limbs in and out), constant time in e
+JFSX_HD void mod_exp28(const uint32_t *x32, const uint32_t *e, const uint32_t *m32, uint32_t minv32,
+                       const uint32_t *r2_32, uint32_t *out32) {
+    uint32_t m[kL28], x[kL28], r2[kL28];
+    to28(m32, m);
+    to28(x32, x);
+    to28(r2_32, r2);
+    const uint32_t minv = minv32 & kM28;
+    uint32_t tab[kWTab][kL28];
+    uint32_t acc[kL28], b[kL28];
+    for (int w = 0; w < kWTab; w++)
+        for (int j = 0; j < kL28; j++) tab[w][j] = 0;
+    constexpr int kPer = kWBits + 1, kMain = kWTab + kPer * kWDigits;  // steps: table, digits, leave the domain
+#pragma unroll 1
+    for (int st = 0; st <= kMain; st++) {
+        if (st == 0) {  // R' mod m = r2 * 1
+#pragma unroll
+            for (int j = 0; j < kL28; j++) acc[j] = r2[j], b[j] = j == 0;
+        } else if (st == 1) {  // x R' mod m
+#pragma unroll
+            for (int j = 0; j < kL28; j++) acc[j] = x[j], b[j] = r2[j];
+        } else if (st < kWTab) {  // tab[st] = tab[st - 1] * x R'
+#pragma unroll
+            for (int j = 0; j < kL28; j++) b[j] = tab[1][j];
+        } else if (st < kMain) {
+            const int r = st - kWTab;
+            if (r % kPer < kWBits) {
+#pragma unroll
+                for (int j = 0; j < kL28; j++) b[j] = acc[j];
+            } else {
+                uint32_t idx = w_digit(e, kWDigits - 1 - r / kPer);
+                JFSX_RSA_OPAQUE(idx);
+#pragma unroll
+                for (int j = 0; j < kL28; j++) b[j] = 0;
+#pragma unroll
+                for (uint32_t w = 0; w < (uint32_t)kWTab; w++) {
+                    uint32_t msk = ~ct_nz(w ^ idx);
+                    JFSX_RSA_OPAQUE(msk);
+                    JFSX_RSA_TRACE('S', w);
+#pragma unroll
+                    for (int j = 0; j < kL28; j++) b[j] |= tab[w][j] & msk;
+                }
+            }
+        } else {  // out of the Montgomery domain
+#pragma unroll
+            for (int j = 0; j < kL28; j++) b[j] = j == 0;
+        }
+        mont_mul28(acc, b, m, minv, acc);
+        if (st < kWTab) {
+#pragma unroll
+            for (int w = 0; w < kWTab; w++)
+#pragma unroll
+                for (int j = 0; j < kL28; j++) tab[w][j] = st == w ? acc[j] : tab[w][j];
+            if (st == kWTab - 1) {
+#pragma unroll
+                for (int j = 0; j < kL28; j++) acc[j] = tab[0][j];
+            }
+        }
+    }
+    from28(acc, out32);
+}
+
 // One whole unwrap on one thread (the CPU pin; the GPU splits it into the
 // two half exponentiations and a finish kernel): ct = k bytes, big-endian.
 // Returns the message length (msg in em[0..len)) or -1.
@@ -423,9 +554,9 @@ JFSX_HD int decrypt(const Key &k, const uint8_t *ct, uint8_t em[kModBytes]) {
     from_be(ct, kModBytes, c, 2 * kLimbs);
     if (geq(c, k.n, 2 * kLimbs)) return -1;
     reduce_2048(c, k.p, k.pinv, k.r2p, x);
-    mod_exp(x, k.dp, k.dp_bits, k.p, k.pinv, k.r2p, m1);
+    mod_exp28(x, k.dp, k.p, k.pinv, k.r2p28, m1);
     reduce_2048(c, k.q, k.qinv32, k.r2q, x);
-    mod_exp(x, k.dq, k.dq_bits, k.q, k.qinv32, k.r2q, m2);
+    mod_exp28(x, k.dq, k.q, k.qinv32, k.r2q28, m2);
     crt(k, m1, m2, m);
     to_be(m, 2 * kLimbs, em, kModBytes);
     return oaep_decode(em, kModBytes, k.lhash);

@@ -23,7 +23,8 @@ int rsa_unwrap(const uint8_t *p, const uint8_t *q, const uint8_t *dp, const uint
 void sha256(const uint8_t *a, int la, uint8_t *out) { jfsx_rsa::sha256_2(a, la, a, 0, out); }
 
 // x^e mod m (128-byte big-endian operands, m an odd 1024-bit number) on the
-// unwrap's exponentiation; returns the operation-trace hash, *ops the count
+// unwrap's exponentiation (mod_exp28, the one the GPU kernel runs); returns
+// the operation-trace hash, *ops the count
 uint64_t rsa_exp_trace(const uint8_t *m_be, const uint8_t *e_be, const uint8_t *x_be, uint8_t *out_be,
                        uint64_t *ops) {
     using namespace jfsx_rsa;
@@ -31,10 +32,10 @@ uint64_t rsa_exp_trace(const uint8_t *m_be, const uint8_t *e_be, const uint8_t *
     from_be(m_be, 4 * kLimbs, m, kLimbs);
     from_be(e_be, 4 * kLimbs, e, kLimbs);
     from_be(x_be, 4 * kLimbs, x, kLimbs);
-    mont_r2(m, r2);
+    mont_r2(m, r2, 2 * 28 * kL28);
     g_trace = 1469598103934665603ull;
     g_ops = 0;
-    mod_exp(x, e, bit_length(e, kLimbs), m, mont_inv32(m[0]), r2, r);
+    mod_exp28(x, e, m, mont_inv32(m[0]), r2, r);
     to_be(r, kLimbs, out_be, 4 * kLimbs);
     *ops = g_ops;
     return g_trace;

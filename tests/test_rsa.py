@@ -79,9 +79,10 @@ def test_exponentiation_schedule_is_independent_of_the_exponent(rsa, keypair):
     """Constant time in the private exponent (as Go's crypto/internal/bigmod
     Exp, which rsa.DecryptOAEP uses; encrypt.go:132-134): the sequence of
     Montgomery products and window-table reads is the same for the key's real
-    CRT exponent, a tiny one, an all-ones one and zero -- 1024-bit fixed
-    window, one multiply per digit, every table entry read for every digit --
-    and every result equals pow()."""
+    CRT exponent, a tiny one, an all-ones one and zero -- 3-bit fixed window
+    over the full 1024 bits, one multiply per digit, every table entry read
+    for every digit -- and every result equals pow().  (The exponentiation is
+    mod_exp28, the one the GPU kernel runs, in 28-bit limbs.)"""
     _, _, comps = keypair
     p = comps[0]
     pi = int.from_bytes(p, "big")
@@ -96,7 +97,8 @@ def test_exponentiation_schedule_is_independent_of_the_exponent(rsa, keypair):
         traces.add((h, ops.value))
     assert len(traces) == 1, traces
     (_, nops), = traces
-    assert nops == 2 + 14 + 256 * 5 + 1 + 256 * 16  # table, 256 digits x (4 sq + 1 mul), exit; 16 reads per digit
+    # table (8), 342 digits x (3 sq + 1 mul), exit; 8 reads per digit
+    assert nops == 8 + 342 * 4 + 1 + 342 * 8
 
 
 def _oaep_encode(msg, seed, label=b"keys", k=256, db_patch=None):
