@@ -26,9 +26,11 @@ namespace jfsx {
 using jfsx_rsa::kLimbs;
 using jfsx_rsa::kModBytes;
 
-// threads per workgroup of rsa_half_k (half-filled waves, 32 or 16 threads,
-// measured 1.4-1.5x slower: profiles/r5/ab_rsa_chains.txt)
-constexpr int kRsaLanes = 64;
+// threads per workgroup of rsa_half_k
+#ifndef JFSX_RSA_LANES
+#define JFSX_RSA_LANES 64
+#endif
+constexpr int kRsaLanes = JFSX_RSA_LANES;
 
 __global__ __launch_bounds__(kRsaLanes) void rsa_half_k(const jfsx_rsa::Key *__restrict__ key, int n,
                                                         const uint8_t *__restrict__ ct, uint32_t *__restrict__ mh) {
