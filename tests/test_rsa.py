@@ -95,6 +95,14 @@ def test_exponentiation_schedule_is_independent_of_the_exponent(rsa, keypair):
         h = rsa.rsa_exp_trace(p, e.to_bytes(128, "big"), x.to_bytes(128, "big"), out, ctypes.byref(ops))
         assert int.from_bytes(out.raw, "big") == pow(x, e, pi)
         traces.add((h, ops.value))
+    # edge bases: 0, 1 and m - 1 (the largest reduced value)
+    for xe in (0, 1, pi - 1):
+        out = ctypes.create_string_buffer(128)
+        ops = ctypes.c_uint64()
+        e = int.from_bytes(comps[2], "big")
+        h = rsa.rsa_exp_trace(p, e.to_bytes(128, "big"), xe.to_bytes(128, "big"), out, ctypes.byref(ops))
+        assert int.from_bytes(out.raw, "big") == pow(xe, e, pi), xe
+        traces.add((h, ops.value))
     assert len(traces) == 1, traces
     (_, nops), = traces
     # table (8), 342 digits x (3 sq + 1 mul), exit; 8 reads per digit
