@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--codec", choices=["lz4", "unlz4", "zstd", "unzstd"], default="zstd",
                     help="aggcodec: the Compress / Decompress call of cachedStore.upload / load measured in the "
                          "reference's call shape")
+    ap.add_argument("--agg-op", choices=["seal", "open"], default="seal",
+                    help="agg: the per-object call measured: Seal + CRC gen (cachedStore.upload) or Open + plaintext "
+                         "CRC gen for the cache file (cachedStore.load, CS-3)")
     ap.add_argument("--agg-window-us", type=int, default=500, help="agg: aggregation window")
     ap.add_argument("--agg-max-mb", type=int, default=12,
                     help="agg: byte cap of one aggregated batch (several batches pipeline at once)")
@@ -1054,6 +1057,18 @@ def agg_bench(args, world, rank, local, dist, eng):
     blks, n = eng.make_blocks(specs)
     T = args.threads
     per = nb // T
+    is_open = args.agg_op == "open"
+    hdec = hcrc2 = None
+    if is_open:
+        # the objects to open: sealed once here (tags into blks, plaintext
+        # CRC arrays into hcrc); the timed calls open them into hdec and write
+        # the cache file's CRC arrays (JFSX_CRC_GEN of the plaintext) to hcrc2
+        eng.seal_batch(algo, blks, nb, E.CRC_GEN, E.MEM_HOST)
+        hdec = eng.alloc_pinned_node(nb * L, node)
+        hcrc2 = eng.alloc_pinned_node(nb * 4 * nseg, node)
+        ospecs = [dict(sp, src=hout + b * L, dst=hdec + b * L, crc=hcrc2 + 4 * nseg * b, tag=bytes(blks[b].tag))
+                  for b, sp in enumerate(specs)]
+        oblks, _ = eng.make_blocks(ospecs)
 
     def run(call, steps):
         errs = []
@@ -1076,14 +1091,20 @@ def agg_bench(args, world, rank, local, dist, eng):
         return time.perf_counter() - t0
 
     def direct(b):
-        eng._check(eng.L.jfsx_seal_batch(eng.ctx, algo, 1, ctypes.byref(blks[b]), E.CRC_GEN, E.MEM_HOST), "seal")
+        if is_open:
+            eng._check(eng.L.jfsx_open_batch(eng.ctx, algo, 1, ctypes.byref(oblks[b]), E.CRC_GEN, E.MEM_HOST), "open")
+        else:
+            eng._check(eng.L.jfsx_seal_batch(eng.ctx, algo, 1, ctypes.byref(blks[b]), E.CRC_GEN, E.MEM_HOST), "seal")
 
     d_steps = max(1, args.steps // 5)
     run(direct, 1)
     d_el = run(direct, d_steps)
     with E.Aggregator(eng, window_us=args.agg_window_us, max_bytes=args.agg_max_mb << 20) as agg:
         def through(b):
-            agg.seal(algo, blks[b], E.CRC_GEN, E.MEM_HOST)
+            if is_open:
+                agg.open(algo, oblks[b], E.CRC_GEN, E.MEM_HOST)
+            else:
+                agg.seal(algo, blks[b], E.CRC_GEN, E.MEM_HOST)
         warm_up(args, lambda: run(through, 1), host=True)
         c0, b0, k0 = agg.stats()
         barrier(dist)
@@ -1099,41 +1120,57 @@ def agg_bench(args, world, rank, local, dist, eng):
             got = np.ctypeslib.as_array((ctypes.c_uint8 * L).from_address(hout + b * L)).tobytes()
             if bytes(blks[b].tag) != tag or got != c:
                 raise SystemExit("bench: block %d differs from the oracle" % b)
+            if is_open:
+                pl = np.ctypeslib.as_array((ctypes.c_uint8 * L).from_address(hdec + b * L)).tobytes()
+                if pl != p.tobytes():
+                    raise SystemExit("bench: block %d: opened plaintext differs from the oracle's" % b)
             verified += 1
+        if is_open:
+            bad = [b for b in range(nb) if oblks[b].status != E.OK]
+            if bad:
+                raise SystemExit("bench: %d opened blocks failed (block %d: status %d)"
+                                 % (len(bad), bad[0], oblks[bad[0]].status))
     full = None
     if args.verify:
-        crcs = np.ctypeslib.as_array((ctypes.c_uint8 * (nb * 4 * nseg)).from_address(hcrc)).reshape(nb, 4 * nseg)
-        full = full_check(args, E, blks, crcs.copy(), [L] * nb, base)
-        full["what"] = "per-object Seal calls through the aggregator: " + full["what"]
+        crcs = np.ctypeslib.as_array((ctypes.c_uint8 * (nb * 4 * nseg)).from_address(hcrc2 if is_open else hcrc))
+        full = full_check(args, E, blks, crcs.reshape(nb, 4 * nseg).copy(), [L] * nb, base)
+        full["what"] = ("per-object Open calls through the aggregator (every status OK): setup tags and the timed "
+                        "calls' plaintext CRC arrays: " if is_open else
+                        "per-object Seal calls through the aggregator: ") + full["what"]
         verified = nb
     value = world * nb * L * args.steps / el / 1e9
-    cpu = cpu_baseline(args, "seal") if rank == 0 and world == 1 and not args.no_cpu else None
+    cpu = cpu_baseline(args, "open" if is_open else "seal") if rank == 0 and world == 1 and not args.no_cpu else None
     pcie = eng.pcie_probe()
     duplex = min(pcie["duplex_h2d"], pcie["duplex_d2h"])
     if rank == 0:
         print(json.dumps({
-            "metric": "per-object sealed+checksummed GB/s, %d threads, 4 MiB host blocks (aggregator)" % T,
+            "metric": "per-object %s GB/s, %d threads, 4 MiB host blocks (aggregator)" % (
+                "opened+checksummed" if is_open else "sealed+checksummed", T),
             "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8", "data": "synthetic (SplitMix64), pinned host memory",
-            "config": {"workload": "%d one-block Seal calls per step from %d threads, each on its own range of "
-                                   "blocks, %s + CRC32C full, JFSX_MEM_HOST" % (nb, T, args.algo), "blocks_per_gpu": nb, "block_bytes": L, "algo": args.algo,
-                       "mode": "agg", "window_us": args.agg_window_us, "max_batch_bytes": args.agg_max_mb << 20,
+            "config": {"workload": "%d one-block %s calls per step from %d threads, each on its own range of "
+                                   "blocks, %s + CRC32C full, JFSX_MEM_HOST" % (nb, "Open" if is_open else "Seal", T,
+                                                                               args.algo), "blocks_per_gpu": nb, "block_bytes": L, "algo": args.algo,
+                       "mode": "agg", "op": args.agg_op, "window_us": args.agg_window_us,
+                       "max_batch_bytes": args.agg_max_mb << 20,
                        "dispatchers_per_gpu": int(os.environ.get("JFSX_AGG_DISPATCHERS", "4")),
                        "warmup_run": getattr(args, "warm", None),
                        "numa": {"gpu_node": node, "pool_node": pool_node, "cpus_on_node": cpus}},
             "aggregator": {"calls": c1 - c0, "batches": b1 - b0,
                            "mean_batch_blocks": round((k1 - k0) / max(b1 - b0, 1), 2)},
             "direct_one_block_calls_GBs": round(nb * L * d_steps / d_el / 1e9, 2),
-            "direct_note": "the same calls as one-block jfsx_seal_batch calls from the same threads, no aggregator "
+            "direct_note": "the same calls as one-block jfsx_seal_batch / jfsx_open_batch calls from the same threads, "
+                           "no aggregator "
                            "(host batches share the context's pipeline)",
             "roofline": {"bound": "pcie", "achieved": round(value, 2), "peak": duplex, "unit": "GB/s",
                          "frac": round(value / duplex, 4), "peak_basis": "min over directions of simultaneous H2D + "
                          "D2H copies (jfsx_pcie_probe, after the run)", "pcie_measured": pcie,
                          "frac_of_link": round(value / PCIE_GEN5_X16_GBS, 4)},
             "cpu_baseline": cpu, "verified_blocks": verified, "full_check": full}), flush=True)
-    for h in (hin, hout, hcrc):
-        eng.free_pinned(h)
+    for h in (hin, hout, hcrc, hdec, hcrc2):
+        if h:
+            eng.free_pinned(h)
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
