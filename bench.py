@@ -49,9 +49,21 @@ def parse():
     ap.add_argument("--codec", choices=["lz4", "unlz4", "zstd", "unzstd"], default="zstd",
                     help="aggcodec: the Compress / Decompress call of cachedStore.upload / load measured in the "
                          "reference's call shape")
-    ap.add_argument("--agg-op", choices=["seal", "open"], default="seal",
+    ap.add_argument("--agg-op", choices=["seal", "open", "checksum", "verify", "readat"], default="seal",
                     help="agg: the per-object call measured: Seal + CRC gen (cachedStore.upload) or Open + plaintext "
-                         "CRC gen for the cache file (cachedStore.load, CS-3)")
+                         "CRC gen for the cache file (cachedStore.load, CS-3); heap buffers only: checksum() of a "
+                         "page (jfsx_agg_crc32c), the whole-block cache-hit verify (jfsx_cache_verify, level full), "
+                         "or configs[4]'s ragged ReadAt at random unaligned ranges (--level shrink|extend)")
+    ap.add_argument("--buffers", choices=["pinned", "heap"], default="pinned",
+                    help="agg: where the callers' blocks live -- engine-pinned memory, or ordinary pageable heap "
+                         "memory as the reference's Go-heap slices (encrypt.go:183, :258; page.go:42-50), staged by "
+                         "the engine's bounce pool")
+    ap.add_argument("--agg-crc", choices=["none", "seg", "obj", "both"], default="seg",
+                    help="agg --buffers heap seal/open: the checksums each data_encrypt_ex / data_decrypt_ex call "
+                         "returns: checksum() of the plaintext (seg), the object-store CRC (obj), both, or none")
+    ap.add_argument("--level", choices=["shrink", "extend"], default="shrink",
+                    help="agg --agg-op readat: the cache checksum level (disk_cache.go:1265-1307)")
+    ap.add_argument("--reads-per-block", type=int, default=4, help="agg --agg-op readat: random reads per image")
     ap.add_argument("--agg-window-us", type=int, default=500, help="agg: aggregation window")
     ap.add_argument("--agg-max-mb", type=int, default=12,
                     help="agg: byte cap of one aggregated batch (several batches pipeline at once)")
@@ -160,20 +172,70 @@ def cpu_model():
     return ""
 
 
-def cpu_baseline(args, mode="seal", lens=None):
+ORIG_AFFINITY = None  # the process's CPUs before any NUMA pinning (main)
+
+
+def node_cpu_set(node):
+    try:
+        return parse_cpulist(open("/sys/devices/system/node/node%d/cpulist" % node).read())
+    except (OSError, ValueError):
+        return set()
+
+
+def best_placement(fn, node):
+    """Run a CPU baseline fn() (-> dict with "value", "cores", "sample") on
+    every core the process may use, and again on the cores of NUMA node
+    `node` (the GPU's socket) when that is a proper subset; returns the
+    faster, with the other beside it as "other_placement".  The process's
+    affinity is restored afterwards."""
+    cur = os.sched_getaffinity(0)
+    full = set(ORIG_AFFINITY or cur)
+    runs = []
+    places = [("all %d CPUs of the process" % len(full), full)]
+    nc = node_cpu_set(node) & full if node is not None and node >= 0 else set()
+    if nc and nc != full:
+        places.append(("pinned to NUMA node %d (%d CPUs, the GPU's socket)" % (node, len(nc)), nc))
+    try:
+        for name, cpus in places:
+            os.sched_setaffinity(0, cpus)
+            r = fn()
+            r["placement"] = name
+            runs.append(r)
+    finally:
+        os.sched_setaffinity(0, cur)
+    runs.sort(key=lambda r: -r["value"])
+    best = dict(runs[0])
+    if len(runs) > 1:
+        best["other_placement"] = {k: runs[1][k] for k in ("value", "cores", "placement")}
+    best["core_s_per_GB"] = round(best["cores"] / best["value"], 4) if best["value"] else None
+    return best
+
+
+def cpu_baseline(args, mode="seal", lens=None, node=None):
     """The reference's per-block CPU work, one worker per core, timed on this
     host over a bounded sample of the same workload (about --cpu-seconds):
-      seal  checksum() + aead.Seal            (encrypt.go:192, disk_cache.go:1218-1231)
-      open  aead.Open + the ReadAt CRC verify (encrypt.go:215, disk_cache.go:1315-1327)
-      crc   the ReadAt CRC verify alone       (a cache hit)
+      seal     checksum() + aead.Seal            (encrypt.go:192, disk_cache.go:1218-1231)
+      open     aead.Open + the ReadAt CRC verify (encrypt.go:215, disk_cache.go:1315-1327)
+      crc      the ReadAt CRC verify alone       (a cache hit)
+      encrypt  dataEncryptor.Encrypt: header + Seal into the object buffer at
+               offset 271, + checksum() of the plaintext (encrypt.go:164-194)
+      objdecrypt  dataEncryptor.Decrypt: header parse + Open from offset 271,
+               + checksum() of the plaintext for the cache file (encrypt.go:196-216)
     The AEAD runs through OpenSSL EVP (AES-NI/VAES + VPCLMULQDQ stitched GCM,
     SIMD ChaCha20-Poly1305: the class of Go's assembly), the
     CRC32C as 3-stream SSE4.2 like Go's castagnoliSSE42Triple.  lens: the
-    bench's own ragged lengths (configs[4]); else 4 MiB blocks."""
+    bench's own ragged lengths (configs[4]); else 4 MiB blocks.  Run on every
+    core and on the GPU's NUMA node (node given): the faster is the baseline,
+    the other is reported beside it (best_placement)."""
+    return best_placement(lambda: _cpu_baseline_once(args, mode, lens), node)
+
+
+def _cpu_baseline_once(args, mode, lens):
     from oracle import oracle as orc
     threads, note = host_cores()
     algo = orc.AES256GCM if args.algo == "aes256gcm" else orc.CHACHA20P1305
-    bmode = {"seal": orc.BASE_SEAL, "open": orc.BASE_OPEN, "crc": orc.BASE_CRC}[mode]
+    bmode = {"seal": orc.BASE_SEAL, "open": orc.BASE_OPEN, "crc": orc.BASE_CRC, "encrypt": orc.BASE_ENCRYPT,
+             "objdecrypt": orc.BASE_DECRYPT}[mode]
     sample = [int(x) for x in lens[:256]] if lens is not None else None
     nblk = len(sample) if sample else 256  # 1 GiB of 4 MiB blocks: BASELINE.json configs[0]
     nbytes = sum(sample) if sample else nblk * BLOCK
@@ -196,11 +258,40 @@ def cpu_baseline(args, mode="seal", lens=None):
         total_s += s_
     what = {"seal": "%s seal (%s) + CRC32C full (3-stream SSE4.2)" % (args.algo, impl),
             "open": "%s open (%s, tag checked) + CRC32C verify against the stored CRCs" % (args.algo, impl),
-            "crc": "CRC32C verify against the stored CRCs (3-stream SSE4.2)"}[mode]
+            "crc": "CRC32C verify against the stored CRCs (3-stream SSE4.2)",
+            "encrypt": "dataEncryptor.Encrypt: object header (256-B wrapped key) + %s seal (%s) into the object "
+                       "buffer at offset 271 + checksum() of the plaintext (3-stream SSE4.2); the output buffer is "
+                       "reused (Go's make([]byte) and its zeroing are not charged)" % (args.algo, impl),
+            "objdecrypt": "dataEncryptor.Decrypt: header parse + %s open (%s, tag checked) from offset 271 + "
+                          "checksum() of the plaintext (3-stream SSE4.2)" % (args.algo, impl)}[mode]
     blocks = ("%d ragged blocks (the bench's own lengths, %.3f GiB)" % (nblk, nbytes / 2**30) if sample
               else "1 GiB (256 x 4 MiB blocks)")
     return {"value": round(reps * nbytes / total_s / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
             "sample": "%d x %s %s, %d threads (%s), %s" % (reps, blocks, what, threads, note, cpu_model())}
+
+
+def cpu_readat_baseline(args, lens, reads, level, node=None):
+    """cacheFile.ReadAt (disk_cache.go:1255-1329) on the host cores: the copy
+    out of the cache file and the level's CRC verify (3-stream SSE4.2), one
+    thread per core, over the bench's own images and (block, off, size) reads,
+    repeated to about --cpu-seconds; GB/s of bytes returned."""
+    from oracle import oracle as orc
+    lv = {"full": 1, "shrink": 2, "extend": 3}[level]
+
+    def once():
+        threads, note = host_cores()
+        secs, nbytes = orc.bench_readat(threads, lv, lens, SEED, reads, 1)
+        if secs < 0:
+            raise SystemExit("bench: ReadAt CPU baseline failed (rc %s)" % secs)
+        reps = max(1, min(64, int(args.cpu_seconds / max(secs, 1e-3))))
+        secs, nbytes = orc.bench_readat(threads, lv, lens, SEED, reads, reps)
+        if secs < 0:
+            raise SystemExit("bench: ReadAt CPU baseline failed (rc %s)" % secs)
+        return {"value": round(nbytes / secs / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+                "sample": "%d x %d ReadAt calls at level %s over %d cache-file images (%.3f GiB of data; the bench's "
+                          "own images and ranges), copy + CRC32C verify (3-stream SSE4.2), %d threads (%s), %s" % (
+                              reps, len(reads), level, len(lens), sum(lens) / 2**30, threads, note, cpu_model())}
+    return best_placement(once, node)
 
 
 def shard_plan(args, nshard, s):
@@ -243,13 +334,15 @@ def dry_run(args, world, rank, local, dist):
     L = args.block_bytes
     pinned = resident * (2 * L + 4 * -(-L // (32 << 10))) if args.mem == "host" else 0
     pinned_max = max_over_ranks(dist, float(pinned), local)
+    # the CPU leg runs without an engine too: rank 0, after the timed region
+    cpu = cpu_baseline(args, "seal") if rank == 0 and not args.no_cpu else None
     if rank == 0:
         print(json.dumps({"metric": "dry run (no engine)", "value": None, "unit": "GB/s", "n_gpus": world,
                           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3, 3),
                           "dry_run": True, "last_rank_first_block": int(first), "scaling": scaling(args),
                           "blocks_total": int(total), "block_range": [int(lo), int(hi)],
                           "per_gpu_blocks_max": int(per_max), "resident_blocks": resident, "loops_per_step": len(loops),
-                          "pinned_bytes_per_rank_max": int(pinned_max),
+                          "pinned_bytes_per_rank_max": int(pinned_max), "cpu_baseline": cpu,
                           "config": {"blocks_per_gpu": args.blocks, "total_gib": args.total_gib or None,
                                      "parallelism": "block-sharded x%d, no collective" % world}}), flush=True)
     if dist is not None:
@@ -261,6 +354,8 @@ def scaling(args):
 
 
 def main():
+    global ORIG_AFFINITY
+    ORIG_AFFINITY = os.sched_getaffinity(0)
     args = parse()
     if args.engine == "mctx":
         if int(os.environ.get("WORLD_SIZE", "1")) > 1:
@@ -284,6 +379,8 @@ def main():
         return resident_bench(args, world, rank, local, dist)
     eng = E.Engine(local, E.CTX_BITSLICE if args.aes == "bitslice" else 0)
     if args.mode == "agg":
+        if args.buffers == "heap" or args.agg_op in ("checksum", "verify", "readat"):
+            return agg_heap_bench(args, world, rank, local, dist, eng)
         return agg_bench(args, world, rank, local, dist, eng)
     if args.mode == "aggcodec":
         return aggcodec_bench(args, world, rank, local, dist, eng)
@@ -507,9 +604,11 @@ def resident_bench(args, world, rank, local, dist):
     k_avg_ms = sum(ms / max(n, 1) for ms, n in ktimes) / len(ktimes)
     launches = sum(n for _, n in ktimes)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:
+        # rank 0 only, after the timed region (at N > 1 the other ranks have
+        # finished their GPU work by then)
         cpu = cpu_baseline(args, "open" if mode in ("open", "decrypt") else mode,
-                           shards[0].lens if args.ragged else None)
+                           shards[0].lens if args.ragged else None, node=engs[0].numa_node())
         if mode == "decrypt" and rsa:
             # each object also pays one RSA-OAEP private-key unwrap on the host
             # (encrypt.go:207-210): per thread, block time + unwrap time
@@ -966,7 +1065,7 @@ def host_ingest(args, world, rank, local, dist):
     value = S.sum_over_ranks(dist, step_plain, local) * args.steps / el / 1e9
     ngpu = len(engs) if m else world
     peak = S.sum_over_ranks(dist, sum(sh.peak for sh in shards), local)
-    cpu = cpu_baseline(args, "seal") if rank == 0 and world == 1 and not args.no_cpu else None
+    cpu = cpu_baseline(args, "seal", node=shards[0].node) if rank == 0 and not args.no_cpu else None
     launches = sum(n for _, n in ktimes)
     plain_launch = int(step_plain * args.steps / max(launches, 1))
     traffic, traffic_src, binding = pmc_traffic(args, plain_launch)
@@ -1139,7 +1238,8 @@ def agg_bench(args, world, rank, local, dist, eng):
                         "per-object Seal calls through the aggregator: ") + full["what"]
         verified = nb
     value = world * nb * L * args.steps / el / 1e9
-    cpu = cpu_baseline(args, "open" if is_open else "seal") if rank == 0 and world == 1 and not args.no_cpu else None
+    cpu = (cpu_baseline(args, "open" if is_open else "seal", node=node) if rank == 0 and not args.no_cpu
+           else None)
     pcie = eng.pcie_probe()
     duplex = min(pcie["duplex_h2d"], pcie["duplex_d2h"])
     if rank == 0:
@@ -1171,6 +1271,318 @@ def agg_bench(args, world, rank, local, dist, eng):
     for h in (hin, hout, hcrc, hdec, hcrc2):
         if h:
             eng.free_pinned(h)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def host_cpu_seconds():
+    """user + system CPU seconds of this process so far (every thread: the
+    callers, the aggregator's dispatchers, the engine's bounce copies)"""
+    import resource
+    r = resource.getrusage(resource.RUSAGE_SELF)
+    return r.ru_utime + r.ru_stime
+
+
+def readat_ranges(lens, per_block, seed):
+    """configs[4]'s reads: per image, per_block (off, size) ranges, uniform
+    offsets and sizes (unaligned, SplitMix64 of (seed, block, k)), each
+    inside the data: [(block, off, size)]"""
+    out = []
+    for b, n in enumerate(lens):
+        for k in range(per_block):
+            z = ragged_len(seed ^ 0x5245414441, b * 64 + k, 2**40)
+            off = z % n
+            size = 1 + (z >> 20) % (n - off)
+            out.append((b, off, size))
+    return out
+
+
+def agg_heap_bench(args, world, rank, local, dist, eng):
+    """The drop-in's per-object calls on ordinary pageable heap memory (the
+    reference's Go-heap slices: io.ReadAll's result and a fresh make([]byte)
+    in Encrypt, encrypt.go:183, :258; cache pages, page.go:42-50), from
+    --threads callers at once (max-uploads, cmd/flags.go:124-128):
+      seal      jfsx_agg_data_encrypt_ex: plaintext -> object (header with a
+                256-B wrapped key, C, tag) + --agg-crc checksums
+      open      jfsx_agg_data_decrypt_ex: object -> plaintext + checksums
+      checksum  jfsx_agg_crc32c GEN: checksum() of a page (disk_cache.go:1218-1231)
+      verify    jfsx_cache_verify, level full, whole block: the cache hit
+                (disk_cache.go:1255-1329 with off 0, size = length)
+      readat    jfsx_cache_verify at --level shrink|extend on configs[4]'s
+                ragged images, random unaligned ranges
+    The engine copies each pageable block into its own pinned bounce buffer on
+    the calling thread (include/jfsx.h JFSX_MEM_HOST).  value = plaintext (or
+    returned) GB/s; host_cpu = this process's CPU seconds over the timed
+    region, beside the CPU baseline's cores x seconds for the same bytes."""
+    import ctypes
+    import threading
+    import numpy as np
+    from juicefs_amd import engine as E
+    op = args.agg_op
+    T = args.threads
+    L = args.block_bytes
+    algo = E.AES256GCM if args.algo == "aes256gcm" else E.CHACHA20P1305
+    node = eng.numa_node()
+    cpus = numa_pin(node) if node >= 0 else 0
+    ragged = op == "readat" or args.ragged
+    nb = max(1, min(args.blocks, 512) // T) * T
+    base = rank * nb
+    lens = [ragged_len(SEED, base + b, L) for b in range(nb)] if ragged else [L] * nb
+    nseg = -(-L // E.SEG)
+    cs = 4 * nseg          # CRC array stride
+    S = L + 287            # object stride: 3 + 256 + 12 header, C, 16-B tag
+    IS = L + cs            # cache-file image stride: data, BE32 CRCs
+    # heap (pageable) buffers, filled from the device generator
+    pt = np.empty(nb * L, np.uint8)
+    tmp = eng.alloc(L)
+    for b in range(nb):
+        eng.gen_synthetic(tmp, lens[b], SEED, base + b)
+        eng.sync()
+        eng._check(eng.L.jfsx_memcpy_d2h(eng.ctx, pt.ctypes.data + b * L, tmp.ptr, lens[b]), "memcpy")
+    tmp.free()
+    keys = np.zeros((nb, 32), np.uint8)
+    nonces = np.zeros((nb, 12), np.uint8)
+    for b in range(nb):
+        k, nn = E.gen_key(SEED, base + b)
+        keys[b] = np.frombuffer(bytes(k), np.uint8)
+        nonces[b] = np.frombuffer(bytes(nn), np.uint8)
+    wrapped = np.random.default_rng(SEED).integers(0, 256, 256, dtype=np.uint8)
+    segs = np.zeros(nb * cs, np.uint8)       # checksum() arrays the calls return
+    ocrc = np.zeros(nb, np.uint32)           # object-store CRCs (seal) / expected (open)
+    want_seg = args.agg_crc in ("seg", "both")
+    want_obj = args.agg_crc in ("obj", "both")
+    pp, kp, np_, wp, sp, op_ = (pt.ctypes.data, keys.ctypes.data, nonces.ctypes.data, wrapped.ctypes.data,
+                                segs.ctypes.data, ocrc.ctypes.data)
+    objs = out = imgs = reads = None
+    verified = {}
+    agg = E.Aggregator(eng, window_us=args.agg_window_us, max_bytes=args.agg_max_mb << 20)
+    A = agg.h
+    if op in ("seal", "open"):
+        objs = np.empty(nb * S, np.uint8)
+        obp = objs.ctypes.data
+        enc_agg, enc_dir = eng.L.jfsx_agg_data_encrypt_ex, eng.L.jfsx_data_encrypt_ex
+        dec_agg, dec_dir = eng.L.jfsx_agg_data_decrypt_ex, eng.L.jfsx_data_decrypt_ex
+
+        def encrypt(b, olen, h=A, fn=enc_agg, obj=want_obj, seg=want_seg):
+            return fn(h, algo, kp + 32 * b, np_ + 12 * b, wp, 256, pp + L * b, lens[b], obp + S * b, S,
+                      ctypes.byref(olen), op_ + 4 * b if obj else None, sp + cs * b if seg else None)
+        if op == "open":
+            # the stored objects (and their object CRCs) made once, untimed
+            olen = ctypes.c_uint64()
+            for b in range(nb):
+                rc = encrypt(b, olen, obj=True, seg=False)
+                if rc:
+                    raise SystemExit("bench: setup encrypt failed (%d)" % rc)
+            out = np.empty(nb * L, np.uint8)
+            dp = out.ctypes.data
+            got = np.zeros(nb, np.uint32)
+            gp = got.ctypes.data
+
+            def call_with(h, fn):
+                def call(b, st):
+                    return fn(h, algo, kp + 32 * b, obp + S * b, lens[b] + 287, dp + L * b, L, ctypes.byref(st),
+                              op_ + 4 * b if want_obj else None, gp + 4 * b if want_obj else None,
+                              sp + cs * b if want_seg else None)
+                return call
+            through, direct = call_with(A, dec_agg), call_with(eng.ctx, dec_dir)
+        else:
+            def through(b, st):
+                return encrypt(b, st)
+
+            def direct(b, st):
+                return encrypt(b, st, h=eng.ctx, fn=enc_dir)
+    elif op == "checksum":
+        R = (E.jfsx_range * nb)()
+        for b in range(nb):
+            R[b].data, R[b].len, R[b].crc = pp + L * b, lens[b], sp + cs * b
+        crc_agg, crc_dir = eng.L.jfsx_agg_crc32c, eng.L.jfsx_crc32c_segments
+
+        def through(b, st):
+            return crc_agg(A, ctypes.byref(R[b]), E.CRC_GEN, E.MEM_HOST)
+
+        def direct(b, st):
+            return crc_dir(eng.ctx, 1, ctypes.byref(R[b]), E.CRC_GEN, E.MEM_HOST)
+    else:
+        # cache-file images (data || checksum()); the trailers made by the
+        # engine itself, untimed (checked against the oracle afterwards)
+        imgs = np.empty(nb * IS, np.uint8)
+        ip = imgs.ctypes.data
+        for b in range(nb):
+            ctypes.memmove(ip + IS * b, pp + L * b, lens[b])
+        R = (E.jfsx_range * nb)()
+        for b in range(nb):
+            R[b].data, R[b].len, R[b].crc = ip + IS * b, lens[b], ip + IS * b + lens[b]
+        eng.crc32c_segments(R, nb, E.CRC_GEN, E.MEM_HOST)
+        out = np.empty(nb * L, np.uint8)
+        dp = out.ctypes.data
+        level = "full" if op == "verify" else args.level
+        lv = {"full": 1, "shrink": 2, "extend": 3}[level]
+        reads = ([(b, 0, lens[b]) for b in range(nb)] if op == "verify"
+                 else readat_ranges(lens, args.reads_per_block, SEED + base))
+        cv = eng.L.jfsx_cache_verify
+        flen = [lens[b] + 4 * max(1, -(-lens[b] // E.SEG)) for b in range(nb)]
+        nret = np.zeros(len(reads), np.uint64)
+
+        def through(r, st):
+            b, off, size = reads[r]
+            n, g, e, s = st
+            rc = cv(eng.ctx, ip + IS * b, flen[b], lens[b], lv, off, size, dp + L * b, ctypes.byref(n),
+                    ctypes.byref(g), ctypes.byref(e), ctypes.byref(s))
+            nret[r] = n.value
+            return rc
+        direct = None
+    units = list(range(len(reads))) if reads is not None else list(range(nb))
+    unit_bytes = [reads[r][2] for r in units] if reads is not None else lens
+    per = len(units) // T
+    errs = []
+
+    def run(call, steps):
+        def worker(t):
+            try:
+                st = ((ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_int64())
+                      if op in ("verify", "readat") else ctypes.c_uint64())
+                for _ in range(steps):
+                    for u in units[t * per:(t + 1) * per]:
+                        rc = call(u, st)
+                        if rc:
+                            raise RuntimeError("unit %d: jfsx rc %d" % (u, rc))
+            except BaseException as e:  # noqa: B902 -- reported below
+                errs.append(e)
+        ts = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+        t0 = time.perf_counter()
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        if errs:
+            raise SystemExit("bench: %s" % errs[0])
+        return time.perf_counter() - t0
+    step_bytes = sum(unit_bytes[:per * T])
+    d_val = None
+    if direct is not None:
+        d_steps = max(1, args.steps // 5)
+        run(direct, 1)
+        d_val = round(step_bytes * d_steps / run(direct, d_steps) / 1e9, 2)
+    warm_up(args, lambda: run(through, 1), host=True)
+    c0, b0, k0 = agg.stats()
+    m0 = eng.metrics(reset=False)
+    barrier(dist)
+    cpu0 = host_cpu_seconds()
+    el = max_over_ranks(dist, run(through, args.steps), local)
+    cpu_used = host_cpu_seconds() - cpu0
+    c1, b1, k1 = agg.stats()
+    agg.close()
+    value = world * step_bytes * args.steps / el / 1e9
+    # checker only, after the timed region
+    full = None
+    if args.verify:
+        import hashlib
+        from oracle import oracle as orc
+        oalgo = orc.AES256GCM if algo == E.AES256GCM else orc.CHACHA20P1305
+        samples = list(range(0, nb, max(1, nb // max(args.verify, 1))))[:args.verify]
+        if op in ("seal", "open"):
+            arr = segs.reshape(nb, cs).copy()
+            tags = objs.reshape(nb, S)
+            f = full_check(args, E, None, arr, lens, base) if want_seg else {"blocks": nb}
+            etags, _, _ = orc.expect_batch(oalgo, host_cores()[0], lens, SEED, base, cs)
+            gt = np.stack([tags[b, lens[b] + 271:lens[b] + 287] for b in range(nb)])
+            bad = np.nonzero((gt != etags).any(axis=1))[0]
+            if bad.size:
+                raise SystemExit("bench: object %d: tag differs from the oracle (%d objects)" % (bad[0], bad.size))
+            f["tags_sha256"] = hashlib.sha256(gt.tobytes()).hexdigest()
+            for b in samples:
+                p = orc.gen_block(SEED, base + b, lens[b])
+                key, nonce = orc.gen_key(SEED, base + b)
+                o = tags[b, :lens[b] + 287].tobytes()
+                if o != orc.data_encrypt(oalgo, key, nonce, wrapped.tobytes(), p.tobytes()):
+                    raise SystemExit("bench: object %d differs from the oracle's Encrypt" % b)
+                if op == "open" and out[L * b:L * b + lens[b]].tobytes() != p.tobytes():
+                    raise SystemExit("bench: object %d: decrypted plaintext differs from the oracle's" % b)
+            if want_obj or op == "open":
+                bad = [b for b in range(nb) if int(orc.object_checksum(tags[b, :lens[b] + 287].tobytes(), hw=True))
+                       != int(ocrc[b])]
+                if bad:
+                    raise SystemExit("bench: object %d: object CRC differs from the oracle (%d)" % (bad[0], len(bad)))
+            f["what"] = ("per-object %s calls on heap buffers: tags of all %d objects%s%s equal to the oracle's, %d "
+                         "whole objects%s equal to the oracle's Encrypt" % (
+                             "Encrypt" if op == "seal" else "Decrypt", nb,
+                             ", the calls' plaintext checksum() arrays" if want_seg else "",
+                             ", every object CRC" if (want_obj or op == "open") else "", len(samples),
+                             " and their decrypted plaintexts" if op == "open" else ""))
+            full = f
+        elif op == "checksum":
+            full = full_check(args, E, None, segs.reshape(nb, cs).copy(), lens, base)
+            full["what"] = "checksum() calls on heap pages: " + full["what"]
+        else:
+            trail = np.stack([np.pad(imgs[IS * b + lens[b]:IS * b + lens[b] + 4 * max(1, -(-lens[b] // E.SEG))],
+                                     (0, cs - 4 * max(1, -(-lens[b] // E.SEG)))) for b in range(nb)])
+            full = full_check(args, E, None, trail, lens, base)
+            want = np.array([min(s, lens[b] - o) for b, o, s in reads], np.uint64)
+            if (nret != want).any():
+                r = int(np.nonzero(nret != want)[0][0])
+                raise SystemExit("bench: read %d returned %d bytes, ReadAt returns %d" % (r, nret[r], want[r]))
+            for r in range(0, len(reads), max(1, len(reads) // max(args.verify, 1)))[:args.verify]:
+                b, o, s = reads[r]
+                img = imgs[IS * b:IS * b + lens[b] + 4 * max(1, -(-lens[b] // E.SEG))].tobytes()
+                rc, data = orc.cache_readat(img, lens[b], lv, o, s)[:2]
+                if rc != 0 or data != out[L * b:L * b + s].tobytes():
+                    raise SystemExit("bench: read %d differs from the oracle's ReadAt" % r)
+            full["what"] = ("cache-file trailers of all %d images equal to the oracle's; every one of %d %s reads "
+                            "returned ReadAt's byte count with status OK (each verified its window); %d reads' bytes "
+                            "equal to the oracle's ReadAt" % (nb, len(reads), level,
+                                                             min(args.verify, len(reads))))
+    m1 = eng.metrics(reset=False)
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        if op in ("verify", "readat"):
+            cpu = cpu_readat_baseline(args, lens, reads, "full" if op == "verify" else args.level, node=node)
+        else:
+            cpu = cpu_baseline(args, {"seal": "encrypt", "open": "objdecrypt", "checksum": "crc"}[op],
+                               lens if ragged else None, node=node)
+    pcie = eng.pcie_probe()
+    duplex = min(pcie["duplex_h2d"], pcie["duplex_d2h"])
+    gb = world * step_bytes * args.steps / 1e9
+    host_cpu = {"cpu_seconds": round(cpu_used, 3), "cpu_s_per_GB": round(cpu_used / gb, 4),
+                "cores_busy": round(cpu_used / el, 2),
+                "note": "getrusage(RUSAGE_SELF) over the timed region: every thread of this process (the Python "
+                        "callers and their ctypes calls, the aggregator's dispatchers, the bounce copies in and out)"}
+    if cpu:
+        host_cpu["cpu_baseline_core_s_per_GB"] = cpu["core_s_per_GB"]
+    what = {"seal": "encrypted+checksummed", "open": "decrypted+checksummed", "checksum": "checksummed",
+            "verify": "cache-hit verified (ReadAt, level full)", "readat": "read (ReadAt, level %s)" % args.level}[op]
+    if rank == 0:
+        print(json.dumps({
+            "metric": "per-object %s GB/s, %d threads, %s heap buffers" % (
+                what, T, "ragged 64 KiB-4 MiB" if ragged else "4 MiB"),
+            "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic (SplitMix64), pageable heap memory (numpy)",
+            "config": {"workload": "%d %s calls per step from %d threads on pageable heap buffers%s" % (
+                len(units), {"seal": "jfsx_agg_data_encrypt_ex", "open": "jfsx_agg_data_decrypt_ex",
+                             "checksum": "jfsx_agg_crc32c (GEN)", "verify": "jfsx_cache_verify (level full, whole block)",
+                             "readat": "jfsx_cache_verify (level %s, random unaligned ranges)" % args.level}[op],
+                T, (", %s, checksums: %s" % (args.algo, args.agg_crc)) if op in ("seal", "open") else ""),
+                "blocks_per_gpu": nb, "block_bytes": "ragged" if ragged else L, "algo": args.algo,
+                "mode": "agg", "op": op, "buffers": "heap", "agg_crc": args.agg_crc if op in ("seal", "open") else None,
+                "level": args.level if op == "readat" else None,
+                "reads": len(reads) if reads is not None else None, "window_us": args.agg_window_us,
+                "max_batch_bytes": args.agg_max_mb << 20, "warmup_run": getattr(args, "warm", None),
+                "numa": {"gpu_node": node, "cpus_on_node": cpus}},
+            "aggregator": {"calls": c1 - c0, "batches": b1 - b0,
+                           "mean_batch_blocks": round((k1 - k0) / max(b1 - b0, 1), 2)} if op != "verify" and
+            op != "readat" else None,
+            "direct_calls_GBs": d_val,
+            "engine_metrics_delta": {k: getattr(m1, k) - getattr(m0, k) for k in
+                                     ("seal_batches", "seal_bytes", "open_batches", "open_bytes", "crc_batches",
+                                      "crc_bytes")},
+            "host_cpu": host_cpu,
+            "roofline": {"bound": "pcie", "achieved": round(value, 2), "peak": duplex, "unit": "GB/s",
+                         "frac": round(value / duplex, 4),
+                         "peak_basis": "min over directions of simultaneous H2D + D2H copies (jfsx_pcie_probe, "
+                                       "after the run)", "pcie_measured": pcie, "h2d_one_way": pcie["h2d"],
+                         "frac_of_link": round(value / PCIE_GEN5_X16_GBS, 4)},
+            "cpu_baseline": cpu, "verified_blocks": nb if full else 0, "full_check": full}), flush=True)
     eng.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define JFSX_ABI_VERSION 8
+#define JFSX_ABI_VERSION 9
 
 /* algorithms (encrypt.go:142-145) */
 #define JFSX_AES256GCM 0     /* "aes256gcm-rsa" (also the "" default)   */
@@ -62,10 +62,25 @@ extern "C" {
  * checksums (pkg/object/checksum.go:31-53, s3.go:173-176); fold them into the
  * whole-object value with jfsx_object_crc32c. */
 #define JFSX_CRC_CT 4
+/* flag OR'ed into JFSX_CRC_GEN only: BOTH checksums in one call -- crc points
+ * at 8*max(1,ceil(len/32K)) bytes, the plaintext segment CRCs (checksum() of
+ * the block, as CRC_GEN) followed by the ciphertext segment CRCs (as
+ * CRC_GEN|CRC_CT).  This is what an upload of one block to an S3-class store
+ * with a disk cache needs: bcache.stage checksums the plaintext and the store's
+ * Put checksums the sealed object (pkg/chunk/cached_store.go:439-451,
+ * pkg/object/s3.go:173-176).  The ciphertext pass runs on the copy of the
+ * block already in device memory, so it adds no host or PCIe traffic. */
+#define JFSX_CRC_BOTH 8
 
 /* where src/dst/crc pointers of a batch live */
 #define JFSX_MEM_DEVICE 0 /* device memory (jfsx_alloc_device / hipMalloc) */
 #define JFSX_MEM_HOST 1   /* host memory; staged through the engine          */
+/* JFSX_MEM_HOST buffers may be page-locked (jfsx_alloc_pinned*, or memory the
+ * HIP runtime knows as registered) or ordinary pageable memory (a Go-heap
+ * slice, malloc).  Page-locked blocks are copied by DMA directly; the engine
+ * copies a pageable block into pinned staging it owns on the calling thread
+ * before the upload, and a pageable output out of it after the download, and
+ * never keeps a pointer to caller memory past the call (cgo's rules). */
 
 /* per-block status */
 #define JFSX_OK 0
@@ -277,6 +292,21 @@ int jfsx_agg_data_encrypt(jfsx_agg *agg, int algo, const uint8_t key[32], const 
                           uint64_t out_cap, uint64_t *out_len, uint32_t *obj_crc);
 int jfsx_agg_data_decrypt(jfsx_agg *agg, int algo, const uint8_t key[32], const void *obj, uint64_t olen, void *out,
                           uint64_t out_cap, uint64_t *out_len, const uint32_t *expect_crc, uint32_t *got_crc);
+/* The same, and checksum() of the plaintext in the same pass (seg_crc,
+ * nullable: 4*max(1,ceil(len/32K)) bytes, the cache file's trailer): the
+ * block the reference touches twice -- wSlice.upload stages it in the disk
+ * cache (bcache.stage -> checksum, disk_cache.go:433-483) and then uploads it
+ * (store.upload -> Encrypt, cached_store.go:415-472); store.load decrypts it
+ * and then caches it (bcache.cache -> checksum, cached_store.go:673-748) --
+ * crosses PCIe once.  With obj_crc / expect_crc as well, both checksums come
+ * out of the one call (JFSX_CRC_BOTH).  Decrypt: seg_crc is zeroed when the
+ * call fails (tag or object checksum), as the plaintext is. */
+int jfsx_agg_data_encrypt_ex(jfsx_agg *agg, int algo, const uint8_t key[32], const uint8_t nonce[12],
+                             const uint8_t *wrapped, int wlen, const void *plaintext, uint64_t len, void *out,
+                             uint64_t out_cap, uint64_t *out_len, uint32_t *obj_crc, uint8_t *seg_crc);
+int jfsx_agg_data_decrypt_ex(jfsx_agg *agg, int algo, const uint8_t key[32], const void *obj, uint64_t olen,
+                             void *out, uint64_t out_cap, uint64_t *out_len, const uint32_t *expect_crc,
+                             uint32_t *got_crc, uint8_t *seg_crc);
 
 /* Multi-device context (SURVEY §8b jfsx_open_ctx(dev_mask), §8e): one
  * jfsx_ctx per selected GPU (bit d of dev_mask = device d; 0 = every visible
@@ -340,6 +370,14 @@ int jfsx_data_encrypt(jfsx_ctx *ctx, int algo, const uint8_t key[32], const uint
 int jfsx_data_decrypt(jfsx_ctx *ctx, int algo, const uint8_t key[32], const void *obj, uint64_t olen,
                       void *out, uint64_t out_cap, uint64_t *out_len, const uint32_t *expect_crc,
                       uint32_t *got_crc);
+/* the two above with checksum() of the plaintext in the same pass (seg_crc,
+ * nullable; see jfsx_agg_data_encrypt_ex) */
+int jfsx_data_encrypt_ex(jfsx_ctx *ctx, int algo, const uint8_t key[32], const uint8_t nonce[12],
+                         const uint8_t *wrapped, int wlen, const void *plaintext, uint64_t len, void *out,
+                         uint64_t out_cap, uint64_t *out_len, uint32_t *obj_crc, uint8_t *seg_crc);
+int jfsx_data_decrypt_ex(jfsx_ctx *ctx, int algo, const uint8_t key[32], const void *obj, uint64_t olen,
+                         void *out, uint64_t out_cap, uint64_t *out_len, const uint32_t *expect_crc,
+                         uint32_t *got_crc, uint8_t *seg_crc);
 
 /* crc32.Update(crc, MakeTable(Castagnoli), data) on the host (small spans:
  * object header and tag) */

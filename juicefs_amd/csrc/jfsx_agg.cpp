@@ -264,10 +264,11 @@ struct jfsx_agg {
         }
     }
 
-    // Host-memory Seal / Open pipeline through the context (jfsx_seal_batch):
-    // several such batches of one device run at once.  Everything else holds
-    // its context for the whole call, so a device runs one of those at a time.
-    static bool piped(const Req &r) { return (r.op == kSeal || r.op == kOpen) && r.mem == JFSX_MEM_HOST; }
+    // Host-memory Seal / Open / CRC calls pipeline through the context
+    // (jfsx_seal_batch, jfsx_crc32c_segments): several such batches of one
+    // device run at once.  Everything else holds its context for the whole
+    // call, so a device runs one of those at a time.
+    static bool piped(const Req &r) { return (r.op == kSeal || r.op == kOpen || r.op == kCrc) && r.mem == JFSX_MEM_HOST; }
 
     // Dispatcher k: take the group of the oldest request once it is full (block
     // or byte cap) or its window has closed -- or, for a pipelined group, as

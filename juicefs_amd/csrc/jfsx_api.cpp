@@ -20,6 +20,7 @@
 #include <map>
 #include <mutex>
 #include <shared_mutex>
+#include <thread>
 #include <vector>
 
 #include "jfsx_internal.h"
@@ -86,6 +87,55 @@ void note_alloc(void *p, size_t bytes, int device) {
 void forget_alloc(void *p) {
     std::unique_lock<std::shared_mutex> g(g_alloc_mu);
     g_allocs.erase((uintptr_t)p);
+}
+
+// Page-locked host allocations made through jfsx_alloc_pinned(_node), by
+// address: a host call streams such blocks with no bounce copy.
+std::shared_mutex g_pin_mu;
+std::map<uintptr_t, uintptr_t> g_pinned;  // base -> end
+
+void note_pinned(void *p, size_t bytes) {
+    std::unique_lock<std::shared_mutex> g(g_pin_mu);
+    g_pinned[(uintptr_t)p] = (uintptr_t)p + bytes;
+}
+void forget_pinned(void *p) {
+    std::unique_lock<std::shared_mutex> g(g_pin_mu);
+    g_pinned.erase((uintptr_t)p);
+}
+
+// JFSX_HOST_BOUNCE: "auto" (default) bounces pageable memory only, "0" never
+// bounces (pageable pointers go to hipMemcpyAsync as they are: the runtime's
+// own staged copy, an A/B reference), "all" bounces every host block.
+int bounce_policy() {
+    static const int v = [] {
+        const char *e = getenv("JFSX_HOST_BOUNCE");
+        if (!e || !strcmp(e, "auto")) return 1;
+        if (!strcmp(e, "0")) return 0;
+        return 2;
+    }();
+    return v;
+}
+
+// true when [p, p + n) may be handed to the DMA engines as it is: engine-pinned
+// memory, or host memory the HIP runtime reports as registered (another
+// library's pinned buffers).  Everything else -- the Go heap, malloc, numpy --
+// is pageable and goes through the context's bounce pool.
+bool host_pinned(const void *p, uint64_t n) {
+    const int pol = bounce_policy();
+    if (pol != 1 || !n) return pol != 2;
+    const uintptr_t a = (uintptr_t)p;
+    {
+        std::shared_lock<std::shared_mutex> g(g_pin_mu);
+        auto it = g_pinned.upper_bound(a);
+        if (it != g_pinned.begin()) {
+            --it;
+            if (a < it->second) return a + n <= it->second;
+        }
+    }
+    hipPointerAttribute_t at;
+    const bool reg = hipPointerGetAttributes(&at, p) == hipSuccess && at.type == hipMemoryTypeHost;
+    (void)hipGetLastError();
+    return reg;
 }
 
 // ---------------------------------------------------------------------------
@@ -209,6 +259,7 @@ struct Workspace {
     size_t crc_off = 0;     // host_crc GEN: offset of the CRC words in that download
     size_t res_off = 0;     // offset of the results (BlkOut[n], CRC words) in h
     bool crc_back = false;  // host_crc GEN: finish_aead copies the CRC words to the callers' arrays
+    int crc_mult = 1;       // CRC arrays per block (2 with JFSX_CRC_BOTH)
     bool timed = false;     // the batch's main kernel is bracketed by timing events
 };
 
@@ -239,6 +290,23 @@ struct PipeGroup {
     jfsx_blk *dv = nullptr;  // the call's per-block result records of this group
     bool open = false;
     int rc = 0;
+    char *bounce = nullptr;  // pinned bounce region of the group's pageable blocks (owner only)
+    size_t bcap = 0;
+};
+
+// Engine-owned pinned staging for callers' pageable memory (SURVEY §8b
+// "Ownership": the reference's pages and objects are Go-heap slices,
+// pkg/chunk/page.go:42-50, pkg/object/encrypt.go:183, :258).  A host call
+// copies its pageable blocks into a bounce buffer on its own thread before it
+// enqueues them, and out of it on its own thread after its D2H, so concurrent
+// callers copy in parallel and the DMA engines only ever see page-locked
+// memory.  Grow-only per context: idle buffers are kept (up to a retention
+// cap) and handed to the next call whose group fits.
+struct BouncePool {
+    std::mutex mu;
+    std::multimap<size_t, char *> idle;  // capacity -> buffer
+    size_t idle_bytes = 0;
+    std::atomic<uint64_t> allocs{0}, bytes_in{0}, bytes_out{0};
 };
 
 }  // namespace
@@ -272,10 +340,9 @@ struct jfsx_ctx {
     size_t rsa_hcap = 0;
     double ms_total = 0;
     uint64_t launches = 0;
-    std::mutex arena_mu;     // cache-verify staging (jfsx_cache_verify)
-    char *arena = nullptr;   // pinned, grow-only
-    size_t arena_cap = 0;
-    std::mutex err_mu;       // last HIP failure on this context (jfsx_last_error)
+    BouncePool bounce;       // pinned staging of pageable caller memory (host calls)
+    int numa_node = -1;      // host NUMA node of the device (bounce buffers are placed there)
+    std::mutex err_mu;     // last HIP failure on this context (jfsx_last_error)
     ErrRec err;
     jfsx_metrics met{};      // jfsx_ctx_metrics (updated under mu)
 };
@@ -422,9 +489,19 @@ constexpr uint64_t kGcmMaxLen = (((uint64_t)1 << 32) - 2) * 16;
 constexpr uint64_t kGcmMinTask = 2 * (uint64_t)kSeg;  // 64 KiB
 constexpr uint64_t kCpMaxLen = ((uint64_t)1 << 38) - 64;
 
+// bytes per task of crc_segments_k: up to kCrcTaskBytes, but small enough that
+// a small batch still spreads over every CU (~2 tasks per CU), and a whole
+// number of 16-segment rounds (one 16-wave workgroup per task, jfsx_crc.hip)
+uint64_t crc_task_bytes(uint64_t total) {
+    const uint64_t round = 16 * (uint64_t)kSeg;
+    return std::min<uint64_t>(kCrcTaskBytes, std::max<uint64_t>(round, (total / 512 + round - 1) / round * round));
+}
+
 int check_aead_args(int algo, int n, const jfsx_blk *blks, int crc_mode, bool device) {
     if (algo != JFSX_AES256GCM && algo != JFSX_CHACHA20P1305) return JFSX_EINVAL;
-    if (crc_mode < 0 || (crc_mode & ~(3 | JFSX_CRC_CT)) || (crc_mode & 3) == 3 || crc_mode == JFSX_CRC_CT || n < 0)
+    // NONE, GEN, VERIFY, GEN|CT, VERIFY|CT, GEN|BOTH
+    if (crc_mode < 0 || (crc_mode & ~(3 | JFSX_CRC_CT | JFSX_CRC_BOTH)) || (crc_mode & 3) == 3 ||
+        crc_mode == JFSX_CRC_CT || ((crc_mode & JFSX_CRC_BOTH) && crc_mode != (JFSX_CRC_GEN | JFSX_CRC_BOTH)) || n < 0)
         return JFSX_EINVAL;
     for (int i = 0; i < n; i++) {
         const jfsx_blk &b = blks[i];
@@ -465,12 +542,27 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
                  bool collect = true, hipStream_t fin = nullptr, hipEvent_t main_ev = nullptr,
                  bool host_crc = false, bool zc = false) {
     const bool gcm = algo == JFSX_AES256GCM;
+    // JFSX_CRC_BOTH: the AEAD kernels checksum the plaintext (CRC_GEN) into the
+    // first half of each CRC array and crc_segments_k checksums the ciphertext
+    // in device memory into the second half -- before an in-place Open
+    // overwrites it, after a Seal wrote it
+    const bool both = (crc_mode & JFSX_CRC_BOTH) != 0;
+    const int mult = both ? 2 : 1;
+    crc_mode &= ~JFSX_CRC_BOTH;
     std::vector<uint64_t> lens(n);
     uint64_t crc_calc_words = 0, crc_words = 0;
     for (int i = 0; i < n; i++) {
         lens[i] = blks[i].len;
         if ((crc_mode & 3) == JFSX_CRC_VERIFY) crc_calc_words += nseg_of(blks[i].len);
-        crc_words += nseg_of(blks[i].len);
+        crc_words += mult * nseg_of(blks[i].len);
+    }
+    std::vector<Task> ctasks;  // the ciphertext pass (BOTH)
+    if (both) {
+        uint64_t total = 0;
+        for (int i = 0; i < n; i++) total += lens[i];
+        const uint64_t per = crc_task_bytes(total);
+        for (int i = 0; i < n; i++)
+            for (uint64_t c0 = 0; c0 < lens[i]; c0 += per) ctasks.push_back(Task{(uint32_t)i, 0, c0, std::min(c0 + per, lens[i])});
     }
     const bool hc_in = host_crc && (crc_mode & 3) == JFSX_CRC_VERIFY;
     const bool hc_out = host_crc && (crc_mode & 3) == JFSX_CRC_GEN;
@@ -489,6 +581,8 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
     const size_t o_tagin = off; off = align256(off + 16 * (size_t)n);
     const size_t o_queue = off; off = align256(off + 4);  // persistent kernel's task counter (uploaded as 0)
     const size_t o_crcin = off; if (hc_in) off = align256(off + 4 * crc_words);
+    const size_t o_cblk = off; if (both) off = align256(off + sizeof(BlkDev) * n);
+    const size_t o_ctask = off; if (both) off = align256(off + sizeof(Task) * std::max<size_t>(ctasks.size(), 1));
     const size_t h_bytes = off;  // everything above is uploaded from the pinned mirror
     const size_t o_out = off; off = align256(off + sizeof(BlkOut) * n);
     const size_t o_crcout = off; if (hc_out) off = align256(off + 4 * crc_words);
@@ -521,9 +615,16 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
             hb[i].crc = (uint8_t *)(d + o_crcin + 4 * cw);
         } else if (hc_out) {
             hb[i].crc = zc ? (uint8_t *)(h + o_hres + (o_crcout - o_out) + 4 * cw) : (uint8_t *)(d + o_crcout + 4 * cw);
-            if (zc && b.len == 0) *(uint32_t *)hb[i].crc = 0;  // checksum() of nothing: one zero word
+            if (zc && b.len == 0) memset(hb[i].crc, 0, 4 * mult);  // checksum() of nothing: one zero word
         }
-        cw += nseg_of(b.len);
+        if (both) {
+            BlkDev &cb = ((BlkDev *)(h + o_cblk))[i];
+            memset(&cb, 0, sizeof(cb));
+            cb.src = open ? hb[i].src : hb[i].dst;
+            cb.len = b.len;
+            cb.crc = hb[i].crc + 4 * nseg_of(b.len);
+        }
+        cw += mult * nseg_of(b.len);
         hb[i].crc_calc = nullptr;
         if ((crc_mode & 3) == JFSX_CRC_VERIFY) {
             hb[i].crc_calc = (uint32_t *)(d + o_calc) + calc;
@@ -553,6 +654,11 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
         // critical path for every batch
         order_largest_first(ht, nt, (size_t)(gcm ? kMaxTaskBytes : kCpTaskBytes) >> 12);
     }
+    if (!ctasks.empty()) memcpy(h + o_ctask, ctasks.data(), sizeof(Task) * ctasks.size());
+    // the ciphertext pass of BOTH on stream st
+    auto ct_pass = [&](hipStream_t st) {
+        launch_crc_segments(st, (int)ctasks.size(), (const Task *)(d + o_ctask), (const BlkDev *)(d + o_cblk), c->tabs);
+    };
     const KeyIn *dk = (const KeyIn *)(d + o_keys);
     const BlkDev *db = (const BlkDev *)(d + o_blk);
     const Task *dt = (const Task *)(d + o_task);
@@ -584,7 +690,8 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
     }
     if ((crc_mode & 3) == JFSX_CRC_GEN && !(zc && hc_out))
         for (int i = 0; i < n; i++)
-            if (blks[i].len == 0) HIP_OK(hipMemsetAsync(hb[i].crc, 0, 4, s));
+            if (blks[i].len == 0) HIP_OK(hipMemsetAsync(hb[i].crc, 0, 4 * mult, s));
+    if (both && open) ct_pass(s);
     if (c->timing) HIP_OK(hipEventRecord(k0, s));
     if (gcm)
         launch_gcm_main(s, (int)nt, c->ncu, dq, open, crc_mode, c->bitslice, dt, db, (const GcmSched *)(d + o_sched),
@@ -593,6 +700,7 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
         launch_cp_main(s, (int)nt, c->ncu, dq, open, crc_mode, dt, db, (const CpSched *)(d + o_sched), dpart, dpexp,
                        c->tabs);
     if (c->timing) HIP_OK(hipEventRecord(k1, s));
+    if (both && !open) ct_pass(s);
     if (fin) {
         HIP_OK(hipEventRecord(main_ev, s));
         HIP_OK(hipStreamWaitEvent(fs, main_ev, 0));
@@ -606,6 +714,7 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
     w.down = zc ? 0 : down;
     w.crc_off = o_crcout - o_out;
     w.crc_back = hc_out;
+    w.crc_mult = mult;
     w.res_off = o_hres;
     if (collect && !zc) HIP_OK(hipMemcpyAsync(h, dout, down, hipMemcpyDeviceToHost, fs));
     w.n = n;
@@ -634,7 +743,7 @@ int finish_aead(jfsx_ctx *c, Workspace &w, hipEvent_t k0, hipEvent_t k1, bool op
     if (w.crc_back) {
         const char *hw = w.h + w.res_off + w.crc_off;
         for (int i = 0; i < w.n; i++) {
-            const size_t cb = 4 * nseg_of(blks[i].len);
+            const size_t cb = 4 * (size_t)w.crc_mult * nseg_of(blks[i].len);
             memcpy(blks[i].crc, hw, cb);
             hw += cb;
         }
@@ -711,9 +820,95 @@ std::vector<std::pair<int, int>> host_groups(const jfsx_ctx *c, int n, const jfs
     return groups;
 }
 
+// Enqueue the CRC-only transform (crc_segments_k + crc_finalize_k) for n
+// ranges of device memory, given as block records (src, len, crc), on stream
+// s with workspace w: the counterpart of enqueue_aead for checksum() and the
+// ReadAt verify (disk_cache.go:1218-1231, :1315-1327).  up / up_ev, collect,
+// host_crc and zc mean what they mean for enqueue_aead: the host pipeline
+// passes the data's upload stream, keeps the CRC arrays in the descriptor
+// upload (VERIFY) and the result download (GEN), and lets the compute stream
+// pull the descriptors out of the pinned mirror.
+int enqueue_crc(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEvent_t k1, int n, const jfsx_blk *blks,
+                int mode, hipStream_t up = nullptr, hipEvent_t up_ev = nullptr, bool collect = true,
+                bool host_crc = false, bool zc = false) {
+    uint64_t total = 0, calc_words = 0, crc_words = 0;
+    for (int i = 0; i < n; i++) {
+        total += blks[i].len;
+        crc_words += nseg_of(blks[i].len);
+        if (mode == JFSX_CRC_VERIFY) calc_words += nseg_of(blks[i].len);
+    }
+    const uint64_t per = crc_task_bytes(total);
+    std::vector<Task> tasks;
+    for (int i = 0; i < n; i++)
+        for (uint64_t c0 = 0; c0 < blks[i].len; c0 += per)
+            tasks.push_back(Task{(uint32_t)i, 0, c0, std::min(c0 + per, blks[i].len)});
+    const bool hc_in = host_crc && mode == JFSX_CRC_VERIFY, hc_out = host_crc && mode == JFSX_CRC_GEN;
+    const size_t nt = tasks.size();
+    size_t off = 0;
+    const size_t o_blk = off; off = align256(off + sizeof(BlkDev) * n);
+    const size_t o_task = off; off = align256(off + sizeof(Task) * std::max<size_t>(nt, 1));
+    const size_t o_crcin = off; if (hc_in) off = align256(off + 4 * crc_words);
+    const size_t h_bytes = off;
+    const size_t o_out = off; off = align256(off + sizeof(BlkOut) * n);
+    const size_t o_crcout = off; if (hc_out) off = align256(off + 4 * crc_words);
+    const size_t down = hc_out ? o_crcout + 4 * crc_words - o_out : sizeof(BlkOut) * n;
+    const size_t o_calc = off; off = align256(off + 4 * std::max<uint64_t>(calc_words, 1));
+    int rc;
+    if ((rc = ensure_dev(c, &w.d, &w.dcap, off))) return rc;
+    const size_t o_hres = zc ? h_bytes : 0;
+    if ((rc = ensure_host(&w.h, &w.hcap, zc ? h_bytes + down : std::max(h_bytes, down)))) return rc;
+    char *h = w.h, *d = w.d;
+    BlkDev *hb = (BlkDev *)(h + o_blk);
+    uint64_t calc = 0, cw = 0;
+    for (int i = 0; i < n; i++) {
+        const jfsx_blk &b = blks[i];
+        memset(&hb[i], 0, sizeof(BlkDev));
+        hb[i].src = (const uint8_t *)b.src;
+        hb[i].len = b.len;
+        hb[i].crc = b.crc;
+        if (hc_in) {
+            memcpy(h + o_crcin + 4 * cw, b.crc, 4 * nseg_of(b.len));
+            hb[i].crc = (uint8_t *)(d + o_crcin + 4 * cw);
+        } else if (hc_out) {
+            hb[i].crc = zc ? (uint8_t *)(h + o_hres + (o_crcout - o_out) + 4 * cw) : (uint8_t *)(d + o_crcout + 4 * cw);
+        }
+        cw += nseg_of(b.len);
+        if (mode == JFSX_CRC_VERIFY) {
+            hb[i].crc_calc = (uint32_t *)(d + o_calc) + calc;
+            calc += nseg_of(b.len);
+        }
+    }
+    if (nt) memcpy(h + o_task, tasks.data(), sizeof(Task) * nt);
+    BlkOut *dout = zc ? (BlkOut *)(h + o_hres) : (BlkOut *)(d + o_out);
+    launch_begin();
+    if (zc) launch_pull(s, d, h, h_bytes);
+    else HIP_OK(hipMemcpyAsync(d, h, h_bytes, hipMemcpyHostToDevice, up ? up : s));
+    if (up) {
+        HIP_OK(hipEventRecord(up_ev, up));
+        HIP_OK(hipStreamWaitEvent(s, up_ev, 0));
+    }
+    if (c->timing) HIP_OK(hipEventRecord(k0, s));
+    launch_crc_segments(s, (int)nt, (const Task *)(d + o_task), (const BlkDev *)(d + o_blk), c->tabs);
+    if (c->timing) HIP_OK(hipEventRecord(k1, s));
+    launch_crc_finalize(s, n, mode, (const BlkDev *)(d + o_blk), dout);
+    HIP_OK(hipGetLastError());
+    w.dout = dout;
+    w.down = zc ? 0 : down;
+    w.crc_off = o_crcout - o_out;
+    w.crc_back = hc_out;
+    w.crc_mult = 1;
+    w.res_off = o_hres;
+    if (collect && !zc) HIP_OK(hipMemcpyAsync(h, dout, down, hipMemcpyDeviceToHost, s));
+    w.n = n;
+    w.nt = nt;
+    w.timed = c->timing;
+    return 0;
+}
+
 // Collect the group in flight in slot s (s.mu held; called by the group's own
 // caller, or by any caller that needs the slot next): wait for its D2H and
-// write its per-block results into the owner's records.
+// write its per-block results into the owner's records.  Only results: the
+// owner copies its bounced outputs out itself.
 void pipe_collect(jfsx_ctx *c, PipeSlot &s) {
     PipeGroup *g = s.owner;
     if (!g) return;
@@ -731,14 +926,6 @@ void pipe_collect(jfsx_ctx *c, PipeSlot &s) {
     g->rc = finish_aead(c, s.w, s.ev_k0, s.ev_k1, g->open, g->dv);
 }
 
-// One group into an empty slot (c->mu and s.mu held): the blocks' data runs up
-// on s_in into the slot's staging (coalesced where the callers' blocks are
-// adjacent), then the descriptors with any VERIFY CRC arrays; keysetup / main
-// / finalize on the transform stream; the outputs, then the BlkOut records
-// with any GEN CRC arrays, down on s_out, chained by the slot's events.  dv[i]
-// (the call's copy of blks[i]) is pointed at the staging copy.  (A variant
-// whose kernel wrote the outputs straight into engine-pinned caller memory
-// over PCIe ran at 25 GB/s against 38.7 staged and was removed.)
 // The host pipeline's metadata path: with it (the default) the compute stream
 // pulls each group's descriptors out of the pinned mirror with a small kernel
 // and finalize writes the per-block results (and GEN CRC words) straight into
@@ -753,7 +940,19 @@ bool zero_copy_meta() {
     return v;
 }
 
-int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, int algo, bool open, int nb, const jfsx_blk *blks, jfsx_blk *dv,
+enum PipeOp { kPipeSeal, kPipeOpen, kPipeCrc };
+
+// One group into an empty slot (s.mu and c->mu held): the blocks' data runs up
+// on s_in into the slot's staging (coalesced where the blocks are adjacent in
+// host memory -- a group's bounced blocks always are), then the transform on
+// the compute stream (AEAD: keysetup / main / finalize; CRC: crc_segments /
+// crc_finalize); the AEAD outputs run down on s_out, chained by the slot's
+// events.  blks hold page-locked host addresses only (run_host substituted the
+// bounce buffer for pageable ones); dv[i] (the call's copy of the caller's
+// record) is pointed at the staging copy.  (A variant whose kernel wrote the
+// outputs straight into engine-pinned caller memory over PCIe ran at 25 GB/s
+// against 38.7 staged and was removed.)
+int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, PipeOp op, int algo, int nb, const jfsx_blk *blks, jfsx_blk *dv,
                  int crc_mode) {
     Workspace &w = s.w;
     size_t need = 0;
@@ -761,10 +960,10 @@ int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, int algo, bool open, int nb, const jf
     int rc;
     if ((rc = ensure_dev(c, &w.stage, &w.scap, std::max<size_t>(need, 256)))) return rc;
     size_t off = 0;
-    // staging in the order of the callers' source addresses: blocks that are
-    // neighbours in host memory (pages of one pinned pool) then sit side by
-    // side in staging too, and their copies coalesce both ways whatever order
-    // the callers submitted them in
+    // staging in the order of the source addresses: blocks that are
+    // neighbours in host memory (pages of one pinned pool, or one bounce
+    // buffer) then sit side by side in staging too, and their copies coalesce
+    // both ways whatever order the callers submitted them in
     std::vector<int> ord(nb);
     for (int i = 0; i < nb; i++) ord[i] = i;
     if (nb > 1)
@@ -796,18 +995,21 @@ int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, int algo, bool open, int nb, const jf
             if (align256(blks[i].len) != blks[i].len && (rc = flush_in())) return rc;
         }
         dv[i].src = buf;
-        dv[i].dst = buf;
+        dv[i].dst = op == kPipeCrc ? nullptr : buf;
     }
     if ((rc = flush_in())) return rc;
-    // keysetup, main and finalize on the compute stream.  (Moving keysetup onto
-    // s_in and finalize onto s_out, to overlap them with neighbouring groups'
-    // main kernels, measured 30-33 GB/s against 38-40 at 20 per-object callers:
-    // the copy engines then wait behind those kernels.)
-    // the CRC arrays pass through the descriptor upload and the result
-    // download (host_crc)
-    if ((rc = enqueue_aead(c, w, c->stream, s.ev_k0, s.ev_k1, algo, open, nb, dv, crc_mode, c->s_in, s.ev_in, false,
-                           nullptr, nullptr, true, zero_copy_meta())))
-        return rc;
+    // the transform on the compute stream.  (Moving keysetup onto s_in and
+    // finalize onto s_out, to overlap them with neighbouring groups' main
+    // kernels, measured 30-33 GB/s against 38-40 at 20 per-object callers:
+    // the copy engines then wait behind those kernels.)  The CRC arrays pass
+    // through the descriptor upload and the result download (host_crc).
+    if (op == kPipeCrc)
+        rc = enqueue_crc(c, w, c->stream, s.ev_k0, s.ev_k1, nb, dv, crc_mode, c->s_in, s.ev_in, false, true,
+                         zero_copy_meta());
+    else
+        rc = enqueue_aead(c, w, c->stream, s.ev_k0, s.ev_k1, algo, op == kPipeOpen, nb, dv, crc_mode, c->s_in,
+                          s.ev_in, false, nullptr, nullptr, true, zero_copy_meta());
+    if (rc) return rc;
     HIP_OK(hipEventRecord(s.ev_comp, c->stream));
     HIP_OK(hipStreamWaitEvent(c->s_out, s.ev_comp, 0));
     char *oh = nullptr;
@@ -821,7 +1023,7 @@ int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, int algo, bool open, int nb, const jf
         on = 0;
         return 0;
     };
-    for (int k = 0; k < nb; k++) {
+    for (int k = 0; k < nb && op != kPipeCrc; k++) {
         const int i = ord[k];
         if (!blks[i].len) continue;
         char *hd = (char *)blks[i].dst;
@@ -840,62 +1042,260 @@ int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, int algo, bool open, int nb, const jf
     return 0;
 }
 
-// Host-memory batch (host ingest and the per-object shim).  No lock is held
-// while the call waits: groups are enqueued one at a time under c->mu into the
-// next pipeline slot (collecting whatever group still occupies it), then the
-// call waits for its own groups' D2H events.  So concurrent callers keep the
-// H2D and D2H engines busy back to back instead of filling and draining the
-// ring once per call.  Open releases no plaintext of a block whose tag failed:
-// its destination is wiped before the call returns.  On an enqueue error the
-// three streams are drained first, so an error return means nothing of the
-// batch is still copying into the caller's buffers.
-int run_aead_host(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mode) {
-    int rc = check_aead_args(algo, n, blks, crc_mode, false);
-    if (rc || n == 0) return rc;
+// A pipeline slot for the next group, locked.  Under c->mu only the choice is
+// made: the first slot from the ring position on that is unlocked and whose
+// group (if any) has finished its D2H, else the next slot in ring order.  The
+// wait for a busy slot then happens under that slot's lock alone, so a caller
+// waiting for another caller's group holds up nothing else on the context
+// (device batches, CRC and codec calls, other callers' enqueues).
+PipeSlot *claim_slot(jfsx_ctx *c) {
+    PipeSlot *s = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        for (int k = 0; k < kPipe && !s; k++) {
+            PipeSlot &q = c->pipe[(c->pipe_next + k) % kPipe];
+            if (!q.mu.try_lock()) continue;
+            bool idle = !q.owner;
+            if (!idle) {
+                idle = hipEventQuery(q.ev_out) == hipSuccess;
+                (void)hipGetLastError();  // hipErrorNotReady is not a failure of this call
+            }
+            if (idle) {
+                s = &q;
+                c->pipe_next = (c->pipe_next + k + 1) % kPipe;
+            } else {
+                q.mu.unlock();
+            }
+        }
+        if (s) return s;
+        s = &c->pipe[c->pipe_next];
+        c->pipe_next = (c->pipe_next + 1) % kPipe;
+    }
+    s->mu.lock();
+    return s;
+}
+
+// bounce buffers: capacity classes of 1 MiB up to 16 MiB, then 16 MiB
+size_t bounce_class(size_t need) {
+    const size_t mib = (size_t)1 << 20, step = need <= 16 * mib ? mib : 16 * mib;
+    return (std::max<size_t>(need, 1) + step - 1) / step * step;
+}
+
+// idle buffers kept per context (JFSX_BOUNCE_RETAIN_MB, default 1 GiB)
+size_t bounce_retain() {
+    static const size_t v = [] {
+        const char *e = getenv("JFSX_BOUNCE_RETAIN_MB");
+        return (e ? (size_t)atoll(e) : (size_t)1024) << 20;
+    }();
+    return v;
+}
+
+int alloc_pinned_on(int node, size_t bytes, void **p);
+
+char *bounce_get(jfsx_ctx *c, size_t need, size_t *cap) {
+    BouncePool &b = c->bounce;
+    {
+        std::lock_guard<std::mutex> g(b.mu);
+        auto it = b.idle.lower_bound(need);
+        if (it != b.idle.end() && it->first <= std::max(2 * need, need + ((size_t)1 << 20))) {
+            char *p = it->second;
+            *cap = it->first;
+            b.idle_bytes -= it->first;
+            b.idle.erase(it);
+            return p;
+        }
+    }
+    const size_t n = bounce_class(need);
+    void *p = nullptr;
+    if (alloc_pinned_on(c->numa_node, n, &p)) return nullptr;
+    b.allocs++;
+    *cap = n;
+    return (char *)p;
+}
+
+void bounce_put(jfsx_ctx *c, char *p, size_t cap) {
+    BouncePool &b = c->bounce;
+    {
+        std::lock_guard<std::mutex> g(b.mu);
+        if (b.idle_bytes + cap <= bounce_retain()) {
+            b.idle.emplace(cap, p);
+            b.idle_bytes += cap;
+            return;
+        }
+    }
+    (void)hipHostFree(p);
+}
+
+// memcpy of a group's blocks into / out of its bounce buffer: on the calling
+// thread (each per-object caller copies its own block, so max-uploads callers
+// copy in parallel); one caller's big group (a host-ingest batch from pageable
+// memory) is split over helper threads so the host copy keeps up with PCIe
+int copy_threads() {  // JFSX_COPY_THREADS (default 8)
+    static const int v = [] {
+        const char *e = getenv("JFSX_COPY_THREADS");
+        const int t = e ? atoi(e) : 8;
+        return t >= 1 && t <= 64 ? t : 8;
+    }();
+    return v;
+}
+
+void par_copy(std::vector<std::pair<char *, const char *>> &ds, const std::vector<size_t> &lens) {
+    size_t total = 0;
+    for (size_t l : lens) total += l;
+    const size_t mib = (size_t)1 << 20;
+    const int nt = total >= 32 * mib ? (int)std::min<size_t>((size_t)copy_threads(), total / (8 * mib)) : 1;
+    // bytes [lo, hi) of the concatenated items
+    auto work = [&](size_t lo, size_t hi) {
+        size_t base = 0;
+        for (size_t k = 0; k < ds.size() && base < hi; base += lens[k], k++) {
+            const size_t a = std::max(lo, base), b = std::min(hi, base + lens[k]);
+            if (a < b) memcpy(ds[k].first + (a - base), ds[k].second + (a - base), b - a);
+        }
+    };
+    if (nt <= 1) {
+        work(0, total);
+        return;
+    }
+    std::vector<std::thread> ts;
+    for (int t = 1; t < nt; t++) ts.emplace_back(work, total * t / nt, total * (t + 1) / nt);
+    work(0, total / nt);
+    for (std::thread &t : ts) t.join();
+}
+
+// Host-memory call (host ingest, the per-object shim, checksum() / ReadAt
+// verify on host memory).  The call is cut into groups; for each group the
+// calling thread (1) copies its pageable blocks into a bounce buffer, (2)
+// claims a pipeline slot, collects whatever group still occupies it, (3)
+// enqueues the group under c->mu and moves on.  It then waits for its own
+// groups' D2H events only, copying each group's bounced outputs out as it
+// completes (after at most a few groups in flight, when it holds bounce
+// buffers, so one big pageable call pins no more than that).  So concurrent
+// callers keep the H2D and D2H engines busy back to back instead of filling
+// and draining the ring once per call.  Open releases no plaintext of a block
+// whose tag failed: its destination is wiped before the call returns.  On an
+// enqueue error the three streams are drained first, so an error return means
+// nothing of the call is still copying into the caller's buffers.
+int run_host(jfsx_ctx *c, PipeOp op, int algo, int n, jfsx_blk *blks, int crc_mode) {
+    int rc = 0;
+    const bool open = op == kPipeOpen;
     const std::vector<std::pair<int, int>> groups = host_groups(c, n, blks, crc_mode);
-    std::vector<jfsx_blk> dv(blks, blks + n);
+    std::vector<jfsx_blk> dv(blks, blks + n), hv(blks, blks + n);
+    std::vector<char> out_b(n, 0);  // block i's output sits in the bounce buffer
     std::vector<PipeGroup> recs(groups.size());
-    size_t issued = 0;
+    size_t issued = 0, done = 0, held = 0;  // groups enqueued / finished; bounce bytes held
     using SClock = std::chrono::steady_clock;
     auto us = [](SClock::time_point a, SClock::time_point b) {
         return (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(b - a).count();
     };
+    std::vector<std::pair<char *, const char *>> cp;
+    std::vector<size_t> cl;
+    // wait for group g, copy its bounced outputs out, release its bounce buffer
+    auto finish = [&](size_t g) {
+        PipeGroup &r = recs[g];
+        {
+            std::lock_guard<std::mutex> sl(r.slot->mu);
+            if (r.slot->owner == &r) pipe_collect(c, *r.slot);
+        }
+        if (!r.rc) {
+            cp.clear();
+            cl.clear();
+            for (int i = groups[g].first; i < groups[g].second; i++)
+                if (out_b[i] && !(open && dv[i].status == JFSX_ETAG)) {
+                    cp.push_back({(char *)blks[i].dst, (const char *)hv[i].dst});
+                    cl.push_back(blks[i].len);
+                    c->bounce.bytes_out += blks[i].len;
+                }
+            par_copy(cp, cl);
+        }
+        if (r.bounce) {
+            bounce_put(c, r.bounce, r.bcap);
+            held -= r.bcap;
+            r.bounce = nullptr;
+        }
+        if (r.rc && !rc) rc = r.rc;
+    };
     for (size_t g = 0; g < groups.size() && !rc; g++) {
-        std::lock_guard<std::mutex> lk(c->mu);
-        PipeSlot &s = c->pipe[c->pipe_next];
-        c->pipe_next = (c->pipe_next + 1) % kPipe;
-        std::lock_guard<std::mutex> sl(s.mu);
+        const int b0 = groups[g].first, b1 = groups[g].second;
+        PipeGroup &r = recs[g];
+        // (1) bounce the group's pageable blocks: one region per block, used
+        // by its input (copied in here) and / or its output (copied out by
+        // finish); in place when src == dst
+        size_t need = 0;
+        std::vector<size_t> boff(b1 - b0, SIZE_MAX);
+        std::vector<char> in_pg(b1 - b0, 0);
+        for (int i = b0; i < b1; i++) {
+            const jfsx_blk &b = blks[i];
+            if (!b.len) continue;
+            in_pg[i - b0] = !host_pinned(b.src, b.len);
+            out_b[i] = op != kPipeCrc && (b.dst == b.src ? in_pg[i - b0] : !host_pinned(b.dst, b.len));
+            if (!in_pg[i - b0] && !out_b[i]) continue;
+            boff[i - b0] = need;
+            need += align256(b.len);
+        }
+        if (need) {
+            if (!(r.bounce = bounce_get(c, need, &r.bcap))) {
+                rc = JFSX_ENOMEM;
+                break;
+            }
+            held += r.bcap;
+            cp.clear();
+            cl.clear();
+            for (int i = b0; i < b1; i++) {
+                if (boff[i - b0] == SIZE_MAX) continue;
+                char *q = r.bounce + boff[i - b0];
+                if (in_pg[i - b0]) {
+                    cp.push_back({q, (const char *)blks[i].src});
+                    cl.push_back(blks[i].len);
+                    hv[i].src = q;
+                    c->bounce.bytes_in += blks[i].len;
+                }
+                if (out_b[i]) hv[i].dst = q;
+            }
+            par_copy(cp, cl);
+        }
+        // (2) a slot, (3) the enqueue
         const SClock::time_point t0 = SClock::now();
+        PipeSlot &s = *claim_slot(c);
         pipe_collect(c, s);
         const SClock::time_point t1 = SClock::now();
-        const int b0 = groups[g].first, b1 = groups[g].second;
-        rc = pipe_enqueue(c, s, algo, open, b1 - b0, blks + b0, dv.data() + b0, crc_mode);
+        {
+            std::lock_guard<std::mutex> lk(c->mu);
+            rc = pipe_enqueue(c, s, op, algo, b1 - b0, hv.data() + b0, dv.data() + b0, crc_mode);
+            if (rc) {
+                (void)hipStreamSynchronize(c->s_in);
+                (void)hipStreamSynchronize(c->stream);
+                (void)hipStreamSynchronize(c->s_out);
+                s.w.n = 0;
+                s.w.nt = 0;
+                s.w.timed = false;
+                s.w.crc_back = false;
+            }
+        }
         c->ps_slot_us += us(t0, t1);
         c->ps_enq_us += us(t1, SClock::now());
         c->ps_groups++;
-        c->ps_blocks += (uint64_t)(groups[g].second - groups[g].first);
+        c->ps_blocks += (uint64_t)(b1 - b0);
         if (rc) {
-            (void)hipStreamSynchronize(c->s_in);
-            (void)hipStreamSynchronize(c->stream);
-            (void)hipStreamSynchronize(c->s_out);
-            s.w.n = 0;
-            s.w.nt = 0;
-            s.w.timed = false;
+            s.mu.unlock();
+            if (r.bounce) {
+                bounce_put(c, r.bounce, r.bcap);
+                held -= r.bcap;
+                r.bounce = nullptr;
+            }
             break;
         }
-        recs[g].slot = &s;
-        recs[g].dv = dv.data() + b0;
-        recs[g].open = open;
-        s.owner = &recs[g];
+        r.slot = &s;
+        r.dv = dv.data() + b0;
+        r.open = open;
+        s.owner = &r;
+        s.mu.unlock();
         issued++;
+        // a call holding bounce buffers keeps at most 4 groups / 1 GiB of them
+        // in flight
+        while (held && (issued - done > 4 || held > ((size_t)1 << 30))) finish(done++);
     }
     const SClock::time_point tw = SClock::now();
-    for (size_t g = 0; g < issued; g++) {
-        PipeSlot &s = *recs[g].slot;
-        std::lock_guard<std::mutex> sl(s.mu);
-        if (s.owner == &recs[g]) pipe_collect(c, s);
-        if (recs[g].rc && !rc) rc = recs[g].rc;
-    }
+    while (done < issued) finish(done++);
     c->ps_own_us += us(tw, SClock::now());
     if (rc) return rc;
     for (int i = 0; i < n; i++) {
@@ -903,107 +1303,71 @@ int run_aead_host(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int c
         blks[i].crc_bad_seg = dv[i].crc_bad_seg;
         blks[i].crc_got = dv[i].crc_got;
         blks[i].crc_expect = dv[i].crc_expect;
-        if (!open) memcpy(blks[i].tag, dv[i].tag, 16);
+        if (op != kPipeOpen && op != kPipeCrc) memcpy(blks[i].tag, dv[i].tag, 16);
     }
     return open ? wipe_failed(c->stream, n, blks, crc_mode, false) : 0;
 }
 
-int run_crc(jfsx_ctx *c, int n, jfsx_range *r, int mode) {
+int run_aead_host(jfsx_ctx *c, int algo, bool open, int n, jfsx_blk *blks, int crc_mode) {
+    int rc = check_aead_args(algo, n, blks, crc_mode, false);
+    if (rc || n == 0) return rc;
+    return run_host(c, open ? kPipeOpen : kPipeSeal, algo, n, blks, crc_mode);
+}
+
+int check_crc_args(int n, const jfsx_range *r, int mode, bool device) {
     if (n < 0 || (mode != JFSX_CRC_GEN && mode != JFSX_CRC_VERIFY)) return JFSX_EINVAL;
-    if (n == 0) return 0;
-    uint64_t calc_words = 0;
-    std::vector<Task> tasks;
-    // one 16-wave workgroup per task (jfsx_crc.hip): up to kCrcTaskBytes, but
-    // small enough that a small batch still spreads over every CU (~2 tasks
-    // per CU), and a whole number of 16-segment rounds
-    uint64_t total = 0;
-    for (int i = 0; i < n; i++) total += r[i].len;
-    const uint64_t round = 16 * (uint64_t)kSeg;
-    const uint64_t per = std::min<uint64_t>(kCrcTaskBytes, std::max<uint64_t>(round, (total / 512 + round - 1) / round * round));
     for (int i = 0; i < n; i++) {
-        if (r[i].len && (!r[i].data || !aligned16(r[i].data))) return JFSX_EINVAL;
+        if (r[i].len && (!r[i].data || (device && !aligned16(r[i].data)))) return JFSX_EINVAL;
         if (!r[i].crc) return JFSX_EINVAL;
-        for (uint64_t c0 = 0; c0 < r[i].len; c0 += per) tasks.push_back(Task{(uint32_t)i, 0, c0, std::min(c0 + per, r[i].len)});
-        if (mode == JFSX_CRC_VERIFY) calc_words += nseg_of(r[i].len);
-    }
-    const size_t nt = tasks.size();
-    size_t off = 0;
-    const size_t o_blk = off; off = align256(off + sizeof(BlkDev) * n);
-    const size_t o_task = off; off = align256(off + sizeof(Task) * std::max<size_t>(nt, 1));
-    const size_t h_bytes = off;
-    const size_t o_out = off; off = align256(off + sizeof(BlkOut) * n);
-    const size_t o_calc = off; off = align256(off + 4 * std::max<uint64_t>(calc_words, 1));
-    int rc;
-    Workspace &w = c->ws[0];
-    if ((rc = ensure_dev(c, &w.d, &w.dcap, off))) return rc;
-    if ((rc = ensure_host(&w.h, &w.hcap, std::max(h_bytes, sizeof(BlkOut) * n)))) return rc;
-    char *h = w.h, *d = w.d;
-    BlkDev *hb = (BlkDev *)(h + o_blk);
-    uint64_t calc = 0;
-    for (int i = 0; i < n; i++) {
-        memset(&hb[i], 0, sizeof(BlkDev));
-        hb[i].src = (const uint8_t *)r[i].data;
-        hb[i].len = r[i].len;
-        hb[i].crc = r[i].crc;
-        if (mode == JFSX_CRC_VERIFY) {
-            hb[i].crc_calc = (uint32_t *)(d + o_calc) + calc;
-            calc += nseg_of(r[i].len);
-        }
-    }
-    if (nt) memcpy(h + o_task, tasks.data(), sizeof(Task) * nt);
-    hipStream_t s = c->stream;
-    HIP_OK(hipMemcpyAsync(d, h, h_bytes, hipMemcpyHostToDevice, s));
-    if (c->timing) HIP_OK(hipEventRecord(c->ev_k0[0], s));
-    launch_begin();
-    launch_crc_segments(s, (int)nt, (const Task *)(d + o_task), (const BlkDev *)(d + o_blk), c->tabs);
-    if (c->timing) HIP_OK(hipEventRecord(c->ev_k1[0], s));
-    launch_crc_finalize(s, n, mode, (const BlkDev *)(d + o_blk), (BlkOut *)(d + o_out));
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipMemcpyAsync(h, d + o_out, sizeof(BlkOut) * n, hipMemcpyDeviceToHost, s));
-    HIP_OK(hipStreamSynchronize(s));
-    if (c->timing && nt) {
-        float ms = 0;
-        HIP_OK(hipEventElapsedTime(&ms, c->ev_k0[0], c->ev_k1[0]));
-        add_kernel_ms(c, ms);
-    }
-    const BlkOut *ho = (const BlkOut *)h;
-    for (int i = 0; i < n; i++) {
-        r[i].status = ho[i].status;
-        r[i].bad_seg = ho[i].bad_seg;
-        r[i].got = ho[i].got;
-        r[i].expect = ho[i].expect;
     }
     return 0;
 }
 
+// ranges as the block records the pipeline and enqueue_crc take
+std::vector<jfsx_blk> ranges_as_blocks(int n, const jfsx_range *r) {
+    std::vector<jfsx_blk> b(n);
+    for (int i = 0; i < n; i++) {
+        memset(&b[i], 0, sizeof(jfsx_blk));
+        b[i].src = r[i].data;
+        b[i].len = r[i].len;
+        b[i].crc = r[i].crc;
+    }
+    return b;
+}
+
+void blocks_to_ranges(int n, const jfsx_blk *b, jfsx_range *r) {
+    for (int i = 0; i < n; i++) {
+        r[i].status = b[i].status;
+        r[i].bad_seg = b[i].crc_bad_seg;
+        r[i].got = b[i].crc_got;
+        r[i].expect = b[i].crc_expect;
+    }
+}
+
+// Device-memory CRC batch: one enqueue, one sync (under c->mu).
+int run_crc(jfsx_ctx *c, int n, jfsx_range *r, int mode) {
+    int rc = check_crc_args(n, r, mode, true);
+    if (rc || n == 0) return rc;
+    std::vector<jfsx_blk> b = ranges_as_blocks(n, r);
+    if ((rc = enqueue_crc(c, c->ws[0], c->stream, c->ev_k0[0], c->ev_k1[0], n, b.data(), mode))) {
+        (void)hipStreamSynchronize(c->stream);
+        c->ws[0].timed = false;
+        return rc;
+    }
+    HIP_OK(hipStreamSynchronize(c->stream));
+    if ((rc = finish_aead(c, c->ws[0], c->ev_k0[0], c->ev_k1[0], true, b.data()))) return rc;
+    blocks_to_ranges(n, b.data(), r);
+    return 0;
+}
+
+// Host-memory CRC call: through the host pipeline, like a host AEAD call (no
+// context lock held while it waits; pageable ranges bounced by the caller).
 int run_crc_host(jfsx_ctx *c, int n, jfsx_range *r, int mode) {
-    size_t need = 0;
-    for (int i = 0; i < n; i++) need += align256(r[i].len) + align256(4 * nseg_of(r[i].len));
-    int rc;
-    Workspace &w = c->ws[0];
-    if ((rc = ensure_dev(c, &w.stage, &w.scap, std::max<size_t>(need, 256)))) return rc;
-    std::vector<jfsx_range> dv(r, r + n);
-    size_t off = 0;
-    hipStream_t s = c->stream;
-    for (int i = 0; i < n; i++) {
-        char *buf = w.stage + off;
-        off += align256(r[i].len);
-        char *cb = w.stage + off;
-        off += align256(4 * nseg_of(r[i].len));
-        if (r[i].len) HIP_OK(hipMemcpyAsync(buf, r[i].data, r[i].len, hipMemcpyHostToDevice, s));
-        if (mode == JFSX_CRC_VERIFY) HIP_OK(hipMemcpyAsync(cb, r[i].crc, 4 * nseg_of(r[i].len), hipMemcpyHostToDevice, s));
-        dv[i].data = buf;
-        dv[i].crc = (uint8_t *)cb;
-    }
-    if ((rc = run_crc(c, n, dv.data(), mode))) return rc;
-    for (int i = 0; i < n; i++) {
-        r[i].status = dv[i].status;
-        r[i].bad_seg = dv[i].bad_seg;
-        r[i].got = dv[i].got;
-        r[i].expect = dv[i].expect;
-        if (mode == JFSX_CRC_GEN) HIP_OK(hipMemcpyAsync(r[i].crc, dv[i].crc, 4 * nseg_of(r[i].len), hipMemcpyDeviceToHost, s));
-    }
-    HIP_OK(hipStreamSynchronize(s));
+    int rc = check_crc_args(n, r, mode, false);
+    if (rc || n == 0) return rc;
+    std::vector<jfsx_blk> b = ranges_as_blocks(n, r);
+    if ((rc = run_host(c, kPipeCrc, 0, n, b.data(), mode))) return rc;
+    blocks_to_ranges(n, b.data(), r);
     return 0;
 }
 
@@ -1207,6 +1571,7 @@ int jfsx_ctx_open(int device, uint32_t flags, jfsx_ctx **out) {
     jfsx_ctx *c = new jfsx_ctx();
     c->device = device;
     c->bitslice = (flags & JFSX_CTX_BITSLICE) != 0;
+    (void)jfsx_device_numa_node(device, &c->numa_node);
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
         c->ncu = ncu;
@@ -1279,7 +1644,8 @@ int jfsx_ctx_close(jfsx_ctx *c) {
     if (c->d_tab) (void)hipFree(c->d_tab);
     if (c->rsa_d) (void)hipFree(c->rsa_d);
     if (c->rsa_h) (void)hipHostFree(c->rsa_h);
-    if (c->arena) (void)hipHostFree(c->arena);
+    for (auto &kv : c->bounce.idle) (void)hipHostFree(kv.second);
+    c->bounce.idle.clear();
     for (int k = 0; k < kRing; k++) {
         Workspace &w = c->ws[k];
         if (w.d) (void)hipFree(w.d);
@@ -1429,6 +1795,7 @@ int jfsx_alloc_pinned(jfsx_ctx *c, size_t bytes, void **p) {
     // portable: the multi-device context's other GPUs DMA from it as well
     const hipError_t e = hipHostMalloc(p, bytes, hipHostMallocPortable);
     if (e == hipSuccess) {
+        note_pinned(*p, bytes);
         return 0;
     }
     note_hip_error(e, __FILE__, __LINE__, "hipHostMalloc(pinned)");
@@ -1464,29 +1831,36 @@ constexpr int kMpolDefault = 0, kMpolBind = 2, kMpolFNode = 1, kMpolFAddr = 2;
 constexpr unsigned long kMaxNodes = 1024;
 }  // namespace
 
-int jfsx_alloc_pinned_node(jfsx_ctx *c, size_t bytes, int node, void **p) {
-    if (!c || !p || node < -1 || node >= (int)kMaxNodes) return JFSX_EINVAL;
-    CtxScope es_(c);
-    HIP_OK(hipSetDevice(c->device));
-    if (node < 0 && jfsx_device_numa_node(c->device, &node)) node = -1;
-    // Bind this thread's allocations to the node while the runtime allocates
-    // and pins the pages (hipHostMallocNumaUser: they follow the caller's
-    // policy), then restore the thread's own policy.  Where the node cannot be
-    // bound (a cpuset without it), the default placement is used.
+namespace {
+// pinned portable host memory whose pages are bound to `node` (-1: default
+// placement).  Binds this thread's allocations to the node while the runtime
+// allocates and pins the pages (hipHostMallocNumaUser: they follow the
+// caller's policy), then restores the thread's own policy.  Where the node
+// cannot be bound (a cpuset without it), the default placement is used.
+int alloc_pinned_on(int node, size_t bytes, void **p) {
     unsigned long old_mask[kMaxNodes / 64] = {0}, mask[kMaxNodes / 64] = {0};
     int old_mode = kMpolDefault;
     bool bound = false;
-    if (node >= 0 && syscall(SYS_get_mempolicy, &old_mode, old_mask, kMaxNodes, nullptr, 0) == 0) {
+    if (node >= 0 && node < (int)kMaxNodes && syscall(SYS_get_mempolicy, &old_mode, old_mask, kMaxNodes, nullptr, 0) == 0) {
         mask[node / 64] = 1ul << (node % 64);
         bound = syscall(SYS_set_mempolicy, kMpolBind, mask, kMaxNodes) == 0;
     }
     const hipError_t e = hipHostMalloc(p, bytes, hipHostMallocPortable | (bound ? hipHostMallocNumaUser : 0));
     if (bound) (void)syscall(SYS_set_mempolicy, old_mode, old_mode == kMpolDefault ? nullptr : old_mask, kMaxNodes);
-    if (e == hipSuccess) {
-        return 0;
-    }
+    if (e == hipSuccess) return 0;
     note_hip_error(e, __FILE__, __LINE__, "hipHostMalloc(pinned, NUMA node)");
     return JFSX_ENOMEM;
+}
+}  // namespace
+
+int jfsx_alloc_pinned_node(jfsx_ctx *c, size_t bytes, int node, void **p) {
+    if (!c || !p || node < -1 || node >= (int)kMaxNodes) return JFSX_EINVAL;
+    CtxScope es_(c);
+    HIP_OK(hipSetDevice(c->device));
+    if (node < 0 && jfsx_device_numa_node(c->device, &node)) node = -1;
+    const int rc = alloc_pinned_on(node, bytes, p);
+    if (rc == 0) note_pinned(*p, bytes);
+    return rc;
 }
 
 int jfsx_host_numa_node(const void *p, size_t bytes, int *node) {
@@ -1508,6 +1882,7 @@ int jfsx_host_numa_node(const void *p, size_t bytes, int *node) {
 
 int jfsx_free_pinned(jfsx_ctx *c, void *p) {
     if (!c) return JFSX_EINVAL;
+    forget_pinned(p);
     HIP_OK(hipHostFree(p));
     return 0;
 }
@@ -1576,10 +1951,16 @@ int jfsx_open_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *blks, int crc_mode, 
 
 int jfsx_crc32c_segments(jfsx_ctx *c, int n, jfsx_range *ranges, int mode, int mem) {
     if (!c || (n > 0 && !ranges)) return JFSX_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    if (mem != JFSX_MEM_HOST && mem != JFSX_MEM_DEVICE) return JFSX_EINVAL;
     CtxScope es_(c);
     HIP_OK(hipSetDevice(c->device));
-    const int rc = mem == JFSX_MEM_HOST ? run_crc_host(c, n, ranges, mode) : run_crc(c, n, ranges, mode);
+    int rc;
+    if (mem == JFSX_MEM_HOST) {
+        rc = run_crc_host(c, n, ranges, mode);  // the host pipeline locks per group
+    } else {
+        std::lock_guard<std::mutex> g(c->mu);
+        rc = run_crc(c, n, ranges, mode);
+    }
     if (rc == 0) tally_crc(c, n, ranges);
     return rc;
 }
@@ -1713,20 +2094,14 @@ int jfsx_cache_verify(jfsx_ctx *c, const void *file, uint64_t file_size, uint64_
             if (eof2) {
                 rc = JFSX_EOF;
             } else if (clen) {
-                // stage the window in the context's pinned arena (grow-only):
-                // the H2D then runs as one DMA, with no per-call pinning
-                std::lock_guard<std::mutex> ga(c->arena_mu);
+                // the window goes to the host pipeline as it is: a pageable
+                // window (the caller's buffer, or the widened read of the
+                // extend level) is bounced by this thread, a pinned one
+                // streams directly; concurrent readers share the pipeline
                 int e;
-                {
-                    std::lock_guard<std::mutex> g(c->mu);
-    CtxScope es_(c);
-                    HIP_OK(hipSetDevice(c->device));
-                    if ((e = ensure_host(&c->arena, &c->arena_cap, clen))) return e;
-                }
-                memcpy(c->arena, rb + cstart, clen);
                 jfsx_range r;
                 memset(&r, 0, sizeof(r));
-                r.data = c->arena;
+                r.data = rb + cstart;
                 r.len = clen;
                 r.crc = ebuf.data();
                 e = jfsx_crc32c_segments(c, 1, &r, JFSX_CRC_VERIFY, JFSX_MEM_HOST);
@@ -1829,7 +2204,7 @@ using AeadFn = std::function<int(jfsx_blk *, int crc_mode)>;
 
 int data_encrypt(const AeadFn &seal, int algo, const uint8_t key[32], const uint8_t nonce[12], const uint8_t *wrapped,
                  int wlen, const void *plaintext, uint64_t len, void *out, uint64_t out_cap, uint64_t *out_len,
-                 uint32_t *obj_crc) {
+                 uint32_t *obj_crc, uint8_t *seg_crc) {
     // encrypt.go:182-193: [BE16 klen][nlen][wrapped key][nonce][Seal(plaintext)]
     if (!key || !nonce || wlen < 0 || wlen > 65535 || (wlen && !wrapped) || !out) return JFSX_EINVAL;
     if (algo != JFSX_AES256GCM && algo != JFSX_CHACHA20P1305) return JFSX_EINVAL;
@@ -1848,23 +2223,41 @@ int data_encrypt(const AeadFn &seal, int algo, const uint8_t key[32], const uint
     b.src = plaintext;
     b.dst = o + hdr;
     b.len = len;
+    // the checksums the call asks for, in one pass: checksum() of the
+    // plaintext (seg_crc, straight into the caller's array), the ciphertext
+    // segment CRCs the object checksum is folded from (obj_crc), or both
+    const uint64_t ns = nseg_of(len);
     std::vector<uint8_t> segs;
-    if (obj_crc) {
-        segs.resize(4 * nseg_of(len));
+    int mode = JFSX_CRC_NONE;
+    if (obj_crc && seg_crc) {
+        segs.resize(8 * ns);
         b.crc = segs.data();
+        mode = JFSX_CRC_GEN | JFSX_CRC_BOTH;
+    } else if (obj_crc) {
+        segs.resize(4 * ns);
+        b.crc = segs.data();
+        mode = JFSX_CRC_GEN | JFSX_CRC_CT;
+    } else if (seg_crc) {
+        b.crc = seg_crc;
+        mode = JFSX_CRC_GEN;
     }
-    int rc = seal(&b, obj_crc ? JFSX_CRC_GEN | JFSX_CRC_CT : JFSX_CRC_NONE);
+    int rc = seal(&b, mode);
     if (rc) return rc;
     memcpy(o + hdr + len, b.tag, 16);
-    if (obj_crc && (rc = jfsx_object_crc32c(o, hdr, segs.data(), len, b.tag, obj_crc))) return rc;
+    const uint8_t *ct_segs = obj_crc && seg_crc ? segs.data() + 4 * ns : segs.data();
+    if (obj_crc && seg_crc) memcpy(seg_crc, segs.data(), 4 * ns);
+    if (obj_crc && (rc = jfsx_object_crc32c(o, hdr, ct_segs, len, b.tag, obj_crc))) return rc;
     if (out_len) *out_len = hdr + len + 16;
     return 0;
 }
 
 int data_decrypt(const AeadFn &open, const uint8_t key[32], const void *obj, uint64_t olen, void *out,
-                 uint64_t out_cap, uint64_t *out_len, const uint32_t *expect_crc, uint32_t *got_crc) {
+                 uint64_t out_cap, uint64_t *out_len, const uint32_t *expect_crc, uint32_t *got_crc,
+                 uint8_t *seg_crc) {
     // encrypt.go:196-216; with expect_crc, the object checksum the store kept
-    // (checksum.go:55-82) is verified in the same pass over C
+    // (checksum.go:55-82) is verified in the same pass over C; with seg_crc,
+    // checksum() of the plaintext for the cache file the load path writes next
+    // (cached_store.go:745 -> disk_cache.go:469) comes out of the same pass
     if (!key || !obj || !out) return JFSX_EINVAL;
     int kl = 0, nl = 0;
     int rc = jfsx_parse_header(obj, olen, &kl, &nl);
@@ -1884,20 +2277,33 @@ int data_decrypt(const AeadFn &open, const uint8_t key[32], const void *obj, uin
     b.dst = out;
     b.len = len;
     memcpy(b.tag, o + hdr + len, 16);
+    const uint64_t ns = nseg_of(len);
     std::vector<uint8_t> segs;
-    if (expect_crc) {
-        segs.resize(4 * nseg_of(len));
+    int mode = JFSX_CRC_NONE;
+    if (expect_crc && seg_crc) {
+        segs.resize(8 * ns);
         b.crc = segs.data();
+        mode = JFSX_CRC_GEN | JFSX_CRC_BOTH;
+    } else if (expect_crc) {
+        segs.resize(4 * ns);
+        b.crc = segs.data();
+        mode = JFSX_CRC_GEN | JFSX_CRC_CT;
+    } else if (seg_crc) {
+        b.crc = seg_crc;
+        mode = JFSX_CRC_GEN;
     }
-    rc = open(&b, expect_crc ? JFSX_CRC_GEN | JFSX_CRC_CT : JFSX_CRC_NONE);
+    rc = open(&b, mode);
     if (rc) return rc;
     if (expect_crc) {
         // the store's read fails first ("verify checksum failed"), before Decrypt sees the bytes
-        if ((rc = jfsx_object_crc32c(o, hdr, segs.data(), len, o + hdr + len, got_crc))) return rc;
+        const uint8_t *ct_segs = seg_crc ? segs.data() + 4 * ns : segs.data();
+        if ((rc = jfsx_object_crc32c(o, hdr, ct_segs, len, o + hdr + len, got_crc))) return rc;
         if (*got_crc != *expect_crc) {
             if (len) memset(out, 0, len);
+            if (seg_crc) memset(seg_crc, 0, 4 * ns);
             return JFSX_ECRC;
         }
+        if (seg_crc) memcpy(seg_crc, segs.data(), 4 * ns);  // zeros when the tag failed
     }
     if (b.status == JFSX_ETAG) return JFSX_ETAG;
     if (out_len) *out_len = len;
@@ -1907,34 +2313,60 @@ int data_decrypt(const AeadFn &open, const uint8_t key[32], const void *obj, uin
 
 extern "C" {
 
+int jfsx_data_encrypt_ex(jfsx_ctx *c, int algo, const uint8_t key[32], const uint8_t nonce[12], const uint8_t *wrapped,
+                         int wlen, const void *plaintext, uint64_t len, void *out, uint64_t out_cap, uint64_t *out_len,
+                         uint32_t *obj_crc, uint8_t *seg_crc) {
+    if (!c) return JFSX_EINVAL;
+    return data_encrypt([&](jfsx_blk *b, int m) { return jfsx_seal_batch(c, algo, 1, b, m, JFSX_MEM_HOST); }, algo,
+                        key, nonce, wrapped, wlen, plaintext, len, out, out_cap, out_len, obj_crc, seg_crc);
+}
+
+int jfsx_data_decrypt_ex(jfsx_ctx *c, int algo, const uint8_t key[32], const void *obj, uint64_t olen, void *out,
+                         uint64_t out_cap, uint64_t *out_len, const uint32_t *expect_crc, uint32_t *got_crc,
+                         uint8_t *seg_crc) {
+    if (!c || (algo != JFSX_AES256GCM && algo != JFSX_CHACHA20P1305)) return JFSX_EINVAL;
+    return data_decrypt([&](jfsx_blk *b, int m) { return jfsx_open_batch(c, algo, 1, b, m, JFSX_MEM_HOST); }, key,
+                        obj, olen, out, out_cap, out_len, expect_crc, got_crc, seg_crc);
+}
+
 int jfsx_data_encrypt(jfsx_ctx *c, int algo, const uint8_t key[32], const uint8_t nonce[12], const uint8_t *wrapped,
                       int wlen, const void *plaintext, uint64_t len, void *out, uint64_t out_cap, uint64_t *out_len,
                       uint32_t *obj_crc) {
-    if (!c) return JFSX_EINVAL;
-    return data_encrypt([&](jfsx_blk *b, int m) { return jfsx_seal_batch(c, algo, 1, b, m, JFSX_MEM_HOST); }, algo,
-                        key, nonce, wrapped, wlen, plaintext, len, out, out_cap, out_len, obj_crc);
+    return jfsx_data_encrypt_ex(c, algo, key, nonce, wrapped, wlen, plaintext, len, out, out_cap, out_len, obj_crc,
+                                nullptr);
 }
 
 int jfsx_data_decrypt(jfsx_ctx *c, int algo, const uint8_t key[32], const void *obj, uint64_t olen, void *out,
                       uint64_t out_cap, uint64_t *out_len, const uint32_t *expect_crc, uint32_t *got_crc) {
-    if (!c || (algo != JFSX_AES256GCM && algo != JFSX_CHACHA20P1305)) return JFSX_EINVAL;
-    return data_decrypt([&](jfsx_blk *b, int m) { return jfsx_open_batch(c, algo, 1, b, m, JFSX_MEM_HOST); }, key,
-                        obj, olen, out, out_cap, out_len, expect_crc, got_crc);
+    return jfsx_data_decrypt_ex(c, algo, key, obj, olen, out, out_cap, out_len, expect_crc, got_crc, nullptr);
+}
+
+int jfsx_agg_data_encrypt_ex(jfsx_agg *a, int algo, const uint8_t key[32], const uint8_t nonce[12],
+                             const uint8_t *wrapped, int wlen, const void *plaintext, uint64_t len, void *out,
+                             uint64_t out_cap, uint64_t *out_len, uint32_t *obj_crc, uint8_t *seg_crc) {
+    if (!a) return JFSX_EINVAL;
+    return data_encrypt([&](jfsx_blk *b, int m) { return jfsx_agg_seal(a, algo, b, m, JFSX_MEM_HOST); }, algo, key,
+                        nonce, wrapped, wlen, plaintext, len, out, out_cap, out_len, obj_crc, seg_crc);
+}
+
+int jfsx_agg_data_decrypt_ex(jfsx_agg *a, int algo, const uint8_t key[32], const void *obj, uint64_t olen, void *out,
+                             uint64_t out_cap, uint64_t *out_len, const uint32_t *expect_crc, uint32_t *got_crc,
+                             uint8_t *seg_crc) {
+    if (!a || (algo != JFSX_AES256GCM && algo != JFSX_CHACHA20P1305)) return JFSX_EINVAL;
+    return data_decrypt([&](jfsx_blk *b, int m) { return jfsx_agg_open(a, algo, b, m, JFSX_MEM_HOST); }, key, obj,
+                        olen, out, out_cap, out_len, expect_crc, got_crc, seg_crc);
 }
 
 int jfsx_agg_data_encrypt(jfsx_agg *a, int algo, const uint8_t key[32], const uint8_t nonce[12],
                           const uint8_t *wrapped, int wlen, const void *plaintext, uint64_t len, void *out,
                           uint64_t out_cap, uint64_t *out_len, uint32_t *obj_crc) {
-    if (!a) return JFSX_EINVAL;
-    return data_encrypt([&](jfsx_blk *b, int m) { return jfsx_agg_seal(a, algo, b, m, JFSX_MEM_HOST); }, algo, key,
-                        nonce, wrapped, wlen, plaintext, len, out, out_cap, out_len, obj_crc);
+    return jfsx_agg_data_encrypt_ex(a, algo, key, nonce, wrapped, wlen, plaintext, len, out, out_cap, out_len,
+                                    obj_crc, nullptr);
 }
 
 int jfsx_agg_data_decrypt(jfsx_agg *a, int algo, const uint8_t key[32], const void *obj, uint64_t olen, void *out,
                           uint64_t out_cap, uint64_t *out_len, const uint32_t *expect_crc, uint32_t *got_crc) {
-    if (!a || (algo != JFSX_AES256GCM && algo != JFSX_CHACHA20P1305)) return JFSX_EINVAL;
-    return data_decrypt([&](jfsx_blk *b, int m) { return jfsx_agg_open(a, algo, b, m, JFSX_MEM_HOST); }, key, obj,
-                        olen, out, out_cap, out_len, expect_crc, got_crc);
+    return jfsx_agg_data_decrypt_ex(a, algo, key, obj, olen, out, out_cap, out_len, expect_crc, got_crc, nullptr);
 }
 
 int jfsx_gen_synthetic(jfsx_ctx *c, void *dst, uint64_t len, uint64_t seed, uint64_t block) {

@@ -17,6 +17,7 @@ AES256GCM = 0
 CHACHA20P1305 = 1
 CRC_NONE, CRC_GEN, CRC_VERIFY = 0, 1, 2
 CRC_CT = 4  # flag: segment CRCs over the ciphertext (object checksum)
+CRC_BOTH = 8  # flag (with CRC_GEN): plaintext CRCs, then ciphertext CRCs, in one array
 CTX_BITSLICE = 1  # context flag: AES-GCM keystream from the bitsliced AES (VALU)
 MEM_DEVICE, MEM_HOST = 0, 1
 OK, ETAG, ECRC = 0, 1, 2
@@ -46,6 +47,7 @@ EXPORTS = [
     "jfsx_mctx_zstd_compress_batch", "jfsx_ctx_metrics", "jfsx_pcie_probe",
     "jfsx_device_numa_node", "jfsx_alloc_pinned_node", "jfsx_host_numa_node",
     "jfsx_agg_data_encrypt", "jfsx_agg_data_decrypt",
+    "jfsx_data_encrypt_ex", "jfsx_data_decrypt_ex", "jfsx_agg_data_encrypt_ex", "jfsx_agg_data_decrypt_ex",
 ]
 
 
@@ -148,6 +150,10 @@ def load_library(path=LIB_PATH):
             "jfsx_host_numa_node": (I, [P, SZ, ctypes.POINTER(I)]),
             "jfsx_agg_data_encrypt": (I, [P, I, P, P, P, I, P, U64, P, U64, ctypes.POINTER(U64), P]),
             "jfsx_agg_data_decrypt": (I, [P, I, P, P, U64, P, U64, ctypes.POINTER(U64), P, P]),
+            "jfsx_data_encrypt_ex": (I, [P, I, P, P, P, I, P, U64, P, U64, ctypes.POINTER(U64), P, P]),
+            "jfsx_data_decrypt_ex": (I, [P, I, P, P, U64, P, U64, ctypes.POINTER(U64), P, P, P]),
+            "jfsx_agg_data_encrypt_ex": (I, [P, I, P, P, P, I, P, U64, P, U64, ctypes.POINTER(U64), P, P]),
+            "jfsx_agg_data_decrypt_ex": (I, [P, I, P, P, U64, P, U64, ctypes.POINTER(U64), P, P, P]),
             "jfsx_free_pinned": (I, [P, P]),
             "jfsx_alloc_device": (I, [P, SZ, PP]),
             "jfsx_free_device": (I, [P, P]),
@@ -230,6 +236,13 @@ def _u8(b):
     if isinstance(b, np.ndarray):
         return np.ascontiguousarray(b.reshape(-1).view(np.uint8))
     return np.frombuffer(bytes(b), dtype=np.uint8).copy()
+
+
+def _obj_plain_len(o):
+    """plaintext length an encrypted object's header implies (encrypt.go:197-215), 0 if malformed"""
+    if o.size < 3:
+        return 0
+    return max(0, int(o.size) - 3 - ((int(o[0]) << 8) | int(o[1])) - int(o[2]) - 16)
 
 
 def debug_tables():
@@ -576,37 +589,46 @@ class Engine:
             raise EngineError(rc, "jfsx_cache_verify")
         return rc, out[:size].tobytes(), n.value, got.value, exp.value, seg.value
 
-    def data_encrypt(self, algo, key, nonce, wrapped, plaintext, obj_crc=False):
+    def data_encrypt(self, algo, key, nonce, wrapped, plaintext, obj_crc=False, seg_crc=False):
         """Object bytes (encrypt.go:182-193); with obj_crc=True also the
-        object-store checksum of them (checksum.go:31-53): (obj, crc)."""
+        object-store checksum of them (checksum.go:31-53); with seg_crc=True
+        also checksum() of the plaintext (disk_cache.go:1218-1231), from the
+        same call: obj, or a tuple (obj[, crc][, seg_crcs])."""
         p = _u8(plaintext)
         cap = 3 + len(wrapped) + 12 + p.size + 16
         out = np.empty(cap, np.uint8)
         w = _u8(wrapped)
         olen = ctypes.c_uint64()
         crc = ctypes.c_uint32()
-        self._check(self.L.jfsx_data_encrypt(self.ctx, algo, bytes(key), bytes(nonce),
-                                             w.ctypes.data if w.size else None, w.size,
-                                             p.ctypes.data if p.size else None, p.size, out.ctypes.data, cap,
-                                             ctypes.byref(olen), ctypes.byref(crc) if obj_crc else None),
-                    "jfsx_data_encrypt")
+        segs = np.zeros(4 * max(1, -(-p.size // SEG)), np.uint8)
+        self._check(self.L.jfsx_data_encrypt_ex(self.ctx, algo, bytes(key), bytes(nonce),
+                                                w.ctypes.data if w.size else None, w.size,
+                                                p.ctypes.data if p.size else None, p.size, out.ctypes.data, cap,
+                                                ctypes.byref(olen), ctypes.byref(crc) if obj_crc else None,
+                                                segs.ctypes.data if seg_crc else None),
+                    "jfsx_data_encrypt_ex")
         obj = out[:olen.value].tobytes()
-        return (obj, crc.value) if obj_crc else obj
+        res = (obj,) + ((crc.value,) if obj_crc else ()) + ((segs.tobytes(),) if seg_crc else ())
+        return res if len(res) > 1 else obj
 
-    def data_decrypt(self, algo, key, obj, expect_crc=None):
+    def data_decrypt(self, algo, key, obj, expect_crc=None, seg_crc=False):
         """(rc, plaintext) -- rc JFSX_ECRC when expect_crc is given and the
-        object checksum differs; then .last_got_crc holds the computed value."""
+        object checksum differs; then .last_got_crc holds the computed value.
+        With seg_crc=True, (rc, plaintext, checksum() of the plaintext)."""
         o = _u8(obj)
         out = np.empty(max(o.size, 1), np.uint8)
         olen = ctypes.c_uint64()
         exp = ctypes.c_uint32(expect_crc or 0)
         got = ctypes.c_uint32()
-        rc = self.L.jfsx_data_decrypt(self.ctx, algo, bytes(key), o.ctypes.data, o.size, out.ctypes.data,
-                                      out.size, ctypes.byref(olen),
-                                      ctypes.byref(exp) if expect_crc is not None else None,
-                                      ctypes.byref(got) if expect_crc is not None else None)
+        segs = np.full(4 * max(1, -(-_obj_plain_len(o) // SEG)), 0xAA, np.uint8)
+        rc = self.L.jfsx_data_decrypt_ex(self.ctx, algo, bytes(key), o.ctypes.data, o.size, out.ctypes.data,
+                                         out.size, ctypes.byref(olen),
+                                         ctypes.byref(exp) if expect_crc is not None else None,
+                                         ctypes.byref(got) if expect_crc is not None else None,
+                                         segs.ctypes.data if seg_crc else None)
         self.last_got_crc = got.value
-        return rc, out[:olen.value].tobytes() if rc == 0 else b""
+        pt = out[:olen.value].tobytes() if rc == 0 else b""
+        return (rc, pt, segs.tobytes()) if seg_crc else (rc, pt)
 
     def rsa_key(self, p, q, dp, dq, qinv, label=b"keys"):
         """Device copy of an RSA-2048 private key from its CRT components
@@ -845,30 +867,38 @@ class Aggregator:
         """z: a jfsx_zblk, dst_cap >= zstd_bound(src_len)."""
         self.eng._check(self.L.jfsx_agg_zstd_compress(self.h, ctypes.byref(z), mem), "jfsx_agg_zstd_compress")
 
-    def data_encrypt(self, algo, key, nonce, wrapped, plaintext, obj_crc=False):
-        """dataEncryptor.Encrypt through the aggregator (jfsx_agg_data_encrypt):
-        the object bytes, and its object-store CRC32C when obj_crc."""
+    def data_encrypt(self, algo, key, nonce, wrapped, plaintext, obj_crc=False, seg_crc=False):
+        """dataEncryptor.Encrypt through the aggregator (jfsx_agg_data_encrypt_ex):
+        the object bytes, with its object-store CRC32C when obj_crc and
+        checksum() of the plaintext when seg_crc (a tuple then)."""
         p = _u8(plaintext)
         w = _u8(wrapped)
         out = np.empty(3 + w.size + 12 + p.size + 16, np.uint8)
         olen = ctypes.c_uint64()
         crc = ctypes.c_uint32()
-        self.eng._check(self.L.jfsx_agg_data_encrypt(self.h, algo, _u8(key).ctypes.data, _u8(nonce).ctypes.data,
-                                                     w.ctypes.data, w.size, p.ctypes.data, p.size, out.ctypes.data,
-                                                     out.size, ctypes.byref(olen),
-                                                     ctypes.byref(crc) if obj_crc else None),
-                        "jfsx_agg_data_encrypt")
-        return (out.tobytes(), crc.value) if obj_crc else out.tobytes()
+        segs = np.zeros(4 * max(1, -(-p.size // SEG)), np.uint8)
+        self.eng._check(self.L.jfsx_agg_data_encrypt_ex(self.h, algo, _u8(key).ctypes.data, _u8(nonce).ctypes.data,
+                                                        w.ctypes.data, w.size, p.ctypes.data, p.size, out.ctypes.data,
+                                                        out.size, ctypes.byref(olen),
+                                                        ctypes.byref(crc) if obj_crc else None,
+                                                        segs.ctypes.data if seg_crc else None),
+                        "jfsx_agg_data_encrypt_ex")
+        res = (out.tobytes(),) + ((crc.value,) if obj_crc else ()) + ((segs.tobytes(),) if seg_crc else ())
+        return res if len(res) > 1 else res[0]
 
-    def data_decrypt(self, algo, key, obj):
-        """dataEncryptor.Decrypt (after the key unwrap) through the aggregator."""
+    def data_decrypt(self, algo, key, obj, seg_crc=False):
+        """dataEncryptor.Decrypt (after the key unwrap) through the aggregator;
+        with seg_crc, (plaintext, checksum() of it)."""
         o = _u8(obj)
         out = np.empty(max(o.size, 1), np.uint8)
         n = ctypes.c_uint64()
-        self.eng._check(self.L.jfsx_agg_data_decrypt(self.h, algo, _u8(key).ctypes.data, o.ctypes.data, o.size,
-                                                     out.ctypes.data, out.size, ctypes.byref(n), None, None),
-                        "jfsx_agg_data_decrypt")
-        return out[:n.value].tobytes()
+        segs = np.zeros(4 * max(1, -(-_obj_plain_len(o) // SEG)), np.uint8)
+        self.eng._check(self.L.jfsx_agg_data_decrypt_ex(self.h, algo, _u8(key).ctypes.data, o.ctypes.data, o.size,
+                                                        out.ctypes.data, out.size, ctypes.byref(n), None, None,
+                                                        segs.ctypes.data if seg_crc else None),
+                        "jfsx_agg_data_decrypt_ex")
+        pt = out[:n.value].tobytes()
+        return (pt, segs.tobytes()) if seg_crc else pt
 
     def stats(self):
         """(calls, batches, blocks carried by those batches)"""

@@ -239,9 +239,24 @@ static int64_t file_pread(const uint8_t *file, int64_t fsize, uint8_t *dst, int6
  * bad_seg is the index (relative to the file's segment 0) of the first
  * failing segment.
  */
+static int cache_readat(const uint8_t *file, int64_t fsize, int64_t length, int level, int64_t off, int64_t size,
+                        uint8_t *out, int64_t *n_out, uint32_t *got, uint32_t *expect, int64_t *bad_seg, int hw);
+
 ORC_EXPORT int orc_cache_readat(const uint8_t *file, int64_t fsize, int64_t length, int level,
                                 int64_t off, int64_t size, uint8_t *out, int64_t *n_out,
                                 uint32_t *got, uint32_t *expect, int64_t *bad_seg) {
+    return cache_readat(file, fsize, length, level, off, size, out, n_out, got, expect, bad_seg, 0);
+}
+
+/* the same with the 3-stream SSE4.2 CRC (the CPU baseline's ReadAt) */
+ORC_EXPORT int orc_cache_readat_hw(const uint8_t *file, int64_t fsize, int64_t length, int level,
+                                   int64_t off, int64_t size, uint8_t *out, int64_t *n_out,
+                                   uint32_t *got, uint32_t *expect, int64_t *bad_seg) {
+    return cache_readat(file, fsize, length, level, off, size, out, n_out, got, expect, bad_seg, 1);
+}
+
+static int cache_readat(const uint8_t *file, int64_t fsize, int64_t length, int level, int64_t off, int64_t size,
+                        uint8_t *out, int64_t *n_out, uint32_t *got, uint32_t *expect, int64_t *bad_seg, int hw) {
     int eof = 0;
     *n_out = 0;
     if (level == CS_NONE || (level == CS_FULL && (off != 0 || size != length))) {
@@ -301,7 +316,8 @@ ORC_EXPORT int orc_cache_readat(const uint8_t *file, int64_t fsize, int64_t leng
         for (int64_t s = 0, e = 0; s < clen; s = e, k++) {
             e = s + CS_BLOCK;
             if (e > clen) e = clen;
-            uint32_t sum = orc_crc32c_update(0, rb + cstart + s, (uint64_t)(e - s));
+            uint32_t sum = hw ? orc_crc32c_update_hw3(0, rb + cstart + s, (uint64_t)(e - s))
+                              : orc_crc32c_update(0, rb + cstart + s, (uint64_t)(e - s));
             uint32_t ex = get_be32(ebuf + 4 * k);
             if (sum != ex) {
                 *got = sum;
@@ -1126,6 +1142,13 @@ ORC_EXPORT double orc_bench_seal_crc_evp(int algo, int nthreads, uint64_t nblock
 /*           the stored CRCs, as cacheFile.ReadAt's verify does         */
 /*           (encrypt.go:196-216 + disk_cache.go:1315-1327; configs[3])  */
 /*   mode 2  CRC verify only (cache hit, disk_cache.go:1255-1329)        */
+/*   mode 3  dataEncryptor.Encrypt + checksum(p): the object header (a   */
+/*           256-B wrapped key, the nonce) built in the output buffer,   */
+/*           EVP Seal into it at offset 271 (encrypt.go:182-193),        */
+/*           checksum() of the plaintext for the staged cache file       */
+/*   mode 4  dataEncryptor.Decrypt + checksum(p): header parsed, EVP     */
+/*           Open from offset 271 (encrypt.go:196-215), checksum() of    */
+/*           the plaintext for the cache file (cached_store.go:745)      */
 /* Block b has lens[b] bytes (lens NULL: blen each; configs[4] ragged).  */
 /* Inputs (and, for open, the sealed images) are made before the clock */
 /* starts.  Returns wall seconds, -1 without libcrypto (modes 0/1), -2  */
@@ -1176,6 +1199,8 @@ typedef struct {
 } base_job;
 
 static uint64_t base_len(const base_job *j, uint64_t b) { return j->lens ? j->lens[b] : j->maxlen; }
+/* bytes per block of the input array: the object (header, C, tag) for mode 4 */
+static uint64_t base_stride(const base_job *j) { return j->maxlen + (j->mode == 4 ? 287 : 0); }
 
 static void *base_worker(void *arg) {
     base_job *j = (base_job *)arg;
@@ -1186,7 +1211,7 @@ static void *base_worker(void *arg) {
         const uint64_t n = base_len(j, b), k = b - j->b0;
         uint8_t key[32], nonce[12], tag[16];
         orc_gen_key(j->seed, b, key, nonce);
-        uint8_t *in = j->in + k * j->maxlen;
+        uint8_t *in = j->in + k * base_stride(j);
         if (j->mode == 0) {
             orc_checksum(in, (int64_t)n, mycrc, 1);
             if (evp_seal(ctx, j->algo, key, nonce, in, n, j->work, tag)) j->bad = 1;
@@ -1196,8 +1221,25 @@ static void *base_worker(void *arg) {
             const int64_t cl = orc_checksum(j->work, (int64_t)n, mycrc, 1);
             if (memcmp(mycrc, j->crcs + k * j->crcstride, (size_t)cl)) j->bad = 1;
             dg ^= le32(mycrc);
-        } else {
+        } else if (j->mode == 2) {
             const int64_t cl = orc_checksum(in, (int64_t)n, mycrc, 1);
+            if (memcmp(mycrc, j->crcs + k * j->crcstride, (size_t)cl)) j->bad = 1;
+            dg ^= le32(mycrc);
+        } else if (j->mode == 3) {
+            uint8_t *o = j->work;
+            o[0] = 1;  /* BE16(256) */
+            o[1] = 0;
+            o[2] = 12;
+            memcpy(o + 3, j->tags, 256);  /* the wrapped key (any 256 bytes) */
+            memcpy(o + 259, nonce, 12);
+            if (evp_seal(ctx, j->algo, key, nonce, in, n, o + 271, o + 271 + n)) j->bad = 1;
+            orc_checksum(in, (int64_t)n, mycrc, 1);
+            dg ^= le32(o + 271 + n) ^ le32(mycrc);
+        } else {
+            const uint8_t *o = in;
+            const uint64_t kl = ((uint64_t)o[0] << 8) | o[1], hl = 3 + kl + o[2];
+            if (evp_open(ctx, j->algo, key, o + 3 + kl, o + hl, n, o + hl + n, j->work)) j->bad = 1;
+            const int64_t cl = orc_checksum(j->work, (int64_t)n, mycrc, 1);
             if (memcmp(mycrc, j->crcs + k * j->crcstride, (size_t)cl)) j->bad = 1;
             dg ^= le32(mycrc);
         }
@@ -1210,7 +1252,7 @@ static void *base_worker(void *arg) {
 
 ORC_EXPORT double orc_bench_baseline(int algo, int mode, int nthreads, uint64_t nblocks, const uint64_t *lens,
                                      uint64_t blen, uint64_t seed, uint32_t *digest) {
-    if (mode < 0 || mode > 2) return -3.0;
+    if (mode < 0 || mode > 4) return -3.0;
     if (mode != 2 && !evp_load_open()) return -1.0;
     if (nthreads < 1) nthreads = 1;
     uint64_t maxlen = blen;
@@ -1220,7 +1262,7 @@ ORC_EXPORT double orc_bench_baseline(int algo, int mode, int nthreads, uint64_t 
     base_job *jobs = (base_job *)calloc((size_t)nthreads, sizeof(base_job));
     pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
     const uint64_t per = (nblocks + nthreads - 1) / nthreads;
-    void *sctx = mode == 1 ? evp.ctx_new() : NULL;
+    void *sctx = mode == 1 || mode == 4 ? evp.ctx_new() : NULL;
     for (int t = 0; t < nthreads; t++) {
         base_job *j = &jobs[t];
         j->algo = algo;
@@ -1231,14 +1273,15 @@ ORC_EXPORT double orc_bench_baseline(int algo, int mode, int nthreads, uint64_t 
         j->crcstride = crcstride;
         j->b0 = (uint64_t)t * per < nblocks ? (uint64_t)t * per : nblocks;
         j->b1 = j->b0 + per < nblocks ? j->b0 + per : nblocks;
-        const uint64_t nb = j->b1 - j->b0;
-        j->in = (uint8_t *)malloc(nb ? nb * maxlen : 1);
-        j->work = (uint8_t *)malloc(maxlen + 16);
-        j->tags = (uint8_t *)malloc(nb ? 16 * nb : 1);
+        const uint64_t nb = j->b1 - j->b0, stride = base_stride(j);
+        j->in = (uint8_t *)malloc(nb ? nb * stride : 1);
+        j->work = (uint8_t *)malloc(maxlen + 16 + 271);
+        j->tags = (uint8_t *)malloc(nb ? 16 * nb + 256 : 256);
         j->crcs = (uint8_t *)malloc(nb ? nb * crcstride : 1);
+        for (int i = 0; i < 256; i++) j->tags[i] = (uint8_t)(i * 37 + 11);
         for (uint64_t b = j->b0; b < j->b1; b++) {
             const uint64_t n = base_len(j, b), k = b - j->b0;
-            uint8_t *in = j->in + k * maxlen;
+            uint8_t *in = j->in + k * stride;
             orc_gen_block(seed, b, in, n);
             orc_checksum(in, (int64_t)n, j->crcs + k * crcstride, 1);  /* the cache file's stored CRCs */
             if (mode == 1) {  /* stored object: seal it, keep ciphertext and tag */
@@ -1246,6 +1289,16 @@ ORC_EXPORT double orc_bench_baseline(int algo, int mode, int nthreads, uint64_t 
                 orc_gen_key(seed, b, key, nonce);
                 if (evp_seal(sctx, algo, key, nonce, in, n, j->work, j->tags + 16 * k)) j->bad = 1;
                 memcpy(in, j->work, (size_t)n);
+            } else if (mode == 4) {  /* the encrypted object: header, C, tag */
+                uint8_t key[32], nonce[12];
+                orc_gen_key(seed, b, key, nonce);
+                if (evp_seal(sctx, algo, key, nonce, in, n, j->work + 271, j->work + 271 + n)) j->bad = 1;
+                j->work[0] = 1;
+                j->work[1] = 0;
+                j->work[2] = 12;
+                memset(j->work + 3, 0x5A, 256);
+                memcpy(j->work + 259, nonce, 12);
+                memcpy(in, j->work, (size_t)(n + 287));
             }
         }
     }
@@ -1269,6 +1322,89 @@ ORC_EXPORT double orc_bench_baseline(int algo, int mode, int nthreads, uint64_t 
     free(jobs);
     free(th);
     if (digest) *digest = dg;
+    return bad ? -2.0 : el;
+}
+
+/* ------------------------------------------------------------------ */
+/* CPU baseline of cacheFile.ReadAt at a checksum level (configs[4],   */
+/* bench.py --mode agg --agg-op readat): nblocks cache-file images     */
+/* (block b: lens[b] synthetic bytes, then checksum(), made before the */
+/* clock starts); read r takes blk[r]'s image at (off[r], size[r]).    */
+/* nthreads threads split the reads and run them reps times, through   */
+/* cache_readat with the 3-stream SSE4.2 CRC.  Returns wall seconds,   */
+/* -2 if any read failed.  *bytes: the bytes the reads returned.       */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    const uint8_t *const *imgs;
+    const uint64_t *lens, *off, *size;
+    const uint32_t *blk;
+    uint64_t r0, r1, reps, maxsize;
+    int level, bad;
+    uint64_t bytes;
+} readat_job;
+
+static void *readat_worker(void *arg) {
+    readat_job *j = (readat_job *)arg;
+    uint8_t *out = (uint8_t *)malloc(j->maxsize ? j->maxsize : 1);
+    for (uint64_t rep = 0; rep < j->reps; rep++)
+        for (uint64_t r = j->r0; r < j->r1; r++) {
+            const uint64_t b = j->blk[r], len = j->lens[b];
+            int64_t n = 0, bad_seg = -1;
+            uint32_t got = 0, ex = 0;
+            const int rc = cache_readat(j->imgs[b], (int64_t)(len + orc_checksum_len((int64_t)len)), (int64_t)len,
+                                        j->level, (int64_t)j->off[r], (int64_t)j->size[r], out, &n, &got, &ex,
+                                        &bad_seg, 1);
+            if (rc) j->bad = 1;
+            j->bytes += (uint64_t)n;
+        }
+    free(out);
+    return NULL;
+}
+
+ORC_EXPORT double orc_bench_readat(int nthreads, int level, uint64_t nblocks, const uint64_t *lens, uint64_t seed,
+                                   uint64_t nreads, const uint32_t *blk, const uint64_t *off, const uint64_t *size,
+                                   uint64_t reps, uint64_t *bytes) {
+    if (nthreads < 1) nthreads = 1;
+    uint8_t **imgs = (uint8_t **)calloc((size_t)(nblocks ? nblocks : 1), sizeof(uint8_t *));
+    for (uint64_t b = 0; b < nblocks; b++) {
+        const uint64_t n = lens[b];
+        imgs[b] = (uint8_t *)malloc((size_t)(n + orc_checksum_len((int64_t)n)));
+        orc_gen_block(seed, b, imgs[b], n);
+        orc_checksum(imgs[b], (int64_t)n, imgs[b] + n, 1);
+    }
+    uint64_t maxsize = 0;
+    for (uint64_t r = 0; r < nreads; r++) maxsize = size[r] > maxsize ? size[r] : maxsize;
+    readat_job *jobs = (readat_job *)calloc((size_t)nthreads, sizeof(readat_job));
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    const uint64_t per = (nreads + nthreads - 1) / nthreads;
+    double t0 = now_s();
+    for (int t = 0; t < nthreads; t++) {
+        readat_job *j = &jobs[t];
+        j->imgs = (const uint8_t *const *)imgs;
+        j->lens = lens;
+        j->off = off;
+        j->size = size;
+        j->blk = blk;
+        j->level = level;
+        j->reps = reps;
+        j->maxsize = maxsize;
+        j->r0 = (uint64_t)t * per < nreads ? (uint64_t)t * per : nreads;
+        j->r1 = j->r0 + per < nreads ? j->r0 + per : nreads;
+        pthread_create(&th[t], NULL, readat_worker, j);
+    }
+    int bad = 0;
+    uint64_t tot = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        bad |= jobs[t].bad;
+        tot += jobs[t].bytes;
+    }
+    double el = now_s() - t0;
+    for (uint64_t b = 0; b < nblocks; b++) free(imgs[b]);
+    free(imgs);
+    free(jobs);
+    free(th);
+    if (bytes) *bytes = tot;
     return bad ? -2.0 : el;
 }
 

@@ -61,6 +61,8 @@ def lib():
             "orc_data_decrypt": (I64, [I, P, P, I64, P]),
             "orc_bench_seal_crc": (ctypes.c_double, [I, I, U64, U64, U64, P]),
             "orc_bench_baseline": (ctypes.c_double, [I, I, I, U64, P, U64, U64, P]),
+            "orc_bench_readat": (ctypes.c_double, [I, I, U64, P, U64, U64, P, P, P, U64, P]),
+            "orc_cache_readat_hw": (I, [P, I64, I64, I, I64, I64, P, P, P, P, P]),
             "orc_expect_batch": (ctypes.c_double, [I, I, U64, P, U64, U64, U64, P, P, U64]),
             "orc_lz4_bound": (I, [I]),
             "orc_lz4_compress": (I, [P, I, P, I]),
@@ -254,7 +256,7 @@ def bench_seal_crc_evp(algo, nthreads, nblocks, blen, seed):
     return secs, dg.value
 
 
-BASE_SEAL, BASE_OPEN, BASE_CRC = 0, 1, 2
+BASE_SEAL, BASE_OPEN, BASE_CRC, BASE_ENCRYPT, BASE_DECRYPT = 0, 1, 2, 3, 4
 
 
 def bench_baseline(algo, mode, nthreads, nblocks, blen, seed, lens=None):
@@ -267,6 +269,20 @@ def bench_baseline(algo, mode, nthreads, nblocks, blen, seed, lens=None):
     secs = lib().orc_bench_baseline(algo, mode, nthreads, nblocks, ln.ctypes.data if ln is not None else None, blen,
                                     seed, ctypes.byref(dg))
     return secs, dg.value
+
+
+def bench_readat(nthreads, level, lens, seed, reads, reps):
+    """(seconds, bytes returned) of cacheFile.ReadAt (3-stream SSE4.2 CRC) on
+    nthreads threads: cache-file images of the synthetic blocks 0..n-1 of
+    lens[b] bytes, reads = [(block, off, size)], each run reps times."""
+    ln = np.asarray(lens, np.uint64)
+    blk = np.asarray([r[0] for r in reads], np.uint32)
+    off = np.asarray([r[1] for r in reads], np.uint64)
+    size = np.asarray([r[2] for r in reads], np.uint64)
+    nbytes = ctypes.c_uint64()
+    secs = lib().orc_bench_readat(nthreads, level, ln.size, ln.ctypes.data, seed, len(reads), blk.ctypes.data,
+                                  off.ctypes.data, size.ctypes.data, reps, ctypes.byref(nbytes))
+    return secs, nbytes.value
 
 
 def expect_batch(algo, nthreads, lens, seed, block0, crcstride):

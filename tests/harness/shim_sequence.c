@@ -2,8 +2,11 @@
  * the C-ABI exactly as the Go side makes it, checked against the CPU oracle.
  *
  *   §2 gpuEncryptor.Encrypt  -> jfsx_agg_data_encrypt over the multi-device
- *                               aggregator, from many threads (and the one-call
- *                               jfsx_data_encrypt, obj_crc NULL / set)
+ *                               aggregator, from many threads, on malloc'd
+ *                               (pageable, Go-heap-like) buffers (and the
+ *                               one-call jfsx_data_encrypt, obj_crc NULL / set);
+ *                               jfsx_agg_data_encrypt_ex / _decrypt_ex with the
+ *                               plaintext checksum() out of the same call
  *      gpuEncryptor.Decrypt  -> jfsx_parse_header, [key unwrap], jfsx_agg_data_decrypt
  *                               (and jfsx_data_decrypt)
  *   §3 upload goroutines     -> jfsx_agg_seal / jfsx_agg_open on descriptors in
@@ -94,8 +97,14 @@ static void *obj_worker(void *vp) {
         const uint64_t n = kLens[i];
         uint8_t key[32], nonce[12];
         orc_gen_key(SEED, 3000 + i, key, nonce);
+        /* Go-heap shapes: the plaintext is io.ReadAll's slice, the object a
+         * fresh make([]byte) (encrypt.go:183, :258) -- pageable malloc memory,
+         * staged by the engine's bounce pool */
         uint8_t *p = malloc(n + 1), *obj = malloc(n + 287), *ref = malloc(n + 287), *back = malloc(n + 287);
+        const int64_t cl = orc_checksum_len((int64_t)n);
+        uint8_t *seg = malloc((size_t)cl), *seg2 = malloc((size_t)cl), *want = malloc((size_t)cl);
         orc_gen_block(SEED, 3000 + i, p, n);
+        orc_checksum(p, (int64_t)n, want, 1);
         uint64_t olen = 0, pl = 0;
         uint32_t ocrc = 0, got = 0;
         if (jfsx_agg_data_encrypt(a->agg, a->algo, key, nonce, wrapped, 256, p, n, obj, n + 287, &olen, &ocrc) ||
@@ -105,7 +114,22 @@ static void *obj_worker(void *vp) {
         else if (jfsx_agg_data_decrypt(a->agg, a->algo, key, obj, olen, back, olen, &pl, &ocrc, &got) || pl != n ||
                  got != ocrc || memcmp(back, p, n) != 0)
             a->bad++;
-        free(p), free(obj), free(ref), free(back);
+        /* wSlice.upload -> bcache.stage + store.upload: checksum() of the
+         * plaintext and the sealed object (and its object CRC) from one call;
+         * store.load -> bcache.cache: the plaintext and its checksum() */
+        memset(obj, 0, n + 287);
+        ocrc = 0;
+        if (jfsx_agg_data_encrypt_ex(a->agg, a->algo, key, nonce, wrapped, 256, p, n, obj, n + 287, &olen, &ocrc,
+                                     seg) ||
+            memcmp(obj, ref, olen) != 0 || ocrc != orc_crc32c_update(0, obj, olen) || memcmp(seg, want, (size_t)cl))
+            a->bad++;
+        else if (jfsx_agg_data_decrypt_ex(a->agg, a->algo, key, obj, olen, back, olen, &pl, &ocrc, &got, seg2) ||
+                 pl != n || memcmp(back, p, n) != 0 || memcmp(seg2, want, (size_t)cl))
+            a->bad++;
+        else if (jfsx_agg_data_encrypt_ex(a->agg, a->algo, key, nonce, wrapped, 256, p, n, obj, n + 287, &olen, NULL,
+                                          seg) || memcmp(obj, ref, olen) != 0 || memcmp(seg, want, (size_t)cl))
+            a->bad++;
+        free(p), free(obj), free(ref), free(back), free(seg), free(seg2), free(want);
     }
     return NULL;
 }
@@ -124,7 +148,7 @@ static void agg_encrypt_decrypt(jfsx_mctx *m, int algo) {
         CHECK(a[t].bad == 0);
     }
     uint64_t calls = 0, batches = 0, blocks = 0;
-    CHECK(jfsx_agg_stats(agg, &calls, &batches, &blocks) == 0 && calls == 2 * NTHREADS * PER_THREAD);
+    CHECK(jfsx_agg_stats(agg, &calls, &batches, &blocks) == 0 && calls == 5 * NTHREADS * PER_THREAD);
     CHECK(jfsx_agg_free(agg) == 0);
 }
 

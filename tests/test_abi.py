@@ -23,7 +23,7 @@ def test_library_exports_every_symbol():
     L = engine.load_library()
     for name in _declared():
         assert hasattr(L, name), name
-    assert L.jfsx_abi_version() == 8
+    assert L.jfsx_abi_version() == 9
 
 
 def test_struct_layout_matches_header():

@@ -74,7 +74,8 @@ def test_bench_gpus_2_launches_two_ranks():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
                                                             "MASTER_PORT")}
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run",
-                          "--blocks", "5"], env=env, capture_output=True, text=True, timeout=240)
+                          "--blocks", "5", "--cpu-seconds", "0.2"], env=env, capture_output=True, text=True,
+                         timeout=240)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout
@@ -82,13 +83,16 @@ def test_bench_gpus_2_launches_two_ranks():
     assert rec["n_gpus"] == 2 and rec["dry_run"] is True
     assert rec["last_rank_first_block"] == 5  # rank 1 owns blocks [5, 10)
     assert rec["ms_per_step"] >= 1.0  # rank 1's extra 1 ms: the max over ranks is reported
+    # the CPU leg at N > 1: rank 0 times the baseline after the timed region
+    cpu = rec["cpu_baseline"]
+    assert cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["kind"] == "port" and cpu["core_s_per_GB"] > 0
 
 
 def _bench_dry(args):
     import subprocess
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
                                                             "MASTER_PORT")}
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run"] + args, env=env,
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--no-cpu"] + args, env=env,
                          capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
