@@ -1207,7 +1207,9 @@ def agg_bench(args, world, rank, local, dist, eng):
         warm_up(args, lambda: run(through, 1), host=True)
         c0, b0, k0 = agg.stats()
         barrier(dist)
+        cpu0 = host_cpu_seconds()
         el = max_over_ranks(dist, run(through, args.steps), local)
+        cpu_used = host_cpu_seconds() - cpu0
         c1, b1, k1 = agg.stats()
     verified = 0
     if args.verify:
@@ -1240,6 +1242,13 @@ def agg_bench(args, world, rank, local, dist, eng):
     value = world * nb * L * args.steps / el / 1e9
     cpu = (cpu_baseline(args, "open" if is_open else "seal", node=node) if rank == 0 and not args.no_cpu
            else None)
+    gb = world * nb * L * args.steps / 1e9
+    host_cpu = {"cpu_seconds": round(cpu_used, 3), "cpu_s_per_GB": round(cpu_used / gb, 4),
+                "cores_busy": round(cpu_used / el, 2),
+                "cpu_baseline_core_s_per_GB": cpu["core_s_per_GB"] if cpu else None,
+                "note": "getrusage(RUSAGE_SELF) over the timed region: every thread of this process (the Python "
+                        "callers and their ctypes calls, the aggregator's dispatchers); no bounce copies (pinned "
+                        "blocks)"}
     pcie = eng.pcie_probe()
     duplex = min(pcie["duplex_h2d"], pcie["duplex_d2h"])
     if rank == 0:
@@ -1267,7 +1276,7 @@ def agg_bench(args, world, rank, local, dist, eng):
                          "frac": round(value / duplex, 4), "peak_basis": "min over directions of simultaneous H2D + "
                          "D2H copies (jfsx_pcie_probe, after the run)", "pcie_measured": pcie,
                          "frac_of_link": round(value / PCIE_GEN5_X16_GBS, 4)},
-            "cpu_baseline": cpu, "verified_blocks": verified, "full_check": full}), flush=True)
+            "host_cpu": host_cpu, "cpu_baseline": cpu, "verified_blocks": verified, "full_check": full}), flush=True)
     for h in (hin, hout, hcrc, hdec, hcrc2):
         if h:
             eng.free_pinned(h)
@@ -1414,7 +1423,9 @@ def agg_heap_bench(args, world, rank, local, dist, eng):
         for b in range(nb):
             R[b].data, R[b].len, R[b].crc = ip + IS * b, lens[b], ip + IS * b + lens[b]
         eng.crc32c_segments(R, nb, E.CRC_GEN, E.MEM_HOST)
-        out = np.empty(nb * L, np.uint8)
+        # ReadAt's destination: per block for the whole-block verify, per
+        # calling thread for the random reads (several reads of one image)
+        out = np.empty((nb if op == "verify" else T) * L, np.uint8)
         dp = out.ctypes.data
         level = "full" if op == "verify" else args.level
         lv = {"full": 1, "shrink": 2, "extend": 3}[level]
@@ -1426,9 +1437,9 @@ def agg_heap_bench(args, world, rank, local, dist, eng):
 
         def through(r, st):
             b, off, size = reads[r]
-            n, g, e, s = st
-            rc = cv(eng.ctx, ip + IS * b, flen[b], lens[b], lv, off, size, dp + L * b, ctypes.byref(n),
-                    ctypes.byref(g), ctypes.byref(e), ctypes.byref(s))
+            n, g, e, s, t = st
+            rc = cv(eng.ctx, ip + IS * b, flen[b], lens[b], lv, off, size, dp + L * (b if op == "verify" else t),
+                    ctypes.byref(n), ctypes.byref(g), ctypes.byref(e), ctypes.byref(s))
             nret[r] = n.value
             return rc
         direct = None
@@ -1440,7 +1451,7 @@ def agg_heap_bench(args, world, rank, local, dist, eng):
     def run(call, steps):
         def worker(t):
             try:
-                st = ((ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_int64())
+                st = ((ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_int64(), t)
                       if op in ("verify", "readat") else ctypes.c_uint64())
                 for _ in range(steps):
                     for u in units[t * per:(t + 1) * per]:
@@ -1524,9 +1535,13 @@ def agg_heap_bench(args, world, rank, local, dist, eng):
                 raise SystemExit("bench: read %d returned %d bytes, ReadAt returns %d" % (r, nret[r], want[r]))
             for r in range(0, len(reads), max(1, len(reads) // max(args.verify, 1)))[:args.verify]:
                 b, o, s = reads[r]
-                img = imgs[IS * b:IS * b + lens[b] + 4 * max(1, -(-lens[b] // E.SEG))].tobytes()
-                rc, data = orc.cache_readat(img, lens[b], lv, o, s)[:2]
-                if rc != 0 or data != out[L * b:L * b + s].tobytes():
+                img = imgs[IS * b:IS * b + lens[b] + 4 * max(1, -(-lens[b] // E.SEG))]
+                rc, data = orc.cache_readat(img.tobytes(), lens[b], lv, o, s)[:2]
+                # the timed read's bytes (whole-block verify), or the same read
+                # made again (random reads share their thread's destination)
+                mine = (out[L * b:L * b + s].tobytes() if op == "verify"
+                        else eng.cache_verify(img, lens[b], lv, o, s)[1])
+                if rc != 0 or data != mine:
                     raise SystemExit("bench: read %d differs from the oracle's ReadAt" % r)
             full["what"] = ("cache-file trailers of all %d images equal to the oracle's; every one of %d %s reads "
                             "returned ReadAt's byte count with status OK (each verified its window); %d reads' bytes "
@@ -1573,7 +1588,7 @@ def agg_heap_bench(args, world, rank, local, dist, eng):
                            "mean_batch_blocks": round((k1 - k0) / max(b1 - b0, 1), 2)} if op != "verify" and
             op != "readat" else None,
             "direct_calls_GBs": d_val,
-            "engine_metrics_delta": {k: getattr(m1, k) - getattr(m0, k) for k in
+            "engine_metrics_delta": {k: m1[k] - m0[k] for k in
                                      ("seal_batches", "seal_bytes", "open_batches", "open_bytes", "crc_batches",
                                       "crc_bytes")},
             "host_cpu": host_cpu,

@@ -345,6 +345,40 @@ struct jfsx_agg {
     }
 };
 
+namespace jfsx {
+// pinned staging of pageable caller memory (jfsx_api.cpp; the host harness
+// stubs them)
+bool host_pinned(const void *p, uint64_t n);
+char *bounce_acquire(jfsx_ctx *c, size_t need, size_t *cap);
+void bounce_release(jfsx_ctx *c, char *p, size_t cap);
+void bounce_count(jfsx_ctx *c, uint64_t in, uint64_t out);
+}  // namespace jfsx
+
+namespace {
+// A per-object request on pageable memory (a Go-heap slice: io.ReadAll's
+// result, Encrypt's fresh object buffer, encrypt.go:183, :258; a cache page)
+// is staged here, on the calling thread: its block is copied into a pinned
+// bounce buffer of the engine before the request is queued, and its output
+// copied out of it after the request completes.  So max-uploads callers copy
+// in parallel, and the dispatchers, which run the batches, never copy.
+struct Staged {
+    jfsx_ctx *c = nullptr;
+    char *p = nullptr;
+    size_t cap = 0;
+    ~Staged() {
+        if (p) jfsx::bounce_release(c, p, cap);
+    }
+    int get(jfsx_ctx *ctx, uint64_t len) {
+        c = ctx;
+        p = jfsx::bounce_acquire(c, (size_t)((len + 255) & ~(uint64_t)255), &cap);
+        return p ? 0 : JFSX_ENOMEM;
+    }
+};
+
+int agg_aead(jfsx_agg *a, int op, int algo, jfsx_blk *blk, int crc_mode, int mem);
+int agg_crc(jfsx_agg *a, jfsx_range *range, int mode, int mem);
+}  // namespace
+
 namespace {
 // dispatcher threads per context (JFSX_AGG_DISPATCHERS overrides)
 int dispatchers_per_ctx() {
@@ -413,20 +447,17 @@ int jfsx_agg_dev_batches(jfsx_agg *a, int i, uint64_t *batches) {
 
 int jfsx_agg_seal(jfsx_agg *a, int algo, jfsx_blk *blk, int crc_mode, int mem) {
     if (!a || !blk || !valid_algo(algo) || !agg_mem_ok(a, mem)) return JFSX_EINVAL;
-    Req r{kSeal, algo, crc_mode, mem, blk, nullptr, nullptr, blk->len};
-    return a->submit(r);
+    return agg_aead(a, kSeal, algo, blk, crc_mode, mem);
 }
 
 int jfsx_agg_open(jfsx_agg *a, int algo, jfsx_blk *blk, int crc_mode, int mem) {
     if (!a || !blk || !valid_algo(algo) || !agg_mem_ok(a, mem)) return JFSX_EINVAL;
-    Req r{kOpen, algo, crc_mode, mem, blk, nullptr, nullptr, blk->len};
-    return a->submit(r);
+    return agg_aead(a, kOpen, algo, blk, crc_mode, mem);
 }
 
 int jfsx_agg_crc32c(jfsx_agg *a, jfsx_range *range, int mode, int mem) {
     if (!a || !range || !agg_mem_ok(a, mem) || (mode != JFSX_CRC_GEN && mode != JFSX_CRC_VERIFY)) return JFSX_EINVAL;
-    Req r{kCrc, 0, mode, mem, nullptr, range, nullptr, range->len};
-    return a->submit(r);
+    return agg_crc(a, range, mode, mem);
 }
 
 int jfsx_agg_lz4_compress(jfsx_agg *a, jfsx_zblk *z, int mem) {
@@ -452,6 +483,66 @@ int jfsx_agg_zstd_compress(jfsx_agg *a, jfsx_zblk *z, int mem) {
     Req r{kZstdc, 0, 0, mem, nullptr, nullptr, z, z->src_len};
     return a->submit(r);
 }
+
+}  // extern "C"
+
+namespace {
+int agg_aead(jfsx_agg *a, int op, int algo, jfsx_blk *blk, int crc_mode, int mem) {
+    const uint64_t len = blk->len;
+    const bool host = mem == JFSX_MEM_HOST && len && blk->src && blk->dst;
+    const bool in_pg = host && !jfsx::host_pinned(blk->src, len);
+    const bool out_pg = host && (blk->dst == blk->src ? in_pg : !jfsx::host_pinned(blk->dst, len));
+    if (!in_pg && !out_pg) {
+        Req r{op, algo, crc_mode, mem, blk, nullptr, nullptr, len};
+        return a->submit(r);
+    }
+    Staged st;
+    if (st.get(a->cs[0], len)) return JFSX_ENOMEM;
+    jfsx_blk w = *blk;
+    if (in_pg) {
+        memcpy(st.p, blk->src, len);
+        w.src = st.p;
+    }
+    if (out_pg) w.dst = st.p;  // in place in the bounce buffer when both are pageable
+    Req r{op, algo, crc_mode, mem, &w, nullptr, nullptr, len};
+    const int rc = a->submit(r);
+    const void *src = blk->src;
+    void *dst = blk->dst;
+    *blk = w;  // results into the caller's record, its own pointers kept
+    blk->src = src;
+    blk->dst = dst;
+    if (rc == 0 && out_pg) {
+        // an Open whose tag failed releases nothing (the engine zeroed the
+        // bounce copy; the caller's buffer is zeroed here)
+        if (op == kOpen && w.status == JFSX_ETAG) memset(dst, 0, len);
+        else memcpy(dst, st.p, len);
+    }
+    jfsx::bounce_count(st.c, in_pg ? len : 0, rc == 0 && out_pg ? len : 0);
+    return rc;
+}
+
+int agg_crc(jfsx_agg *a, jfsx_range *range, int mode, int mem) {
+    const uint64_t len = range->len;
+    if (mem != JFSX_MEM_HOST || !len || !range->data || jfsx::host_pinned(range->data, len)) {
+        Req r{kCrc, 0, mode, mem, nullptr, range, nullptr, len};
+        return a->submit(r);
+    }
+    Staged st;
+    if (st.get(a->cs[0], len)) return JFSX_ENOMEM;
+    memcpy(st.p, range->data, len);
+    jfsx_range w = *range;
+    w.data = st.p;
+    Req r{kCrc, 0, mode, mem, nullptr, &w, nullptr, len};
+    const int rc = a->submit(r);
+    const void *data = range->data;
+    *range = w;
+    range->data = data;
+    jfsx::bounce_count(st.c, len, 0);
+    return rc;
+}
+}  // namespace
+
+extern "C" {
 
 int jfsx_agg_stats(jfsx_agg *a, uint64_t *calls, uint64_t *batches, uint64_t *blocks) {
     if (!a) return JFSX_EINVAL;

@@ -116,6 +116,9 @@ int bounce_policy() {
     return v;
 }
 
+}  // namespace
+
+namespace jfsx {
 // true when [p, p + n) may be handed to the DMA engines as it is: engine-pinned
 // memory, or host memory the HIP runtime reports as registered (another
 // library's pinned buffers).  Everything else -- the Go heap, malloc, numpy --
@@ -137,6 +140,9 @@ bool host_pinned(const void *p, uint64_t n) {
     (void)hipGetLastError();
     return reg;
 }
+}  // namespace jfsx
+
+namespace {
 
 // ---------------------------------------------------------------------------
 // table construction (host)
@@ -327,6 +333,9 @@ struct jfsx_ctx {
     // (groups, us enqueueing under mu, us waiting for a busy slot, us waiting
     // for one's own groups)
     std::atomic<uint64_t> ps_groups{0}, ps_enq_us{0}, ps_slot_us{0}, ps_own_us{0};
+    // host-memory checks, bounce copies in (with the buffer's acquisition) and
+    // out, waits for one's own groups (us, summed over callers)
+    std::atomic<uint64_t> ps_pin_us{0}, ps_bin_us{0}, ps_bout_us{0}, ps_wait_us{0};
     std::atomic<uint64_t> ps_blocks{0}, ps_h2d{0}, ps_d2h{0};  // blocks, data copies up / down (coalesced runs)
     std::mutex stat_mu; // met, ms_total, launches
     std::atomic<size_t> slot_bytes{(size_t)256 << 20};
@@ -1108,23 +1117,53 @@ char *bounce_get(jfsx_ctx *c, size_t need, size_t *cap) {
     const size_t n = bounce_class(need);
     void *p = nullptr;
     if (alloc_pinned_on(c->numa_node, n, &p)) return nullptr;
+    note_pinned(p, n);  // so host_pinned() knows a bounced block at once
     b.allocs++;
     *cap = n;
     return (char *)p;
 }
 
+// Back to the idle list.  Over the retention cap the largest idle buffers go
+// first, so one big pageable host-ingest call's buffers do not crowd out the
+// per-object ones (which would then be allocated and freed on every call).
 void bounce_put(jfsx_ctx *c, char *p, size_t cap) {
     BouncePool &b = c->bounce;
+    std::vector<char *> drop;
     {
         std::lock_guard<std::mutex> g(b.mu);
-        if (b.idle_bytes + cap <= bounce_retain()) {
-            b.idle.emplace(cap, p);
-            b.idle_bytes += cap;
-            return;
+        b.idle.emplace(cap, p);
+        b.idle_bytes += cap;
+        while (b.idle_bytes > bounce_retain() && !b.idle.empty()) {
+            auto it = std::prev(b.idle.end());
+            b.idle_bytes -= it->first;
+            drop.push_back(it->second);
+            b.idle.erase(it);
         }
     }
-    (void)hipHostFree(p);
+    for (char *q : drop) {
+        forget_pinned(q);
+        (void)hipHostFree(q);
+    }
 }
+
+}  // namespace
+
+namespace jfsx {
+// the aggregator stages pageable per-object requests on the calling thread
+// with these (jfsx_agg.cpp)
+char *bounce_acquire(jfsx_ctx *c, size_t need, size_t *cap) {
+    CtxScope es_(c);
+    (void)hipSetDevice(c->device);
+    return bounce_get(c, need, cap);
+}
+void bounce_release(jfsx_ctx *c, char *p, size_t cap) { bounce_put(c, p, cap); }
+void bounce_count(jfsx_ctx *c, uint64_t in, uint64_t out) {
+    c->bounce.bytes_in += in;
+    c->bounce.bytes_out += out;
+}
+}  // namespace jfsx
+
+namespace {
 
 // memcpy of a group's blocks into / out of its bounce buffer: on the calling
 // thread (each per-object caller copies its own block, so max-uploads callers
@@ -1192,10 +1231,13 @@ int run_host(jfsx_ctx *c, PipeOp op, int algo, int n, jfsx_blk *blks, int crc_mo
     // wait for group g, copy its bounced outputs out, release its bounce buffer
     auto finish = [&](size_t g) {
         PipeGroup &r = recs[g];
+        const SClock::time_point f0 = SClock::now();
         {
             std::lock_guard<std::mutex> sl(r.slot->mu);
             if (r.slot->owner == &r) pipe_collect(c, *r.slot);
         }
+        const SClock::time_point f1 = SClock::now();
+        c->ps_wait_us += us(f0, f1);
         if (!r.rc) {
             cp.clear();
             cl.clear();
@@ -1206,6 +1248,7 @@ int run_host(jfsx_ctx *c, PipeOp op, int algo, int n, jfsx_blk *blks, int crc_mo
                     c->bounce.bytes_out += blks[i].len;
                 }
             par_copy(cp, cl);
+            c->ps_bout_us += us(f1, SClock::now());
         }
         if (r.bounce) {
             bounce_put(c, r.bounce, r.bcap);
@@ -1220,6 +1263,7 @@ int run_host(jfsx_ctx *c, PipeOp op, int algo, int n, jfsx_blk *blks, int crc_mo
         // (1) bounce the group's pageable blocks: one region per block, used
         // by its input (copied in here) and / or its output (copied out by
         // finish); in place when src == dst
+        const SClock::time_point p0 = SClock::now();
         size_t need = 0;
         std::vector<size_t> boff(b1 - b0, SIZE_MAX);
         std::vector<char> in_pg(b1 - b0, 0);
@@ -1232,6 +1276,8 @@ int run_host(jfsx_ctx *c, PipeOp op, int algo, int n, jfsx_blk *blks, int crc_mo
             boff[i - b0] = need;
             need += align256(b.len);
         }
+        const SClock::time_point p1 = SClock::now();
+        c->ps_pin_us += us(p0, p1);
         if (need) {
             if (!(r.bounce = bounce_get(c, need, &r.bcap))) {
                 rc = JFSX_ENOMEM;
@@ -1252,6 +1298,7 @@ int run_host(jfsx_ctx *c, PipeOp op, int algo, int n, jfsx_blk *blks, int crc_mo
                 if (out_b[i]) hv[i].dst = q;
             }
             par_copy(cp, cl);
+            c->ps_bin_us += us(p1, SClock::now());
         }
         // (2) a slot, (3) the enqueue
         const SClock::time_point t0 = SClock::now();
@@ -1638,13 +1685,23 @@ int jfsx_ctx_close(jfsx_ctx *c) {
                 (unsigned long long)c->ps_h2d.load(), (unsigned long long)c->ps_d2h.load(),
                 c->ps_enq_us.load() / (double)c->ps_groups, c->ps_slot_us.load() / (double)c->ps_groups,
                 c->ps_own_us.load() / (double)c->ps_groups);
+    if (getenv("JFSX_PIPE_STATS") && c->ps_groups)
+        fprintf(stderr, "jfsx pipe stats (device %d): per group: host-memory checks %.1f us, bounce in %.1f us, "
+                "bounce out %.1f us, own-group wait %.1f us; bounce: %llu allocations, %.1f MB in, %.1f MB out\n",
+                c->device, c->ps_pin_us.load() / (double)c->ps_groups, c->ps_bin_us.load() / (double)c->ps_groups,
+                c->ps_bout_us.load() / (double)c->ps_groups, c->ps_wait_us.load() / (double)c->ps_groups,
+                (unsigned long long)c->bounce.allocs.load(), c->bounce.bytes_in.load() / 1e6,
+                c->bounce.bytes_out.load() / 1e6);
     async_detach(c);  // queued _async batches run first (jfsx_agg.cpp)
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
     if (c->d_tab) (void)hipFree(c->d_tab);
     if (c->rsa_d) (void)hipFree(c->rsa_d);
     if (c->rsa_h) (void)hipHostFree(c->rsa_h);
-    for (auto &kv : c->bounce.idle) (void)hipHostFree(kv.second);
+    for (auto &kv : c->bounce.idle) {
+        forget_pinned(kv.second);
+        (void)hipHostFree(kv.second);
+    }
     c->bounce.idle.clear();
     for (int k = 0; k < kRing; k++) {
         Workspace &w = c->ws[k];

@@ -5,6 +5,7 @@
 // without a GPU.  Fake devices are contexts 0x1000 + 0x100*d.
 // The stubs record every batch they receive and compute a position-free fake
 // "tag" so results can be matched to their requesters.
+#include <atomic>
 #include <chrono>
 #include <mutex>
 #include <thread>
@@ -56,6 +57,21 @@ int device_of(const void *p, uintptr_t *lo, uintptr_t *hi) {
     *hi = (uintptr_t)(d + 2) << 40;
     return d;
 }
+// staging stubs: every host buffer counts as pinned unless the harness marks
+// a range pageable (harness_pageable); bounce buffers are malloc'd
+uintptr_t h_pg_lo = 0, h_pg_hi = 0;
+std::atomic<int> h_bounces{0};
+bool host_pinned(const void *p, uint64_t n) {
+    const uintptr_t a = (uintptr_t)p;
+    return !(a < h_pg_hi && a + n > h_pg_lo);
+}
+char *bounce_acquire(jfsx_ctx *, size_t need, size_t *cap) {
+    h_bounces++;
+    *cap = need;
+    return (char *)malloc(need ? need : 1);
+}
+void bounce_release(jfsx_ctx *, char *p, size_t) { free(p); }
+void bounce_count(jfsx_ctx *, uint64_t, uint64_t) {}
 }  // namespace jfsx
 
 extern "C" {
