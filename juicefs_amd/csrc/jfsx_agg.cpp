@@ -349,6 +349,8 @@ namespace jfsx {
 // pinned staging of pageable caller memory (jfsx_api.cpp; the host harness
 // stubs them)
 bool host_pinned(const void *p, uint64_t n);
+bool host_pin(const void *p, uint64_t n);
+void host_unpin(const void *p);
 char *bounce_acquire(jfsx_ctx *c, size_t need, size_t *cap);
 void bounce_release(jfsx_ctx *c, char *p, size_t cap);
 void bounce_count(jfsx_ctx *c, uint64_t in, uint64_t out);
@@ -365,8 +367,11 @@ struct Staged {
     jfsx_ctx *c = nullptr;
     char *p = nullptr;
     size_t cap = 0;
+    const void *pin[2] = {nullptr, nullptr};  // caller ranges pinned for the call
     ~Staged() {
         if (p) jfsx::bounce_release(c, p, cap);
+        for (const void *q : pin)
+            if (q) jfsx::host_unpin(q);
     }
     int get(jfsx_ctx *ctx, uint64_t len) {
         c = ctx;
@@ -490,13 +495,23 @@ namespace {
 int agg_aead(jfsx_agg *a, int op, int algo, jfsx_blk *blk, int crc_mode, int mem) {
     const uint64_t len = blk->len;
     const bool host = mem == JFSX_MEM_HOST && len && blk->src && blk->dst;
-    const bool in_pg = host && !jfsx::host_pinned(blk->src, len);
-    const bool out_pg = host && (blk->dst == blk->src ? in_pg : !jfsx::host_pinned(blk->dst, len));
+    bool in_pg = host && !jfsx::host_pinned(blk->src, len);
+    bool out_pg = host && (blk->dst == blk->src ? in_pg : !jfsx::host_pinned(blk->dst, len));
+    Staged st;
+    // first choice: pin the caller's own pages for the call (no copy)
+    if (in_pg && jfsx::host_pin(blk->src, len)) {
+        st.pin[0] = blk->src;
+        in_pg = false;
+        if (blk->dst == blk->src) out_pg = false;
+    }
+    if (out_pg && jfsx::host_pin(blk->dst, len)) {
+        st.pin[1] = blk->dst;
+        out_pg = false;
+    }
     if (!in_pg && !out_pg) {
         Req r{op, algo, crc_mode, mem, blk, nullptr, nullptr, len};
         return a->submit(r);
     }
-    Staged st;
     if (st.get(a->cs[0], len)) return JFSX_ENOMEM;
     jfsx_blk w = *blk;
     if (in_pg) {
@@ -528,6 +543,11 @@ int agg_crc(jfsx_agg *a, jfsx_range *range, int mode, int mem) {
         return a->submit(r);
     }
     Staged st;
+    if (jfsx::host_pin(range->data, len)) {
+        st.pin[0] = range->data;
+        Req r{kCrc, 0, mode, mem, nullptr, range, nullptr, len};
+        return a->submit(r);
+    }
     if (st.get(a->cs[0], len)) return JFSX_ENOMEM;
     memcpy(st.p, range->data, len);
     jfsx_range w = *range;

@@ -102,20 +102,39 @@ void forget_pinned(void *p) {
     std::unique_lock<std::shared_mutex> g(g_pin_mu);
     g_pinned.erase((uintptr_t)p);
 }
+// base of the engine-pinned allocation holding p, 0 if none
+uintptr_t pinned_base(const void *p) {
+    const uintptr_t a = (uintptr_t)p;
+    std::shared_lock<std::shared_mutex> g(g_pin_mu);
+    auto it = g_pinned.upper_bound(a);
+    if (it == g_pinned.begin()) return 0;
+    --it;
+    return a < it->second ? it->first : 0;
+}
 
-// JFSX_HOST_BOUNCE: "auto" (default) bounces pageable memory only, "0" never
-// bounces (pageable pointers go to hipMemcpyAsync as they are: the runtime's
-// own staged copy, an A/B reference), "all" bounces every host block.
-int bounce_policy() {
+// JFSX_HOST_STAGE: how a pageable host block reaches the DMA engines.
+//   bounce (default)    copy it into the context's pinned bounce buffers on
+//                       the calling thread (20 per-object callers: 41.7 GB/s,
+//                       0.22 host CPU-s per GB, profiles/r6)
+//   register            pin the caller's own pages for the call
+//                       (hipHostRegister / hipHostUnregister around it), and
+//                       bounce where the runtime refuses; no copies (0.10 CPU-s
+//                       per GB) but 28-31 GB/s: under 20 concurrent callers
+//                       the runtime's registration and lookup calls contend
+//   none                hand the pageable pointer to hipMemcpyAsync as it is
+//                       (the runtime's own staged copy: 15.3 GB/s, A/B only)
+//   all                 bounce every host block, pinned or not (tests)
+enum { kStageNone = 0, kStageRegister = 1, kStageBounce = 2, kStageAll = 3 };
+int stage_policy() {
     static const int v = [] {
-        const char *e = getenv("JFSX_HOST_BOUNCE");
-        if (!e || !strcmp(e, "auto")) return 1;
-        if (!strcmp(e, "0")) return 0;
-        return 2;
+        const char *e = getenv("JFSX_HOST_STAGE");
+        if (!e || !strcmp(e, "bounce")) return (int)kStageBounce;
+        if (!strcmp(e, "register")) return (int)kStageRegister;
+        if (!strcmp(e, "none")) return (int)kStageNone;
+        return (int)kStageAll;
     }();
     return v;
 }
-
 }  // namespace
 
 namespace jfsx {
@@ -124,8 +143,8 @@ namespace jfsx {
 // library's pinned buffers).  Everything else -- the Go heap, malloc, numpy --
 // is pageable and goes through the context's bounce pool.
 bool host_pinned(const void *p, uint64_t n) {
-    const int pol = bounce_policy();
-    if (pol != 1 || !n) return pol != 2;
+    const int pol = stage_policy();
+    if (pol == kStageNone || pol == kStageAll || !n) return pol != kStageAll || !n;
     const uintptr_t a = (uintptr_t)p;
     {
         std::shared_lock<std::shared_mutex> g(g_pin_mu);
@@ -139,6 +158,27 @@ bool host_pinned(const void *p, uint64_t n) {
     const bool reg = hipPointerGetAttributes(&at, p) == hipSuccess && at.type == hipMemoryTypeHost;
     (void)hipGetLastError();
     return reg;
+}
+
+// Pin a pageable caller range for the duration of one call (JFSX_HOST_STAGE
+// register): true when it is now page-locked and must be released with
+// host_unpin once the call's DMA has finished; false where the policy is not
+// register or the runtime refuses (the caller then bounces the block).  The
+// Go heap does not move objects, and the range is released before the call
+// returns, so cgo's rule that C keeps no Go pointer past the call holds.
+bool host_pin(const void *p, uint64_t n) {
+    if (stage_policy() != kStageRegister || !n) return false;
+    const hipError_t e = hipHostRegister(const_cast<void *>(p), n, hipHostRegisterPortable);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    note_pinned(const_cast<void *>(p), n);  // host_pinned() then answers from the registry
+    return true;
+}
+void host_unpin(const void *p) {
+    forget_pinned(const_cast<void *>(p));
+    if (hipHostUnregister(const_cast<void *>(p)) != hipSuccess) (void)hipGetLastError();
 }
 }  // namespace jfsx
 
@@ -298,6 +338,7 @@ struct PipeGroup {
     int rc = 0;
     char *bounce = nullptr;  // pinned bounce region of the group's pageable blocks (owner only)
     size_t bcap = 0;
+    std::vector<const void *> pins;  // caller ranges pinned for the group (owner only)
 };
 
 // Engine-owned pinned staging for callers' pageable memory (SURVEY §8b
@@ -962,7 +1003,7 @@ enum PipeOp { kPipeSeal, kPipeOpen, kPipeCrc };
 // outputs straight into engine-pinned caller memory over PCIe ran at 25 GB/s
 // against 38.7 staged and was removed.)
 int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, PipeOp op, int algo, int nb, const jfsx_blk *blks, jfsx_blk *dv,
-                 int crc_mode) {
+                 int crc_mode, const uintptr_t *in_id, const uintptr_t *out_id) {
     Workspace &w = s.w;
     size_t need = 0;
     for (int i = 0; i < nb; i++) need += host_need(blks[i], crc_mode);
@@ -981,6 +1022,7 @@ int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, PipeOp op, int algo, int nb, const jf
     const char *run_h = nullptr;
     char *run_d = nullptr;
     size_t run_n = 0;
+    uintptr_t run_id = 0;
     auto flush_in = [&]() -> int {
         if (run_n) {
             HIP_OK(hipMemcpyAsync(run_d, run_h, run_n, hipMemcpyHostToDevice, c->s_in));
@@ -995,10 +1037,15 @@ int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, PipeOp op, int algo, int nb, const jf
         off += align256(blks[i].len);
         if (blks[i].len) {
             const char *hs = (const char *)blks[i].src;
-            if (!(run_n && run_h + run_n == hs && run_d + run_n == buf) && (rc = flush_in())) return rc;
+            // one copy may only span one host allocation (a pinned pool, a
+            // bounce buffer): in_id names the allocation, 0 = the block's own
+            if (!(run_n && run_h + run_n == hs && run_d + run_n == buf && in_id[i] && in_id[i] == run_id) &&
+                (rc = flush_in()))
+                return rc;
             if (!run_n) {
                 run_h = hs;
                 run_d = buf;
+                run_id = in_id[i];
             }
             run_n += blks[i].len;
             if (align256(blks[i].len) != blks[i].len && (rc = flush_in())) return rc;
@@ -1024,6 +1071,7 @@ int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, PipeOp op, int algo, int nb, const jf
     char *oh = nullptr;
     const char *od = nullptr;
     size_t on = 0;
+    uintptr_t oid = 0;
     auto flush_out = [&]() -> int {
         if (on) {
             HIP_OK(hipMemcpyAsync(oh, od, on, hipMemcpyDeviceToHost, c->s_out));
@@ -1037,10 +1085,11 @@ int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, PipeOp op, int algo, int nb, const jf
         if (!blks[i].len) continue;
         char *hd = (char *)blks[i].dst;
         const char *dd = (const char *)dv[i].dst;
-        if (!(on && oh + on == hd && od + on == dd) && (rc = flush_out())) return rc;
+        if (!(on && oh + on == hd && od + on == dd && out_id[i] && out_id[i] == oid) && (rc = flush_out())) return rc;
         if (!on) {
             oh = hd;
             od = dd;
+            oid = out_id[i];
         }
         on += blks[i].len;
         if (align256(blks[i].len) != blks[i].len && (rc = flush_out())) return rc;
@@ -1220,8 +1269,12 @@ int run_host(jfsx_ctx *c, PipeOp op, int algo, int n, jfsx_blk *blks, int crc_mo
     const std::vector<std::pair<int, int>> groups = host_groups(c, n, blks, crc_mode);
     std::vector<jfsx_blk> dv(blks, blks + n), hv(blks, blks + n);
     std::vector<char> out_b(n, 0);  // block i's output sits in the bounce buffer
+    // the host allocation of each block's source / destination copy, for
+    // coalescing (pinned_base; the bounce buffer; 0: copy the block alone)
+    std::vector<uintptr_t> in_id(n, 0), out_id(n, 0);
     std::vector<PipeGroup> recs(groups.size());
     size_t issued = 0, done = 0, held = 0;  // groups enqueued / finished; bounce bytes held
+    size_t pinned_held = 0;                 // caller ranges pinned by groups in flight
     using SClock = std::chrono::steady_clock;
     auto us = [](SClock::time_point a, SClock::time_point b) {
         return (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(b - a).count();
@@ -1255,6 +1308,8 @@ int run_host(jfsx_ctx *c, PipeOp op, int algo, int n, jfsx_blk *blks, int crc_mo
             held -= r.bcap;
             r.bounce = nullptr;
         }
+        for (const void *q : r.pins) host_unpin(q);
+        r.pins.clear();
         if (r.rc && !rc) rc = r.rc;
     };
     for (size_t g = 0; g < groups.size() && !rc; g++) {
@@ -1272,6 +1327,19 @@ int run_host(jfsx_ctx *c, PipeOp op, int algo, int n, jfsx_blk *blks, int crc_mo
             if (!b.len) continue;
             in_pg[i - b0] = !host_pinned(b.src, b.len);
             out_b[i] = op != kPipeCrc && (b.dst == b.src ? in_pg[i - b0] : !host_pinned(b.dst, b.len));
+            // pin the caller's own pages for the call where the runtime
+            // allows it; what stays unpinned is bounced
+            if (in_pg[i - b0] && host_pin(b.src, b.len)) {
+                r.pins.push_back(b.src);
+                in_pg[i - b0] = 0;
+                if (b.dst == b.src) out_b[i] = 0;
+            }
+            if (out_b[i] && host_pin(b.dst, b.len)) {
+                r.pins.push_back(b.dst);
+                out_b[i] = 0;
+            }
+            in_id[i] = pinned_base(b.src);
+            out_id[i] = op == kPipeCrc ? 0 : pinned_base(b.dst);
             if (!in_pg[i - b0] && !out_b[i]) continue;
             boff[i - b0] = need;
             need += align256(b.len);
@@ -1280,6 +1348,8 @@ int run_host(jfsx_ctx *c, PipeOp op, int algo, int n, jfsx_blk *blks, int crc_mo
         c->ps_pin_us += us(p0, p1);
         if (need) {
             if (!(r.bounce = bounce_get(c, need, &r.bcap))) {
+                for (const void *q : r.pins) host_unpin(q);
+                r.pins.clear();
                 rc = JFSX_ENOMEM;
                 break;
             }
@@ -1293,9 +1363,13 @@ int run_host(jfsx_ctx *c, PipeOp op, int algo, int n, jfsx_blk *blks, int crc_mo
                     cp.push_back({q, (const char *)blks[i].src});
                     cl.push_back(blks[i].len);
                     hv[i].src = q;
+                    in_id[i] = (uintptr_t)r.bounce;
                     c->bounce.bytes_in += blks[i].len;
                 }
-                if (out_b[i]) hv[i].dst = q;
+                if (out_b[i]) {
+                    hv[i].dst = q;
+                    out_id[i] = (uintptr_t)r.bounce;
+                }
             }
             par_copy(cp, cl);
             c->ps_bin_us += us(p1, SClock::now());
@@ -1307,7 +1381,8 @@ int run_host(jfsx_ctx *c, PipeOp op, int algo, int n, jfsx_blk *blks, int crc_mo
         const SClock::time_point t1 = SClock::now();
         {
             std::lock_guard<std::mutex> lk(c->mu);
-            rc = pipe_enqueue(c, s, op, algo, b1 - b0, hv.data() + b0, dv.data() + b0, crc_mode);
+            rc = pipe_enqueue(c, s, op, algo, b1 - b0, hv.data() + b0, dv.data() + b0, crc_mode, in_id.data() + b0,
+                              out_id.data() + b0);
             if (rc) {
                 (void)hipStreamSynchronize(c->s_in);
                 (void)hipStreamSynchronize(c->stream);
@@ -1329,6 +1404,8 @@ int run_host(jfsx_ctx *c, PipeOp op, int algo, int n, jfsx_blk *blks, int crc_mo
                 held -= r.bcap;
                 r.bounce = nullptr;
             }
+            for (const void *q : r.pins) host_unpin(q);
+            r.pins.clear();
             break;
         }
         r.slot = &s;
@@ -1337,9 +1414,13 @@ int run_host(jfsx_ctx *c, PipeOp op, int algo, int n, jfsx_blk *blks, int crc_mo
         s.owner = &r;
         s.mu.unlock();
         issued++;
-        // a call holding bounce buffers keeps at most 4 groups / 1 GiB of them
-        // in flight
-        while (held && (issued - done > 4 || held > ((size_t)1 << 30))) finish(done++);
+        // a call holding bounce buffers or pinned caller pages keeps at most
+        // 4 groups / 1 GiB of them in flight
+        pinned_held += r.pins.size();
+        while ((held || pinned_held) && (issued - done > 4 || held > ((size_t)1 << 30))) {
+            pinned_held -= recs[done].pins.size();
+            finish(done++);
+        }
     }
     const SClock::time_point tw = SClock::now();
     while (done < issued) finish(done++);

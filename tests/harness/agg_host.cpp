@@ -71,6 +71,8 @@ char *bounce_acquire(jfsx_ctx *, size_t need, size_t *cap) {
     return (char *)malloc(need ? need : 1);
 }
 void bounce_release(jfsx_ctx *, char *p, size_t) { free(p); }
+bool host_pin(const void *, uint64_t) { return false; }
+void host_unpin(const void *) {}
 void bounce_count(jfsx_ctx *, uint64_t, uint64_t) {}
 }  // namespace jfsx
 
