@@ -586,13 +586,25 @@ int device_of(const void *p, uintptr_t *lo, uintptr_t *hi);
 }  // namespace jfsx
 
 namespace {
-// a persistent worker thread running one device's part of each batch
+// persistent worker threads running one device's parts of the batches: a
+// few per device (JFSX_MCTX_WORKERS, default 4), so concurrent callers of a
+// multi-device context overlap on every device, as they do on the first one,
+// whose part runs on each calling thread
+int mctx_workers() {
+    static const int v = [] {
+        const char *e = getenv("JFSX_MCTX_WORKERS");
+        const int t = e ? atoi(e) : 4;
+        return t >= 1 && t <= 64 ? t : 4;
+    }();
+    return v;
+}
+
 struct MWorker {
     std::mutex mu;
     std::condition_variable cv;
     std::deque<std::function<void()>> q;
     bool stop = false;
-    std::thread th;
+    std::vector<std::thread> ths;
 
     void run() {
         std::unique_lock<std::mutex> lk(mu);
@@ -776,7 +788,7 @@ int jfsx_mctx_open(uint64_t dev_mask, uint32_t flags, jfsx_mctx **out) {
         m->ws.emplace_back(new MWorker);
         if (k) {
             MWorker *w = m->ws.back().get();
-            w->th = std::thread([w] { w->run(); });
+            for (int t = 0; t < mctx_workers(); t++) w->ths.emplace_back([w] { w->run(); });
         }
     }
     *out = m;
@@ -786,13 +798,13 @@ int jfsx_mctx_open(uint64_t dev_mask, uint32_t flags, jfsx_mctx **out) {
 int jfsx_mctx_close(jfsx_mctx *m) {
     if (!m) return JFSX_EINVAL;
     for (auto &w : m->ws) {
-        if (!w->th.joinable()) continue;
+        if (w->ths.empty()) continue;
         {
             std::lock_guard<std::mutex> g(w->mu);
             w->stop = true;
             w->cv.notify_all();
         }
-        w->th.join();
+        for (std::thread &t : w->ths) t.join();
     }
     for (jfsx_ctx *c : m->cs) jfsx_ctx_close(c);
     delete m;

@@ -1634,7 +1634,10 @@ namespace jfsx {
 // The device that owns p, with the bounds [lo, hi) of the allocation it lies
 // in (so a caller can skip lookups for neighbouring pointers); -1 when p is
 // not device memory.  jfsx_alloc_device allocations are found in the
-// registry; other pointers are asked of the HIP runtime.
+// registry (an allocation must then be released with jfsx_free_device, which
+// drops its entry; one released with hipFree leaves a stale range behind);
+// other pointers are asked of the HIP runtime, which also reports the
+// allocation's bounds, so the caller's range cache covers their neighbours.
 int device_of(const void *p, uintptr_t *lo, uintptr_t *hi) {
     const uintptr_t a = (uintptr_t)p;
     {
@@ -1652,7 +1655,17 @@ int device_of(const void *p, uintptr_t *lo, uintptr_t *hi) {
     *lo = a;
     *hi = a + 1;
     hipPointerAttribute_t at;
-    if (p && hipPointerGetAttributes(&at, p) == hipSuccess && at.type == hipMemoryTypeDevice) return at.device;
+    if (p && hipPointerGetAttributes(&at, p) == hipSuccess && at.type == hipMemoryTypeDevice) {
+        hipDeviceptr_t base = nullptr;
+        size_t size = 0;
+        if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) == hipSuccess && base && size &&
+            (uintptr_t)base <= a && a < (uintptr_t)base + size) {
+            *lo = (uintptr_t)base;
+            *hi = (uintptr_t)base + size;
+        }
+        (void)hipGetLastError();
+        return at.device;
+    }
     (void)hipGetLastError();
     return -1;
 }

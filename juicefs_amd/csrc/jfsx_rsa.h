@@ -15,9 +15,9 @@
 //
 // Constant time with respect to the private key and the decrypted message,
 // as Go's rsa.DecryptOAEP is (crypto/internal/bigmod, subtle.ConstantTime*):
-// the exponentiation runs a fixed 4-bit window over the full 1024-bit
-// exponent length, always multiplies (digit 0 multiplies by the Montgomery
-// one), and reads its window table by a masked scan of all 16 entries; the
+// the exponentiation (mod_exp28) runs a fixed 3-bit window over the full
+// 1024-bit exponent length, always multiplies (digit 0 multiplies by the
+// Montgomery one), and reads its window table by a masked scan of all 8 rows; the
 // modular corrections, the CRT recombination and the OAEP checks select with
 // masks instead of branching.  Branches remain only on public values: the
 // ciphertext length and c >= n (Go rejects both before the private
@@ -544,6 +544,186 @@ JFSX_HD void mod_exp28(const uint32_t *x32, const uint32_t *e, const uint32_t *m
         }
     }
     from28(acc, out32);
+}
+
+// ---------------------------------------------------------------------------
+// The same exponentiation on a PAIR of lanes (the GPU kernel's form).  One
+// lane per exponentiation gives a batch of 16384 objects 32768 threads, 512
+// waves: one wave on half of the chip's 1024 SIMDs, each issuing the whole
+// ~4.4K-instruction product stream alone.  Two lanes per exponentiation split
+// every product by columns -- lane 0 holds columns 0..18, lane 1 columns
+// 19..37 (column 37 stays zero) -- so the batch is 1024 waves issuing about
+// half the instructions each.  Per row of the product the lanes exchange four
+// words: a_i from the lane holding it, the reduction multiplier m_i (lane 0
+// computes it from column 0), and the 64-bit column 19 that moves into lane 0
+// when the accumulator shifts down.  The final carry and borrow chains cross
+// the lanes once each.  Same arithmetic, bounds and schedule as mod_exp28
+// (one multiply site, masked table scan), so constant time in the exponent
+// the same way.
+//
+// X is the exchange between the two lanes: X::hi (0 or 1), X::lo(v) / X::up(v)
+// (v as held by lane 0 / lane 1, in both lanes), X::other(v) (the partner's
+// v), X::tracing() (the lane that records the test trace).  The GPU kernel
+// passes DPP moves; the CPU pin (tests/harness/rsa_host.cpp) runs the two
+// lanes as two threads meeting at a barrier per exchange.
+// ---------------------------------------------------------------------------
+constexpr int kPC = (kL28 + 1) / 2;  // columns per lane (2 kPC = 38 >= kL28)
+
+template <class X>
+JFSX_HD uint64_t lo64(const X &x, uint64_t v) {
+    return (uint64_t)x.lo((uint32_t)v) | (uint64_t)x.lo((uint32_t)(v >> 32)) << 32;
+}
+template <class X>
+JFSX_HD uint64_t other64(const X &x, uint64_t v) {
+    return (uint64_t)x.other((uint32_t)v) | (uint64_t)x.other((uint32_t)(v >> 32)) << 32;
+}
+
+// this lane's kPC limbs of a 28-bit-limb value f[0..kL28)
+template <class X>
+JFSX_HD void pair_pick(const X &x, const uint32_t *f, uint32_t *y) {
+    const uint32_t up = 0u - x.hi;
+#pragma unroll
+    for (int j = 0; j < kPC; j++) y[j] = (f[j] & ~up) | ((kPC + j < kL28 ? f[kPC + j] : 0u) & up);
+}
+
+// out = a b R'^-1 mod m on the pair: a, b, m, out are this lane's kPC limbs
+// (normalized); minv = -m^-1 mod 2^28
+template <class X>
+JFSX_HD void mont_mul28_pair(const X &x, const uint32_t *a, const uint32_t *b, const uint32_t *m, uint32_t minv,
+                             uint32_t *out) {
+    if (x.tracing()) JFSX_RSA_TRACE('M', 2);
+    const uint64_t low = (uint64_t)0 - (uint64_t)(x.hi ^ 1u);  // all-ones in lane 0
+    uint64_t acc[kPC];
+#pragma unroll
+    for (int j = 0; j < kPC; j++) acc[j] = 0;
+    // one row: + a_i b, + m_i m (m_i from lane 0's column 0), then the
+    // columns move down one: column 0 leaves (its carry joins column 1) and
+    // lane 1's first column becomes lane 0's last
+    auto row = [&](uint32_t ai) {
+#pragma unroll
+        for (int j = 0; j < kPC; j++) acc[j] += (uint64_t)ai * b[j];
+        const uint32_t mi = x.lo(((uint32_t)acc[0] * minv) & kM28);
+#pragma unroll
+        for (int j = 0; j < kPC; j++) acc[j] += (uint64_t)mi * m[j];
+        const uint64_t c = acc[0] >> 28, s = other64(x, acc[0]);
+#pragma unroll
+        for (int j = 0; j < kPC - 1; j++) acc[j] = acc[j + 1];
+        acc[kPC - 1] = s & low;
+        acc[0] += c & low;
+    };
+#pragma unroll
+    for (int r = 0; r < kPC; r++) row(x.lo(a[r]));
+#pragma unroll
+    for (int r = 0; r < kL28 - kPC; r++) row(x.up(a[r]));
+    // normalize: each lane on its own, then lane 0's carry through lane 1
+    uint32_t t[kPC], d[kPC];
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < kPC; j++) {
+        c += acc[j];
+        t[j] = (uint32_t)c & kM28;
+        c >>= 28;
+    }
+    c = lo64(x, c) & ~low;
+#pragma unroll
+    for (int j = 0; j < kPC; j++) {
+        c += t[j];
+        t[j] = (uint32_t)c & kM28;
+        c >>= 28;
+    }
+    // t - m: lane 0's borrow first, then lane 1's chain from it
+    uint32_t br = 0;
+#pragma unroll
+    for (int j = 0; j < kPC; j++) br = (t[j] - m[j] - br) >> 31;
+    br = x.lo(br) & (0u - x.hi);
+#pragma unroll
+    for (int j = 0; j < kPC; j++) {
+        const uint32_t v = t[j] - m[j] - br;
+        d[j] = v & kM28;
+        br = v >> 31;
+    }
+    const uint32_t keep = 0u - x.up(br);  // t < m
+#pragma unroll
+    for (int j = 0; j < kPC; j++) out[j] = (t[j] & keep) | (d[j] & ~keep);
+}
+
+// x^e mod m (x < m; 32-bit limbs in, out32 in both lanes), constant time in e:
+// mod_exp28's schedule on the pair
+template <class X>
+JFSX_HD void mod_exp28_pair(const X &x, const uint32_t *x32, const uint32_t *e, const uint32_t *m32,
+                            uint32_t minv32, const uint32_t *r2_32, uint32_t *out32) {
+    uint32_t m[kPC], xv[kPC], r2[kPC];
+    {
+        uint32_t f[kL28];
+        to28(m32, f);
+        pair_pick(x, f, m);
+        to28(x32, f);
+        pair_pick(x, f, xv);
+        to28(r2_32, f);
+        pair_pick(x, f, r2);
+    }
+    const uint32_t minv = minv32 & kM28, one0 = x.hi ^ 1u;  // the Montgomery 1's low limb sits in lane 0
+    uint32_t tab[kWTab][kPC];
+    uint32_t acc[kPC], b[kPC];
+    for (int w = 0; w < kWTab; w++)
+        for (int j = 0; j < kPC; j++) tab[w][j] = 0;
+    constexpr int kPer = kWBits + 1, kMain = kWTab + kPer * kWDigits;
+#pragma unroll 1
+    for (int st = 0; st <= kMain; st++) {
+        if (st == 0) {
+#pragma unroll
+            for (int j = 0; j < kPC; j++) acc[j] = r2[j], b[j] = j == 0 ? one0 : 0u;
+        } else if (st == 1) {
+#pragma unroll
+            for (int j = 0; j < kPC; j++) acc[j] = xv[j], b[j] = r2[j];
+        } else if (st < kWTab) {
+#pragma unroll
+            for (int j = 0; j < kPC; j++) b[j] = tab[1][j];
+        } else if (st < kMain) {
+            const int r = st - kWTab;
+            if (r % kPer < kWBits) {
+#pragma unroll
+                for (int j = 0; j < kPC; j++) b[j] = acc[j];
+            } else {
+                uint32_t idx = w_digit(e, kWDigits - 1 - r / kPer);
+                JFSX_RSA_OPAQUE(idx);
+#pragma unroll
+                for (int j = 0; j < kPC; j++) b[j] = 0;
+#pragma unroll
+                for (uint32_t w = 0; w < (uint32_t)kWTab; w++) {
+                    uint32_t msk = ~ct_nz(w ^ idx);
+                    JFSX_RSA_OPAQUE(msk);
+                    if (x.tracing()) JFSX_RSA_TRACE('S', w);
+#pragma unroll
+                    for (int j = 0; j < kPC; j++) b[j] |= tab[w][j] & msk;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < kPC; j++) b[j] = j == 0 ? one0 : 0u;
+        }
+        mont_mul28_pair(x, acc, b, m, minv, acc);
+        if (st < kWTab) {
+#pragma unroll
+            for (int w = 0; w < kWTab; w++)
+#pragma unroll
+                for (int j = 0; j < kPC; j++) tab[w][j] = st == w ? acc[j] : tab[w][j];
+            if (st == kWTab - 1) {
+#pragma unroll
+                for (int j = 0; j < kPC; j++) acc[j] = tab[0][j];
+            }
+        }
+    }
+    // both halves of the result in both lanes, back to 32-bit limbs
+    uint32_t f[2 * kPC];
+    const uint32_t up = 0u - x.hi;
+#pragma unroll
+    for (int j = 0; j < kPC; j++) {
+        const uint32_t o = x.other(acc[j]);
+        f[j] = (acc[j] & ~up) | (o & up);
+        f[kPC + j] = (o & ~up) | (acc[j] & up);
+    }
+    from28(f, out32);
 }
 
 // One whole unwrap on one thread (the CPU pin; the GPU splits it into the

@@ -2,6 +2,9 @@
 // RSA-OAEP unwrap arithmetic, checked by tests/test_rsa.py against libcrypto.
 #include <stdint.h>
 #include <string.h>
+
+#include <atomic>
+#include <thread>
 // the sequence of Montgomery products and window-table reads, hashed
 static uint64_t g_trace = 1469598103934665603ull, g_ops = 0;
 #define JFSX_RSA_TRACE(tag, v) \
@@ -37,6 +40,62 @@ uint64_t rsa_exp_trace(const uint8_t *m_be, const uint8_t *e_be, const uint8_t *
     g_ops = 0;
     mod_exp28(x, e, m, mont_inv32(m[0]), r2, r);
     to_be(r, kLimbs, out_be, 4 * kLimbs);
+    *ops = g_ops;
+    return g_trace;
+}
+
+// mod_exp28_pair's lane exchange on the CPU: the two lanes are two threads
+// that meet at a barrier for every exchanged word (SIMT lock step)
+struct PairShared {
+    std::atomic<uint32_t> gen{0};
+    std::atomic<int> cnt{0};
+    uint32_t slot[2];
+};
+struct PairThreads {
+    uint32_t hi;
+    PairShared *sh;
+    bool tracing() const { return hi == 0; }
+    void barrier() const {
+        const uint32_t g = sh->gen.load(std::memory_order_acquire);
+        if (sh->cnt.fetch_add(1, std::memory_order_acq_rel) == 1) {
+            sh->cnt.store(0, std::memory_order_relaxed);
+            sh->gen.store(g + 1, std::memory_order_release);
+        } else {
+            for (int k = 0; sh->gen.load(std::memory_order_acquire) == g; k++)
+                if (k > 64) std::this_thread::yield();
+        }
+    }
+    uint32_t xchg(uint32_t v, uint32_t from) const {
+        sh->slot[hi] = v;
+        barrier();
+        const uint32_t r = sh->slot[from];
+        barrier();
+        return r;
+    }
+    uint32_t lo(uint32_t v) const { return xchg(v, 0); }
+    uint32_t up(uint32_t v) const { return xchg(v, 1); }
+    uint32_t other(uint32_t v) const { return xchg(v, hi ^ 1u); }
+};
+
+// rsa_exp_trace on mod_exp28_pair (the GPU kernel's two-lane form); *same =
+// 1 when both lanes returned the same result
+uint64_t rsa_exp_pair_trace(const uint8_t *m_be, const uint8_t *e_be, const uint8_t *x_be, uint8_t *out_be,
+                            uint64_t *ops, int *same) {
+    using namespace jfsx_rsa;
+    uint32_t m[kLimbs], e[kLimbs], x[kLimbs], r2[kLimbs], r[2][kLimbs];
+    from_be(m_be, 4 * kLimbs, m, kLimbs);
+    from_be(e_be, 4 * kLimbs, e, kLimbs);
+    from_be(x_be, 4 * kLimbs, x, kLimbs);
+    mont_r2(m, r2, 2 * 28 * kL28);
+    g_trace = 1469598103934665603ull;
+    g_ops = 0;
+    PairShared sh;
+    auto lane = [&](uint32_t hi) { mod_exp28_pair(PairThreads{hi, &sh}, x, e, m, mont_inv32(m[0]), r2, r[hi]); };
+    std::thread t1(lane, 1u);
+    lane(0u);
+    t1.join();
+    *same = memcmp(r[0], r[1], sizeof(r[0])) == 0;
+    to_be(r[0], kLimbs, out_be, 4 * kLimbs);
     *ops = g_ops;
     return g_trace;
 }

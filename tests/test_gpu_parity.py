@@ -273,8 +273,11 @@ def test_large_tasks_few_slots_vs_oracle(eng, algo):
 
 @pytest.mark.parametrize("algo", [E.AES256GCM, E.CHACHA20P1305])
 def test_host_ingest_pipeline_ring(eng, algo):
-    """MEM_HOST batches streamed through the 3-slot ring (1 MiB slots -> many
-    groups), seal + CRC and open + verify, one tag failure wiped on Open."""
+    """MEM_HOST batches streamed through the context's persistent 8-slot host
+    pipeline (kPipe slots shared by every caller; descriptors pulled into the
+    slot by a kernel, results in its pinned mirror), with 1 MiB slots so one
+    call is many groups that wrap the ring: seal + CRC and open + verify, one
+    tag failure wiped on Open."""
     eng.set_slot_bytes(1 << 20)
     try:
         lens = [300000, 1 << 20, 5, 0, 777777, 2 << 20, 65536, 123457, 1 << 19, 4097]

@@ -18,7 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 @pytest.fixture(scope="module")
 def rsa(tmp_path_factory):
     out = str(tmp_path_factory.mktemp("rsa") / "rsa_host.so")
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", out,
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-pthread", "-o", out,
                            os.path.join(HERE, "harness", "rsa_host.cpp")])
     return ctypes.CDLL(out)
 
@@ -107,6 +107,33 @@ def test_exponentiation_schedule_is_independent_of_the_exponent(rsa, keypair):
     (_, nops), = traces
     # table (8), 342 digits x (3 sq + 1 mul), exit; 8 reads per digit
     assert nops == 8 + 342 * 4 + 1 + 342 * 8
+
+
+def test_pair_exponentiation_matches_pow_with_one_trace(rsa, keypair):
+    """mod_exp28_pair, the GPU kernel's form (each Montgomery product split by
+    columns over two lanes that exchange words per row), run on the CPU as two
+    threads in lock step: every result equals pow(), both lanes return it,
+    and the operation trace is one and the same for every exponent and base,
+    as for mod_exp28."""
+    _, _, comps = keypair
+    for m in (comps[0], comps[1]):
+        mi = int.from_bytes(m, "big")
+        traces = set()
+        cases = [(int.from_bytes(os.urandom(127), "big") % mi, e)
+                 for e in (int.from_bytes(comps[2], "big"), 3, (1 << 1024) - 1, 0, 0x10001)]
+        cases += [(xe, int.from_bytes(comps[3], "big")) for xe in (0, 1, mi - 1)]
+        for xv, e in cases:
+            out = ctypes.create_string_buffer(128)
+            ops, same = ctypes.c_uint64(), ctypes.c_int()
+            rsa.rsa_exp_pair_trace.restype = ctypes.c_uint64
+            h = rsa.rsa_exp_pair_trace(m, e.to_bytes(128, "big"), xv.to_bytes(128, "big"), out,
+                                       ctypes.byref(ops), ctypes.byref(same))
+            assert same.value == 1
+            assert int.from_bytes(out.raw, "big") == pow(xv, e, mi), (xv, e)
+            traces.add((h, ops.value))
+        assert len(traces) == 1, traces
+        (_, nops), = traces
+        assert nops == 8 + 342 * 4 + 1 + 342 * 8
 
 
 def _oaep_encode(msg, seed, label=b"keys", k=256, db_patch=None):
