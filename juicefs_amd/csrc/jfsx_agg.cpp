@@ -192,6 +192,18 @@ struct Req {
 
 }  // namespace jfsx
 
+// A pinned staging arena shared by the pageable per-object requests of one
+// aggregator (see Staged): callers take consecutive 256-byte-aligned slices,
+// so the blocks of one batch usually sit side by side in one allocation and
+// the engine moves them with one H2D and one D2H copy instead of one per block
+// (large copies run nearer the link's rate than 4 MiB ones).
+struct AggArena {
+    char *base;
+    size_t cap, used;
+    int refs;   // slices still held by requests
+    bool open;  // the arena slices are taken from now
+};
+
 using jfsx::Req;
 using jfsx::kSeal;
 using jfsx::kOpen;
@@ -216,6 +228,10 @@ struct jfsx_agg {
     uint64_t calls = 0, batches = 0, blocks = 0;
     std::vector<uint64_t> dev_batches;
     std::vector<std::thread> ths;
+    // staging arenas (arena_reserve / arena_release)
+    std::mutex ar_mu;
+    AggArena *ar_cur = nullptr;
+    std::vector<AggArena *> ar_free, ar_all;
 
     int call(jfsx_ctx *c, const std::vector<Req *> &b, size_t i0, size_t n, std::vector<jfsx_blk> &blks,
              std::vector<jfsx_range> &rng, std::vector<jfsx_zblk> &zs) {
@@ -363,19 +379,77 @@ namespace {
 // bounce buffer of the engine before the request is queued, and its output
 // copied out of it after the request completes.  So max-uploads callers copy
 // in parallel, and the dispatchers, which run the batches, never copy.
+// Blocks up to a quarter of an arena take a slice of the aggregator's shared
+// arena (JFSX_AGG_ARENA_MB, default 64; 0: a bounce buffer of their own, as
+// larger blocks always do).
+size_t arena_bytes() {
+    static const size_t v = [] {
+        const char *e = getenv("JFSX_AGG_ARENA_MB");
+        return (size_t)(e ? atoll(e) : 64) << 20;
+    }();
+    return v;
+}
+
+// a slice of need bytes of the open arena (a fresh one when it is full)
+char *arena_reserve(jfsx_agg *a, size_t need, AggArena **out) {
+    std::lock_guard<std::mutex> g(a->ar_mu);
+    AggArena *cur = a->ar_cur;
+    if (cur && !cur->refs) cur->used = 0;  // nothing of it in flight: start over at its base
+    if (!cur || cur->used + need > cur->cap) {
+        if (cur) {
+            cur->open = false;
+            if (!cur->refs) a->ar_free.push_back(cur);
+        }
+        a->ar_cur = cur = nullptr;
+        if (!a->ar_free.empty()) {
+            cur = a->ar_free.back();
+            a->ar_free.pop_back();
+        } else {
+            size_t cap = 0;
+            char *b = jfsx::bounce_acquire(a->cs[0], arena_bytes(), &cap);
+            if (!b) return nullptr;
+            cur = new (std::nothrow) AggArena{b, cap, 0, 0, false};
+            if (!cur) {
+                jfsx::bounce_release(a->cs[0], b, cap);
+                return nullptr;
+            }
+            a->ar_all.push_back(cur);
+        }
+        cur->used = 0;
+        cur->open = true;
+        a->ar_cur = cur;
+    }
+    char *p = cur->base + cur->used;
+    cur->used += need;
+    cur->refs++;
+    *out = cur;
+    return p;
+}
+
+void arena_release(jfsx_agg *a, AggArena *ar) {
+    std::lock_guard<std::mutex> g(a->ar_mu);
+    if (--ar->refs == 0 && !ar->open) a->ar_free.push_back(ar);
+}
+
 struct Staged {
+    jfsx_agg *a = nullptr;
     jfsx_ctx *c = nullptr;
     char *p = nullptr;
     size_t cap = 0;
+    AggArena *ar = nullptr;                   // p is a slice of this arena
     const void *pin[2] = {nullptr, nullptr};  // caller ranges pinned for the call
     ~Staged() {
-        if (p) jfsx::bounce_release(c, p, cap);
+        if (ar) arena_release(a, ar);
+        else if (p) jfsx::bounce_release(c, p, cap);
         for (const void *q : pin)
             if (q) jfsx::host_unpin(q);
     }
-    int get(jfsx_ctx *ctx, uint64_t len) {
-        c = ctx;
-        p = jfsx::bounce_acquire(c, (size_t)((len + 255) & ~(uint64_t)255), &cap);
+    int get(jfsx_agg *agg, uint64_t len) {
+        a = agg;
+        c = agg->cs[0];
+        const size_t need = (size_t)((len + 255) & ~(uint64_t)255);
+        if (need <= arena_bytes() / 4 && (p = arena_reserve(agg, need, &ar))) return 0;
+        p = jfsx::bounce_acquire(c, need, &cap);
         return p ? 0 : JFSX_ENOMEM;
     }
 };
@@ -438,6 +512,10 @@ int jfsx_agg_free(jfsx_agg *a) {
         a->cv_work.notify_all();
     }
     for (std::thread &t : a->ths) t.join();  // requests already queued run first
+    for (AggArena *ar : a->ar_all) {  // no request holds a slice any more
+        jfsx::bounce_release(a->cs[0], ar->base, ar->cap);
+        delete ar;
+    }
     delete a;
     return 0;
 }
@@ -512,7 +590,7 @@ int agg_aead(jfsx_agg *a, int op, int algo, jfsx_blk *blk, int crc_mode, int mem
         Req r{op, algo, crc_mode, mem, blk, nullptr, nullptr, len};
         return a->submit(r);
     }
-    if (st.get(a->cs[0], len)) return JFSX_ENOMEM;
+    if (st.get(a, len)) return JFSX_ENOMEM;
     jfsx_blk w = *blk;
     if (in_pg) {
         memcpy(st.p, blk->src, len);
@@ -548,7 +626,7 @@ int agg_crc(jfsx_agg *a, jfsx_range *range, int mode, int mem) {
         Req r{kCrc, 0, mode, mem, nullptr, range, nullptr, len};
         return a->submit(r);
     }
-    if (st.get(a->cs[0], len)) return JFSX_ENOMEM;
+    if (st.get(a, len)) return JFSX_ENOMEM;
     memcpy(st.p, range->data, len);
     jfsx_range w = *range;
     w.data = st.p;

@@ -1,0 +1,1 @@
+JFSX_PIPE_STATS=1 JFSX_AGG_ARENA_MB=0 bench.py --mode agg --threads 20 --steps 10 --no-cpu --buffers heap --agg-crc seg --agg-op open

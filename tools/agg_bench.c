@@ -5,7 +5,7 @@
  * Reports GB/s of plaintext for the aggregator and for direct one-block
  * jfsx_seal_batch calls, to separate the engine from the Python harness.
  *
- * usage: agg_bench [threads=20] [blocks=512] [passes=4] [max_mb=16] [window_us=500] [numa=0] [layout=0]
+ * usage: agg_bench [threads=20] [blocks=512] [passes=4] [max_mb=16] [window_us=500] [numa=0] [layout=0] [heap=0]
  * numa=1 binds the pinned blocks to the GPU's NUMA node and runs the threads
  * on that node's CPUs (as bench.py's host ingest does).
  * layout=0: thread t seals blocks t, t + T, ... of one pinned arena, so the
@@ -13,6 +13,10 @@
  * one pinned pool in order); layout=1: thread t owns a contiguous range of
  * blocks, so no two blocks in flight are adjacent (every caller with its own
  * buffers).
+ * heap=1: the blocks live in ordinary pageable memory (malloc, as a Go-heap
+ * slice), so the engine stages them through its pinned bounce buffers.
+ * The aggregator run also reports the process's CPU time (getrusage) per GB
+ * and the cores it kept busy: the host cost of the GPU path without Python.
  * build: cc -O2 -o tools/agg_bench tools/agg_bench.c -Iinclude -Ljuicefs_amd -ljfsx -lpthread \
  *        -Wl,-rpath,'$ORIGIN/../juicefs_amd' */
 #define _GNU_SOURCE
@@ -21,6 +25,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/resource.h>
 #include <time.h>
 
 #include "jfsx.h"
@@ -62,6 +67,12 @@ static void *worker(void *vp) {
     return NULL;
 }
 
+static double cpu_s(void) {
+    struct rusage ru;
+    getrusage(RUSAGE_SELF, &ru);
+    return ru.ru_utime.tv_sec + ru.ru_utime.tv_usec * 1e-6 + ru.ru_stime.tv_sec + ru.ru_stime.tv_usec * 1e-6;
+}
+
 static double run(void) {
     pthread_t th[256];
     const double t0 = now();
@@ -79,6 +90,7 @@ int main(int argc, char **argv) {
     const uint32_t window = argc > 5 ? (uint32_t)atoi(argv[5]) : 500;
     const int numa = argc > 6 ? atoi(argv[6]) : 0;
     layout = argc > 7 ? atoi(argv[7]) : 0;
+    const int heap = argc > 8 ? atoi(argv[8]) : 0;
     int node = -1;
     if (numa && jfsx_device_numa_node(0, &node) == 0 && node >= 0) {
         char path[96], list[4096];
@@ -101,7 +113,13 @@ int main(int argc, char **argv) {
         if (f) fclose(f);
     }
     if (jfsx_ctx_open(0, 0, &ctx)) return 1;
-    if (node >= 0) {
+    if (heap) {
+        hin = aligned_alloc(4096, NB * L);
+        hout = aligned_alloc(4096, NB * L);
+        hcrc = aligned_alloc(4096, NB * 512);
+        if (!hin || !hout || !hcrc) return 1;
+        memset(hout, 0, NB * L);
+    } else if (node >= 0) {
         if (jfsx_alloc_pinned_node(ctx, NB * L, node, (void **)&hin) ||
             jfsx_alloc_pinned_node(ctx, NB * L, node, (void **)&hout) ||
             jfsx_alloc_pinned_node(ctx, NB * 512, node, (void **)&hcrc))
@@ -123,17 +141,27 @@ int main(int argc, char **argv) {
     PASSES = 1;
     run();
     PASSES = passes;
+    const double c0 = cpu_s(), w0 = now();
     const double aggr = run();
+    const double cpu = cpu_s() - c0, wall = now() - w0;
+    const double gb = aggr * wall;
     uint64_t calls, batches, blocks;
     jfsx_agg_stats(agg, &calls, &batches, &blocks);
     printf("{\"threads\": %d, \"blocks\": %d, \"passes\": %d, \"max_mb\": %llu, \"window_us\": %u, "
-           "\"numa_node\": %d, \"layout\": %d, \"direct_GBs\": %.2f, \"agg_GBs\": %.2f, \"agg_batches\": %llu, \"agg_calls\": %llu}\n",
+           "\"numa_node\": %d, \"layout\": %d, \"direct_GBs\": %.2f, \"agg_GBs\": %.2f, \"agg_batches\": %llu, \"agg_calls\": %llu, "
+           "\"heap\": %d, \"agg_cpu_s_per_GB\": %.4f, \"agg_cores_busy\": %.2f}\n",
            T, NB, passes, (unsigned long long)max_mb, window, node, layout, direct, aggr, (unsigned long long)batches,
-           (unsigned long long)calls);
+           (unsigned long long)calls, heap, cpu / gb, cpu / wall);
     jfsx_agg_free(agg);
-    jfsx_free_pinned(ctx, hin);
-    jfsx_free_pinned(ctx, hout);
-    jfsx_free_pinned(ctx, hcrc);
+    if (heap) {
+        free(hin);
+        free(hout);
+        free(hcrc);
+    } else {
+        jfsx_free_pinned(ctx, hin);
+        jfsx_free_pinned(ctx, hout);
+        jfsx_free_pinned(ctx, hcrc);
+    }
     jfsx_ctx_close(ctx);
     return 0;
 }
