@@ -955,6 +955,32 @@ int enqueue_crc(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEven
     return 0;
 }
 
+// How a host thread waits for a pipeline slot's D2H (JFSX_WAIT_POLL_US): by
+// default it queries the event and sleeps 20 us between queries; 0 =
+// hipEventSynchronize, the runtime's wait, which keeps a core busy for the
+// whole wait (with or without hipEventBlockingSync).  A group's wait is about
+// a millisecond and several dispatchers wait at once: 20 per-object callers on
+// pinned blocks kept 5.0 cores busy with the runtime's wait and 1.25 with the
+// sleeping one, at the same 41.6-41.9 GB/s (profiles/r6/wait_poll/).
+int wait_poll_us() {
+    static const int v = [] {
+        const char *e = getenv("JFSX_WAIT_POLL_US");
+        return e ? atoi(e) : 20;
+    }();
+    return v;
+}
+
+hipError_t wait_event(hipEvent_t ev) {
+    const int us = wait_poll_us();
+    if (us <= 0) return hipEventSynchronize(ev);
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e != hipErrorNotReady) return e;
+        (void)hipGetLastError();  // hipErrorNotReady is not a failure
+        std::this_thread::sleep_for(std::chrono::microseconds(us));
+    }
+}
+
 // Collect the group in flight in slot s (s.mu held; called by the group's own
 // caller, or by any caller that needs the slot next): wait for its D2H and
 // write its per-block results into the owner's records.  Only results: the
@@ -963,7 +989,7 @@ void pipe_collect(jfsx_ctx *c, PipeSlot &s) {
     PipeGroup *g = s.owner;
     if (!g) return;
     s.owner = nullptr;
-    const hipError_t e = hipEventSynchronize(s.ev_out);
+    const hipError_t e = wait_event(s.ev_out);
     if (e != hipSuccess) {
         note_hip_error(e, __FILE__, __LINE__, "hipEventSynchronize(pipeline slot)");
         g->rc = JFSX_EIO;
