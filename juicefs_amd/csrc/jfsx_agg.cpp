@@ -332,16 +332,20 @@ struct jfsx_agg {
             if (!q.empty()) cv_work.notify_all();  // the rest may go to an idle dispatcher now
             lk.unlock();
             execute(cs[k], b);
+            // the counters first: a caller that has returned sees its batch
+            // counted (jfsx_agg_stats right after the last call returns)
+            lk.lock();
+            held--;
+            batches++;
+            dev_batches[dev[k]]++;
+            blocks += b.size();
+            lk.unlock();
             for (Req *r : b) {
                 std::lock_guard<std::mutex> g(r->m);  // r may be gone once fin is seen: notify under its lock
                 r->fin = true;
                 r->cv.notify_one();
             }
             lk.lock();
-            held--;
-            batches++;
-            dev_batches[dev[k]]++;
-            blocks += b.size();
             if (!q.empty()) cv_work.notify_all();
         }
     }
@@ -390,40 +394,47 @@ size_t arena_bytes() {
     return v;
 }
 
-// a slice of need bytes of the open arena (a fresh one when it is full)
+// a slice of need bytes of the open arena (a fresh one when it is full).  A
+// new arena is allocated outside the lock (pinned allocation takes
+// milliseconds), so other callers keep reserving from the open one meanwhile.
 char *arena_reserve(jfsx_agg *a, size_t need, AggArena **out) {
-    std::lock_guard<std::mutex> g(a->ar_mu);
-    AggArena *cur = a->ar_cur;
-    if (cur && !cur->refs) cur->used = 0;  // nothing of it in flight: start over at its base
-    if (!cur || cur->used + need > cur->cap) {
-        if (cur) {
-            cur->open = false;
-            if (!cur->refs) a->ar_free.push_back(cur);
-        }
-        a->ar_cur = cur = nullptr;
-        if (!a->ar_free.empty()) {
-            cur = a->ar_free.back();
-            a->ar_free.pop_back();
-        } else {
-            size_t cap = 0;
-            char *b = jfsx::bounce_acquire(a->cs[0], arena_bytes(), &cap);
-            if (!b) return nullptr;
-            cur = new (std::nothrow) AggArena{b, cap, 0, 0, false};
-            if (!cur) {
-                jfsx::bounce_release(a->cs[0], b, cap);
-                return nullptr;
+    for (;;) {
+        {
+            std::lock_guard<std::mutex> g(a->ar_mu);
+            AggArena *cur = a->ar_cur;
+            if (cur && !cur->refs) cur->used = 0;  // nothing of it in flight: start over at its base
+            if (cur && cur->used + need > cur->cap) {  // full: close it
+                cur->open = false;
+                if (!cur->refs) a->ar_free.push_back(cur);
+                a->ar_cur = cur = nullptr;
             }
-            a->ar_all.push_back(cur);
+            if (!cur && !a->ar_free.empty()) {
+                cur = a->ar_free.back();
+                a->ar_free.pop_back();
+                cur->used = 0;
+                cur->open = true;
+                a->ar_cur = cur;
+            }
+            if (cur) {
+                char *p = cur->base + cur->used;
+                cur->used += need;
+                cur->refs++;
+                *out = cur;
+                return p;
+            }
         }
-        cur->used = 0;
-        cur->open = true;
-        a->ar_cur = cur;
+        size_t cap = 0;
+        char *base = jfsx::bounce_acquire(a->cs[0], arena_bytes(), &cap);
+        if (!base) return nullptr;
+        AggArena *fresh = new (std::nothrow) AggArena{base, cap, 0, 0, false};
+        if (!fresh) {
+            jfsx::bounce_release(a->cs[0], base, cap);
+            return nullptr;
+        }
+        std::lock_guard<std::mutex> g(a->ar_mu);
+        a->ar_all.push_back(fresh);
+        a->ar_free.push_back(fresh);  // the next pass takes it (or one another caller freed)
     }
-    char *p = cur->base + cur->used;
-    cur->used += need;
-    cur->refs++;
-    *out = cur;
-    return p;
 }
 
 void arena_release(jfsx_agg *a, AggArena *ar) {
