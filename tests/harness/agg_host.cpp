@@ -78,6 +78,15 @@ void bounce_count(jfsx_ctx *, uint64_t, uint64_t) {}
 
 extern "C" {
 
+// fake bytes of a host block with both pointers set: dst[j] = src[j] ^ key[j % 32]
+// ^ 0x5A (its own inverse), so a test sees whether the staged copy reached
+// the transform and its output came back to the caller's buffer
+void fake_bytes(jfsx_blk &b) {
+    const uint8_t *s = (const uint8_t *)b.src;
+    uint8_t *d = (uint8_t *)b.dst;
+    for (uint64_t j = 0; j < b.len; j++) d[j] = s[j] ^ b.key[j & 31] ^ 0x5A;
+}
+
 // fake transform: tag[i] = key[i] ^ (len >> 8*(i&7)); reserved != 0 -> EINVAL
 int jfsx_seal_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *b, int crc_mode, int mem) {
     for (int i = 0; i < n; i++)
@@ -88,6 +97,7 @@ int jfsx_seal_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *b, int crc_mode, int
     for (int i = 0; i < n; i++) {
         for (int k = 0; k < 16; k++) b[i].tag[k] = b[i].key[k] ^ (uint8_t)(b[i].len >> (8 * (k & 7))) ^ (uint8_t)algo;
         b[i].status = JFSX_OK;
+        if (mem == JFSX_MEM_HOST && b[i].src && b[i].dst) fake_bytes(b[i]);
     }
     return 0;
 }
@@ -101,6 +111,10 @@ int jfsx_open_batch(jfsx_ctx *c, int algo, int n, jfsx_blk *b, int crc_mode, int
         for (int k = 0; k < 16; k++)
             ok &= b[i].tag[k] == (uint8_t)(b[i].key[k] ^ (uint8_t)(b[i].len >> (8 * (k & 7))) ^ (uint8_t)algo);
         b[i].status = ok ? JFSX_OK : JFSX_ETAG;
+        if (mem == JFSX_MEM_HOST && b[i].src && b[i].dst) {
+            if (ok) fake_bytes(b[i]);
+            else memset(b[i].dst, 0, b[i].len);  // the engine releases nothing of a failed block
+        }
     }
     return 0;
 }
@@ -183,6 +197,13 @@ void harness_reset(int sleep_us) {
 }
 
 void harness_set_ndev(int n) { h_ndev = n; }
+// mark [lo, hi) pageable (host_pinned() false there; 0, 0: none); bounce
+// buffers (and staging arenas) allocated so far
+void harness_pageable(uintptr_t lo, uintptr_t hi) {
+    jfsx::h_pg_lo = lo;
+    jfsx::h_pg_hi = hi;
+}
+int harness_bounces(void) { return jfsx::h_bounces.load(); }
 int harness_open_ctx(void) { return h_open_ctx; }
 
 // per batch: device index of its context and the len of its first block

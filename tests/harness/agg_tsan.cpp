@@ -97,6 +97,41 @@ int main() {
         for (auto &th : ts) th.join();
         harness_close(c);
     }
+    // 4) pageable per-object Seal / Open: 24 callers staging through the
+    // shared arenas (slices reserved, copied, released from many threads)
+    {
+        const int T = 24, PER = 8;
+        const uint64_t L = 20000;
+        std::vector<uint8_t> buf((size_t)2 * T * PER * L);
+        for (size_t i = 0; i < buf.size() / 2; i++) buf[i] = (uint8_t)(i * 131);
+        harness_pageable((uintptr_t)buf.data(), (uintptr_t)buf.data() + buf.size());
+        jfsx_agg *a = nullptr;
+        if (jfsx_agg_new((jfsx_ctx *)0x1000, 0, 1 << 20, 200, &a)) return 1;
+        std::vector<std::thread> ts;
+        for (int t = 0; t < T; t++)
+            ts.emplace_back([&, t] {
+                for (int j = 0; j < PER; j++) {
+                    const size_t i = (size_t)t * PER + j;
+                    uint8_t *src = buf.data() + i * L, *obj = buf.data() + (size_t)T * PER * L + i * L;
+                    jfsx_blk b{};
+                    for (int k = 0; k < 32; k++) b.key[k] = (uint8_t)(i + k);
+                    b.src = src;
+                    b.dst = obj;
+                    b.len = L;
+                    if (jfsx_agg_seal(a, 0, &b, 0, JFSX_MEM_HOST) || !tag_ok(b, 0)) bad++;
+                    for (uint64_t x = 0; x < L; x++)
+                        if (obj[x] != (uint8_t)(src[x] ^ b.key[x & 31] ^ 0x5A)) {
+                            bad++;
+                            break;
+                        }
+                    b.src = b.dst = obj;  // Open in place: the plaintext comes back
+                    if (jfsx_agg_open(a, 0, &b, 0, JFSX_MEM_HOST) || b.status != JFSX_OK || memcmp(obj, src, L)) bad++;
+                }
+            });
+        for (auto &th : ts) th.join();
+        jfsx_agg_free(a);
+        harness_pageable(0, 0);
+    }
     if (bad) {
         std::fprintf(stderr, "%d wrong results\n", bad.load());
         return 1;

@@ -10,6 +10,7 @@ import os
 import subprocess
 import threading
 
+import numpy as np
 import pytest
 
 from juicefs_amd import engine as E
@@ -56,6 +57,8 @@ def H(tmp_path_factory):
         ("jfsx_agg_lz4_compress", I, [P, ctypes.POINTER(E.jfsx_zblk), I]),
         ("jfsx_agg_lz4_decompress", I, [P, ctypes.POINTER(E.jfsx_zblk), I]),
         ("jfsx_mctx_lz4_compress_batch", I, [P, I, ctypes.POINTER(E.jfsx_zblk), I]),
+        ("harness_pageable", None, [ctypes.c_size_t, ctypes.c_size_t]),
+        ("harness_bounces", I, []),
     ]:
         f = getattr(L, name)
         f.restype, f.argtypes = res, args
@@ -598,3 +601,73 @@ def test_serial_ops_keep_one_batch_per_device(H):
     sizes = [s for s, _, _ in batches(H)]
     assert sum(sizes) == 40 and len(sizes) <= 3, sizes
     H.jfsx_agg_free(h)
+
+
+def fake_bytes(src, key):
+    """The stub engine's bytes (agg_host.cpp fake_bytes): src ^ key ^ 0x5A."""
+    return src ^ np.resize(np.frombuffer(key, np.uint8), len(src)) ^ np.uint8(0x5A)
+
+
+def test_pageable_per_object_calls_stage_through_shared_arenas(H):
+    """Per-object calls on pageable memory (a Go-heap slice: io.ReadAll's
+    result and Encrypt's fresh object, encrypt.go:183, :258) are staged by the
+    aggregator on the calling thread: the block is copied into a slice of a
+    shared pinned arena, the batch runs on the staged copies, and the output
+    comes back into the caller's own buffer.  20 callers, Seal then Open of
+    each block (every 5th in place), every 7th Open with a bad tag (nothing
+    released: the caller's buffer is zeroed); all callers' blocks share a few
+    arenas (jfsx_agg.cpp arena_reserve); a block larger than a quarter of an
+    arena takes a bounce buffer of its own."""
+    H.harness_reset(300)
+    N, PER, L = 20, 6, 65536 + 100
+    buf = np.zeros((3, N * PER, L), np.uint8)
+    src, obj, back = buf[0], buf[1], buf[2]
+    src[:] = np.random.default_rng(5).integers(0, 256, src.shape, np.uint8)
+    H.harness_pageable(buf.ctypes.data, buf.ctypes.data + buf.nbytes)
+    b0 = H.harness_bounces()
+    h = new_agg(H, window_us=2000)
+    errs = []
+
+    def worker(t):
+        for j in range(PER):
+            i = t * PER + j
+            b, key = mkblk(i, L)
+            b.src, b.dst = src[i].ctypes.data, obj[i].ctypes.data
+            assert H.jfsx_agg_seal(h, E.AES256GCM, ctypes.byref(b), E.CRC_NONE, E.MEM_HOST) == 0
+            assert b.status == E.OK and bytes(b.tag) == fake_tag(key, L, E.AES256GCM)
+            assert b.src == src[i].ctypes.data and b.dst == obj[i].ctypes.data  # the caller's pointers kept
+            if not np.array_equal(obj[i], fake_bytes(src[i], key)):
+                errs.append(("seal", i))
+            o, _ = mkblk(i, L)
+            ctypes.memmove(o.tag, b.tag, 16)
+            if i % 7 == 3:
+                o.tag[0] ^= 1
+            if i % 5 == 0:  # in place: the object buffer becomes the plaintext
+                o.src = o.dst = obj[i].ctypes.data
+                want_buf = obj[i]
+            else:
+                back[i] = 0xEE
+                o.src, o.dst = obj[i].ctypes.data, back[i].ctypes.data
+                want_buf = back[i]
+            assert H.jfsx_agg_open(h, E.AES256GCM, ctypes.byref(o), E.CRC_NONE, E.MEM_HOST) == 0
+            if i % 7 == 3:
+                if o.status != E.ETAG or want_buf.any():
+                    errs.append(("etag", i))
+            elif o.status != E.OK or not np.array_equal(want_buf, src[i]):
+                errs.append(("open", i))
+
+    run_threads(N, worker)
+    assert not errs, errs[:5]
+    assert H.harness_bounces() - b0 <= 4  # a few shared arenas, not one buffer per call
+    # a block over a quarter of an arena: a bounce buffer of its own
+    big = np.zeros(2 * ((16 << 20) + 4096), np.uint8)
+    big[: len(big) // 2] = 7
+    H.harness_pageable(big.ctypes.data, big.ctypes.data + big.nbytes)
+    b, key = mkblk(999, len(big) // 2)
+    b.src, b.dst = big.ctypes.data, big.ctypes.data + len(big) // 2
+    n0 = H.harness_bounces()
+    assert H.jfsx_agg_seal(h, E.AES256GCM, ctypes.byref(b), E.CRC_NONE, E.MEM_HOST) == 0 and b.status == E.OK
+    assert H.harness_bounces() == n0 + 1
+    assert np.array_equal(big[len(big) // 2:], fake_bytes(big[: len(big) // 2], key))
+    H.harness_pageable(0, 0)
+    assert H.jfsx_agg_free(h) == 0
