@@ -264,8 +264,12 @@ def _cpu_baseline_once(args, mode, lens):
                        "reused (Go's make([]byte) and its zeroing are not charged)" % (args.algo, impl),
             "objdecrypt": "dataEncryptor.Decrypt: header parse + %s open (%s, tag checked) from offset 271 + "
                           "checksum() of the plaintext (3-stream SSE4.2)" % (args.algo, impl)}[mode]
-    blocks = ("%d ragged blocks (the bench's own lengths, %.3f GiB)" % (nblk, nbytes / 2**30) if sample
-              else "1 GiB (256 x 4 MiB blocks)")
+    if sample and len(set(sample)) == 1:
+        blocks = "%d blocks of %d bytes (%.3f GiB)" % (nblk, sample[0], nbytes / 2**30)
+    elif sample:
+        blocks = "%d ragged blocks (the bench's own lengths, %.3f GiB)" % (nblk, nbytes / 2**30)
+    else:
+        blocks = "1 GiB (256 x 4 MiB blocks)"
     return {"value": round(reps * nbytes / total_s / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
             "sample": "%d x %s %s, %d threads (%s), %s" % (reps, blocks, what, threads, note, cpu_model())}
 
@@ -1554,7 +1558,7 @@ def agg_heap_bench(args, world, rank, local, dist, eng):
             cpu = cpu_readat_baseline(args, lens, reads, "full" if op == "verify" else args.level, node=node)
         else:
             cpu = cpu_baseline(args, {"seal": "encrypt", "open": "objdecrypt", "checksum": "crc"}[op],
-                               lens if ragged else None, node=node)
+                               lens if (ragged or L != BLOCK) else None, node=node)
     pcie = eng.pcie_probe()
     if op in ("seal", "open"):  # the block goes up and comes back down: both directions at once
         link_peak = min(pcie["duplex_h2d"], pcie["duplex_d2h"])

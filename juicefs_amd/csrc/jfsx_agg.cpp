@@ -204,6 +204,27 @@ struct AggArena {
     bool open;  // the arena slices are taken from now
 };
 
+namespace {
+// pipelined batches that may run before small groups start to wait for more
+// bytes (JFSX_AGG_INFLIGHT, default 2), and the group size that goes at once
+// whatever runs (JFSX_AGG_FILL_MB, default 4: one 4 MiB block)
+int pipe_inflight() {
+    static const int v = [] {
+        const char *e = getenv("JFSX_AGG_INFLIGHT");
+        const int t = e ? atoi(e) : 2;
+        return t >= 1 ? t : 2;
+    }();
+    return v;
+}
+uint64_t pipe_fill() {
+    static const uint64_t v = [] {
+        const char *e = getenv("JFSX_AGG_FILL_MB");
+        return (uint64_t)(e ? atof(e) * 1048576.0 : 4194304.0);
+    }();
+    return v;
+}
+}  // namespace
+
 using jfsx::Req;
 using jfsx::kSeal;
 using jfsx::kOpen;
@@ -224,6 +245,7 @@ struct jfsx_agg {
     std::deque<Req *> q;
     bool stop = false;
     int busy = 0;             // dispatchers running a pipelined batch
+    Clock::time_point last_done{};  // when the last pipelined batch finished
     std::vector<int> serial;  // per device: dispatchers running a non-pipelined batch
     uint64_t calls = 0, batches = 0, blocks = 0;
     std::vector<uint64_t> dev_batches;
@@ -288,9 +310,15 @@ struct jfsx_agg {
 
     // Dispatcher k: take the group of the oldest request once it is full (block
     // or byte cap) or its window has closed -- or, for a pipelined group, as
-    // soon as another pipelined batch is running (the engine is busy: the time
-    // the group spent queued behind that batch was its batching, and holding it
-    // longer would only idle the pipeline) -- then run it on context cs[k].  A
+    // soon as the engine is streaming: another pipelined batch is running, or
+    // one finished within the window (the time the group spent queued behind
+    // that batch was its batching, and holding it longer would only idle the
+    // pipeline).  While pipe_inflight() pipelined batches already run, a group
+    // of small blocks waits for pipe_fill() bytes, its window or the end of a
+    // running batch instead: every group costs the compute stream a fixed
+    // keysetup / main / finalize sequence (about 0.14 ms for a handful of
+    // 64 KiB blocks), so small blocks travel in fewer, larger groups.  Then
+    // run the group on context cs[k].  A
     // non-pipelined group waits while its device runs another one, so requests
     // arriving meanwhile join one batch instead of several small ones.  The
     // dispatchers share the queue: after every wait the head is re-read, since
@@ -310,8 +338,10 @@ struct jfsx_agg {
             uint64_t bytes = 0;
             for (Req *r : q)
                 if (r->same(*head)) cnt++, bytes += r->bytes;
-            const Clock::time_point deadline = head->t0 + window;
-            if (!(stop || (pipe && busy > 0) || cnt >= max_blocks || bytes >= max_bytes || Clock::now() >= deadline)) {
+            const Clock::time_point now = Clock::now(), deadline = head->t0 + window;
+            const bool streaming = busy > 0 || (last_done != Clock::time_point{} && now - last_done < window);
+            const bool pipe_go = pipe && streaming && (busy < pipe_inflight() || bytes >= pipe_fill());
+            if (!(stop || pipe_go || cnt >= max_blocks || bytes >= max_bytes || now >= deadline)) {
                 cv_work.wait_until(lk, deadline);
                 continue;
             }
@@ -336,6 +366,7 @@ struct jfsx_agg {
             // counted (jfsx_agg_stats right after the last call returns)
             lk.lock();
             held--;
+            if (pipe) last_done = Clock::now();
             batches++;
             dev_batches[dev[k]]++;
             blocks += b.size();

@@ -328,6 +328,7 @@ struct PipeSlot {
     Workspace w;
     hipEvent_t ev_in = nullptr, ev_comp = nullptr, ev_out = nullptr;
     hipEvent_t ev_k0 = nullptr, ev_k1 = nullptr;  // main-kernel timing
+    hipEvent_t ev_ks = nullptr;                   // descriptors pulled and keysetup done (s_ks)
     PipeGroup *owner = nullptr;  // group in flight in this slot (its results not yet collected)
 };
 // one group of one host batch: where its results go once its D2H is done
@@ -363,6 +364,7 @@ struct jfsx_ctx {
     hipStream_t stream = nullptr;  // transform stream
     hipStream_t s_in = nullptr;    // host-ingest H2D
     hipStream_t s_out = nullptr;   // host-ingest D2H
+    hipStream_t s_ks = nullptr;    // host pipeline: descriptor pull + keysetup of the next group
     std::mutex mu;                 // enqueue order on the streams; the synchronous paths' workspace
     uint32_t *d_tab = nullptr;  // aes | crc | crcx
     DevTables tabs{};
@@ -590,7 +592,7 @@ int check_aead_args(int algo, int n, const jfsx_blk *blks, int crc_mode, bool de
 int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEvent_t k1, int algo, bool open, int n,
                  const jfsx_blk *blks, int crc_mode, hipStream_t up = nullptr, hipEvent_t up_ev = nullptr,
                  bool collect = true, hipStream_t fin = nullptr, hipEvent_t main_ev = nullptr,
-                 bool host_crc = false, bool zc = false) {
+                 bool host_crc = false, bool zc = false, hipStream_t ksst = nullptr, hipEvent_t ks_ev = nullptr) {
     const bool gcm = algo == JFSX_AES256GCM;
     // JFSX_CRC_BOTH: the AEAD kernels checksum the plaintext (CRC_GEN) into the
     // first half of each CRC array and crc_segments_k checksums the ciphertext
@@ -716,13 +718,16 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
     uint32_t *dpexp = (uint32_t *)(d + o_pexp);
     uint32_t *dq = (uint32_t *)(d + o_queue);
     BlkOut *dout = zc ? (BlkOut *)(h + o_hres) : (BlkOut *)(d + o_out);
-    // keysetup on the upload stream when one is given (fin set), else on s
-    hipStream_t ks = (up && fin) ? up : s, fs = fin ? fin : s;
+    // keysetup on the upload stream when one is given (fin set), on the
+    // keysetup stream ksst (with zc: the pull too) when given, else on s
+    const bool kss = zc && ksst && ks_ev;
+    hipStream_t ks = kss ? ksst : (up && fin) ? up : s, fs = fin ? fin : s;
     launch_begin();
     if (zc) {
-        // the compute stream pulls the descriptors out of the pinned mirror
-        // itself, so the upload stream carries only the blocks' data
-        launch_pull(s, d, h, h_bytes);
+        // the compute stream (or the keysetup stream) pulls the descriptors
+        // out of the pinned mirror itself, so the upload stream carries only
+        // the blocks' data
+        launch_pull(kss ? ksst : s, d, h, h_bytes);
     } else {
         HIP_OK(hipMemcpyAsync(d, h, h_bytes, hipMemcpyHostToDevice, up ? up : s));
     }
@@ -732,8 +737,12 @@ int enqueue_aead(jfsx_ctx *c, Workspace &w, hipStream_t s, hipEvent_t k0, hipEve
         HIP_OK(hipEventRecord(up_ev, up));
         HIP_OK(hipStreamWaitEvent(s, up_ev, 0));
     }
-    if (gcm) launch_gcm_keysetup(ks, n, dk, db, (GcmSched *)(d + o_sched), c->tabs);
+    if (gcm) launch_gcm_keysetup(ks, n, dk, db, (GcmSched *)(d + o_sched), c->tabs, c->bitslice);
     else launch_cp_keysetup(ks, n, dk, db, (CpSched *)(d + o_sched));
+    if (kss) {  // the descriptors and schedules are ready for the compute stream
+        HIP_OK(hipEventRecord(ks_ev, ksst));
+        HIP_OK(hipStreamWaitEvent(s, ks_ev, 0));
+    }
     if (up && (ks != s || zc)) {
         HIP_OK(hipEventRecord(up_ev, up));
         HIP_OK(hipStreamWaitEvent(s, up_ev, 0));
@@ -1016,6 +1025,20 @@ bool zero_copy_meta() {
     return v;
 }
 
+// The host pipeline's keysetup stream (JFSX_KS_STREAM, default on): each
+// group's descriptor pull and keysetup kernel run on a fourth stream, so they
+// overlap the previous group's main kernel instead of queueing behind it on
+// the compute stream (the compute stream waits for them before the main
+// kernel).  For a group of a few small blocks keysetup is most of the
+// compute stream's time (54 us of 137 per group of 64 KiB blocks, rocprof).
+bool ks_stream() {
+    static const bool v = [] {
+        const char *e = getenv("JFSX_KS_STREAM");
+        return !(e && !strcmp(e, "0"));
+    }();
+    return v;
+}
+
 enum PipeOp { kPipeSeal, kPipeOpen, kPipeCrc };
 
 // One group into an empty slot (s.mu and c->mu held): the blocks' data runs up
@@ -1090,7 +1113,8 @@ int pipe_enqueue(jfsx_ctx *c, PipeSlot &s, PipeOp op, int algo, int nb, const jf
                          zero_copy_meta());
     else
         rc = enqueue_aead(c, w, c->stream, s.ev_k0, s.ev_k1, algo, op == kPipeOpen, nb, dv, crc_mode, c->s_in,
-                          s.ev_in, false, nullptr, nullptr, true, zero_copy_meta());
+                          s.ev_in, false, nullptr, nullptr, true, zero_copy_meta(), ks_stream() ? c->s_ks : nullptr,
+                          s.ev_ks);
     if (rc) return rc;
     HIP_OK(hipEventRecord(s.ev_comp, c->stream));
     HIP_OK(hipStreamWaitEvent(c->s_out, s.ev_comp, 0));
@@ -1753,7 +1777,8 @@ int jfsx_ctx_open(int device, uint32_t flags, jfsx_ctx **out) {
     }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->s_ks, hipStreamNonBlocking) != hipSuccess) {
         jfsx_ctx_close(c);
         return JFSX_EIO;
     }
@@ -1762,8 +1787,8 @@ int jfsx_ctx_open(int device, uint32_t flags, jfsx_ctx **out) {
     make_crc_tables(crc, crcx);
     const size_t nbytes = 4 * (aes.size() + crc.size() + crcx.size());
     if (hipMalloc((void **)&c->d_tab, nbytes) != hipSuccess) {
-        (void)hipStreamDestroy(c->stream);
-        delete c;
+        c->d_tab = nullptr;
+        jfsx_ctx_close(c);  // the streams made above
         return JFSX_ENOMEM;
     }
     std::vector<uint32_t> all;
@@ -1787,6 +1812,7 @@ int jfsx_ctx_open(int device, uint32_t flags, jfsx_ctx **out) {
         if (hipEventCreateWithFlags(&p.ev_in, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&p.ev_comp, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&p.ev_out, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&p.ev_ks, hipEventDisableTiming) != hipSuccess ||
             hipEventCreate(&p.ev_k0) != hipSuccess || hipEventCreate(&p.ev_k1) != hipSuccess) {
             jfsx_ctx_close(c);
             return JFSX_EIO;
@@ -1836,12 +1862,13 @@ int jfsx_ctx_close(jfsx_ctx *c) {
         if (p.w.d) (void)hipFree(p.w.d);
         if (p.w.stage) (void)hipFree(p.w.stage);
         if (p.w.h) (void)hipHostFree(p.w.h);
-        hipEvent_t evs[5] = {p.ev_in, p.ev_comp, p.ev_out, p.ev_k0, p.ev_k1};
+        hipEvent_t evs[6] = {p.ev_in, p.ev_comp, p.ev_out, p.ev_k0, p.ev_k1, p.ev_ks};
         for (hipEvent_t e : evs)
             if (e) (void)hipEventDestroy(e);
     }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->s_in) (void)hipStreamDestroy(c->s_in);
+    if (c->s_ks) (void)hipStreamDestroy(c->s_ks);
     if (c->s_out) (void)hipStreamDestroy(c->s_out);
     delete c;
     return 0;

@@ -1029,9 +1029,114 @@ __device__ __forceinline__ g128 g_mul_uy(const g128 &x, const g128 &y, uint4 *M,
     return z;
 }
 
+// g_mul_uy for a one-wave kernel (keysetup): the 32 table rows x selects are
+// loaded before the Horner chain starts (they depend on x alone), so the
+// chain is VALU work only instead of one dependent LDS round trip per step.
+// Holds the rows in 128 VGPRs -- fine in keysetup's 64-thread workgroup, not
+// in the 1024-thread finalize, which keeps g_mul_uy.
+__device__ __forceinline__ g128 g_mul_uy_pre(const g128 &x, const g128 &y, uint4 *M, uint32_t lane) {
+    const g128 y1 = g_mulx(y), y2 = g_mulx(y1), y3 = g_mulx(y2);
+    __syncthreads();  // the previous call's readers are done with M
+    if (lane < 16) {
+        uint32_t m[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            m[k] = ((lane & 8) ? y.w[k] : 0u) ^ ((lane & 4) ? y1.w[k] : 0u) ^ ((lane & 2) ? y2.w[k] : 0u) ^
+                   ((lane & 1) ? y3.w[k] : 0u);
+        M[lane] = make_uint4(m[0], m[1], m[2], m[3]);
+    }
+    __syncthreads();
+    uint4 mv[32];
+#pragma unroll
+    for (int t = 0; t < 32; t++) mv[t] = M[(x.w[t >> 3] >> (28 - 4 * (t & 7))) & 15u];
+    g128 z = {{0, 0, 0, 0}};
+#pragma unroll
+    for (int t = 31; t >= 0; t--) {
+        const uint32_t sh = z.w[3] & 15u;
+        z.w[3] = __builtin_amdgcn_alignbit(z.w[2], z.w[3], 4);
+        z.w[2] = __builtin_amdgcn_alignbit(z.w[1], z.w[2], 4);
+        z.w[1] = __builtin_amdgcn_alignbit(z.w[0], z.w[1], 4);
+        z.w[0] = (z.w[0] >> 4) ^ ((sh & 1u) ? 0xE1000000u >> 3 : 0u) ^ ((sh & 2u) ? 0xE1000000u >> 2 : 0u) ^
+                 ((sh & 4u) ? 0xE1000000u >> 1 : 0u) ^ ((sh & 8u) ? 0xE1000000u : 0u);
+        z.w[0] ^= mv[t].x, z.w[1] ^= mv[t].y, z.w[2] ^= mv[t].z, z.w[3] ^= mv[t].w;
+    }
+    return z;
+}
+
+// JFSX_KS_PHASES (a probe build, scripts/build_variant.sh): workgroup 0 of
+// each keysetup launch stamps the constant 100 MHz clock at its phase
+// boundaries into g_ks_ts; jfsx_debug_ks_phases reads them back
+#ifdef JFSX_KS_PHASES
+__device__ unsigned long long g_ks_ts[16];
+#define KS_STAMP(i)                                                          \
+    do {                                                                     \
+        __syncthreads();                                                     \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_ks_ts[i] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define KS_STAMP(i) ((void)0)
+#endif
+
+// x^S * v in one step for a static S in 1..64 (S g_mulx steps at once): in
+// this bit order a product by x^S rotates the 128-bit register W0..W3 right
+// by S, and the S coefficients that wrapped to the top (T) reduce by
+// x^128 = 1 + x + x^2 + x^7: add T >> 1, T >> 2 and T >> 7 (nothing of T
+// leaves the register for S <= 64, so one fold suffices)
+template <int S>
+__device__ __forceinline__ g128 g_mulxs(g128 v) {
+    constexpr int q = S / 32, r = S % 32;
+    uint32_t a[4], b[4], t[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) a[k] = v.w[(k - q + 4) & 3];
+#pragma unroll
+    for (int k = 0; k < 4; k++) b[k] = r ? __builtin_amdgcn_alignbit(a[(k + 3) & 3], a[k], r) : a[k];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int top = S - 32 * k;  // bits of T in word k
+        t[k] = top >= 32 ? b[k] : top > 0 ? b[k] & ~(0xffffffffu >> top) : 0u;
+    }
+    g128 z;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t p = k ? t[k - 1] : 0u;
+        z.w[k] = b[k] ^ __builtin_amdgcn_alignbit(p, t[k], 1) ^ __builtin_amdgcn_alignbit(p, t[k], 2) ^
+                 __builtin_amdgcn_alignbit(p, t[k], 7);
+    }
+    return z;
+}
+
+// x^i * v for a per-lane i < 128: the products by x^(2^k) of i's set bits,
+// each taken by select (no divergence)
+__device__ __forceinline__ g128 g_mul_xpow(g128 v, uint32_t i) {
+    g128 u;
+#define JFSX_XPOW_STEP(K)                                       \
+    u = g_mulxs<(1 << K)>(v);                                   \
+    if ((i >> K) & 1u) v = u;
+    JFSX_XPOW_STEP(0)
+    JFSX_XPOW_STEP(1)
+    JFSX_XPOW_STEP(2)
+    JFSX_XPOW_STEP(3)
+    JFSX_XPOW_STEP(4)
+    JFSX_XPOW_STEP(5)
+    JFSX_XPOW_STEP(6)
+#undef JFSX_XPOW_STEP
+    return v;
+}
+
+// One wave per block.  A per-object group of a few small blocks waits for
+// this kernel before its main kernel, so its latency counts: the key schedule
+// is expanded in lane 0's registers, H = E_K(0) and E_K(J0) are encrypted by
+// two halves of the wave at once, only the H^(2^k) the block's exponents can
+// reach are squared (k < bit length of its 16-byte block count, + margin;
+// gcm_finalize_k reads h2k[k] only for bits its exponents have), the basis
+// x^i H^64 is one x^i product per lane (g_mul_xpow) instead of a 128-step
+// chain, and the bitsliced S-box masks are made only for a kernel that uses
+// them (need_bs: the bitsliced or hybrid main kernel).
 __global__ __launch_bounds__(64) void gcm_keysetup_k(const KeyIn *__restrict__ keys, const BlkDev *__restrict__ blks,
-                                                    GcmSched *__restrict__ sched, const uint32_t *__restrict__ gtab) {
+                                                    GcmSched *__restrict__ sched, const uint32_t *__restrict__ gtab,
+                                                    int need_bs) {
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    KS_STAMP(0);
     GcmSched *sc = sched + b;
     const KeyIn k = keys[b];
     __shared__ uint32_t aes[512];  // T0 | T2, compact (gT0 / gT2 / gS)
@@ -1040,17 +1145,19 @@ __global__ __launch_bounds__(64) void gcm_keysetup_k(const KeyIn *__restrict__ k
         aes[2 * x + 1] = gtab[x * 64 + 32];
     }
     __syncthreads();
-    // AES-256 key expansion (FIPS-197 5.2), little-endian dwords, kept in LDS:
-    // one lane expands, every lane reads the words it needs by index (a
-    // lane-indexed register array would live in scratch, whose every access is
-    // a memory round trip)
+    KS_STAMP(1);
+    // AES-256 key expansion (FIPS-197 5.2), little-endian dwords: lane 0
+    // expands in registers (static indices), then the schedule goes to LDS,
+    // where every lane reads the words it needs by index
     __shared__ uint32_t sw[60];
-    if (lane < 8) sw[lane] = keys[b].key[lane];
-    __syncthreads();
     if (lane == 0) {
+        uint32_t e[60];
+#pragma unroll
+        for (int i = 0; i < 8; i++) e[i] = k.key[i];
         uint32_t rcon = 1;
+#pragma unroll
         for (int i = 8; i < 60; i++) {
-            uint32_t t = sw[i - 1];
+            uint32_t t = e[i - 1];
             if ((i & 7) == 0) {
                 t = (t >> 8) | (t << 24);  // RotWord
                 t = gS(aes, t & 0xff) | (gS(aes, (t >> 8) & 0xff) << 8) | (gS(aes, (t >> 16) & 0xff) << 16) |
@@ -1061,13 +1168,16 @@ __global__ __launch_bounds__(64) void gcm_keysetup_k(const KeyIn *__restrict__ k
                 t = gS(aes, t & 0xff) | (gS(aes, (t >> 8) & 0xff) << 8) | (gS(aes, (t >> 16) & 0xff) << 16) |
                     (gS(aes, t >> 24) << 24);
             }
-            sw[i] = sw[i - 8] ^ t;
+            e[i] = e[i - 8] ^ t;
         }
+#pragma unroll
+        for (int i = 0; i < 60; i++) sw[i] = e[i];
     }
     __syncthreads();
+    KS_STAMP(2);
     const uint32_t *w = sw;
     if (lane < 60) sc->rk[lane] = sw[lane];
-    {
+    if (need_bs) {
         // bitsliced-AES masks: lane 4(r-1) + w computes dword w of u_r
         const uint32_t my = lane < 56 ? jfsx_bs::round_mask_word(sw, 1 + (int)(lane >> 2), (int)(lane & 3)) : 0u;
         if (lane < 56) sc->bsu[1 + (lane >> 2)][lane & 3] = my;
@@ -1090,18 +1200,37 @@ __global__ __launch_bounds__(64) void gcm_keysetup_k(const KeyIn *__restrict__ k
         sc->k1[2] = w[6] ^ gT0(aes, x2 & 0xff) ^ gT2(aes, (x0 >> 16) & 0xff) ^ rotl8(gT2(aes, x1 >> 24));
         sc->k1[3] = w[7] ^ rotl8(gT0(aes, (x0 >> 8) & 0xff)) ^ gT2(aes, (x1 >> 16) & 0xff) ^ rotl8(gT2(aes, x2 >> 24));
     }
-    // H = E_K(0), E_K(J0)
-    uint32_t zero[4] = {0, 0, 0, 0}, Hm[4], J0[4], EJ0[4];
-    aes_enc_global(aes, w, zero, Hm);
-    J0[0] = k.nonce[0]; J0[1] = k.nonce[1]; J0[2] = k.nonce[2]; J0[3] = 0x01000000u;  // BE32(1)
-    aes_enc_global(aes, w, J0, EJ0);
+    KS_STAMP(3);
+    // H = E_K(0) on lanes 0..31 and E_K(J0) on lanes 32..63, at once
+    uint32_t in[4], o[4], Hm[4], EJ0[4];
+    {
+        const bool j = lane >= 32;
+        in[0] = j ? k.nonce[0] : 0u;
+        in[1] = j ? k.nonce[1] : 0u;
+        in[2] = j ? k.nonce[2] : 0u;
+        in[3] = j ? 0x01000000u : 0u;  // J0 = nonce || BE32(1)
+        aes_enc_global(aes, w, in, o);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            Hm[q] = (uint32_t)__shfl(o[q], 0, 64);
+            EJ0[q] = (uint32_t)__shfl(o[q], 32, 64);
+        }
+    }
     const g128 H = g_from_mem(Hm);
-    // H^(2^k)
+    KS_STAMP(4);
+    // H^(2^k) for the k this block's exponents can reach (at least k < 8,
+    // which the lane powers below use)
+    uint32_t nsq;
+    {
+        const uint64_t nb16 = (blks[b].len + 15) / 16 + 2;
+        const uint32_t bits = 64u - (uint32_t)__builtin_clzll(nb16);
+        nsq = bits + 1 < 8 ? 8u : bits + 1 > 32 ? 32u : bits + 1;
+    }
     __shared__ g128 hs[8];  // H^(2^k), k < 8: uniform values read by index (LDS, not scratch)
     g128 g = H;
-    for (int i = 0; i < 32; i++) {
+    for (uint32_t i = 0; i < nsq; i++) {
         if (i < 8 && lane == 0) hs[i] = g;
-        if ((int)lane == i) {
+        if (lane == i) {
             uint32_t m[4];
             g_to_mem(g, m);
             for (int q = 0; q < 4; q++) sc->h2k[i][q] = m[q];
@@ -1109,6 +1238,7 @@ __global__ __launch_bounds__(64) void gcm_keysetup_k(const KeyIn *__restrict__ k
         g = g_sqr(g);
     }
     __syncthreads();
+    KS_STAMP(5);
 #if JFSX_KS_NIB
     // H^e for e = lane (bits 0..5: six products by the uniform H^(2^q), each
     // kept where the lane's bit is set), then H^(64 + e) = H^e H^64, e < 4
@@ -1116,10 +1246,10 @@ __global__ __launch_bounds__(64) void gcm_keysetup_k(const KeyIn *__restrict__ k
     {
         g128 z = {{0x80000000u, 0, 0, 0}};  // x^0 = 1
         for (int q = 0; q < 6; q++) {
-            const g128 m = g_mul_uy(z, hs[q], gM, lane);
+            const g128 m = g_mul_uy_pre(z, hs[q], gM, lane);
             if ((lane >> q) & 1) z = m;
         }
-        const g128 z64 = g_mul_uy(z, hs[6], gM, lane);
+        const g128 z64 = g_mul_uy_pre(z, hs[6], gM, lane);
         uint32_t m[4];
         g_to_mem(z, m);
         for (int q = 0; q < 4; q++) sc->hpow[lane][q] = m[q];
@@ -1141,22 +1271,23 @@ __global__ __launch_bounds__(64) void gcm_keysetup_k(const KeyIn *__restrict__ k
         for (int q = 0; q < 4; q++) sc->hpow[e][q] = m[q];
     }
 #endif
-    // basis x^i * H^64
-    g128 v = hs[6];
-    for (int i = 0; i < 128; i++) {
-        if ((i & 63) == (int)lane) {
-            uint32_t m[4];
-            g_to_mem(v, m);
-            for (int q = 0; q < 4; q++) sc->basis[i][q] = m[q];
-        }
-        v = g_mulx(v);
+    KS_STAMP(6);
+    // basis x^i H^64: i = lane, and i = lane + 64 as x^64 times that
+    {
+        const g128 v = g_mul_xpow(hs[6], lane), v64 = g_mulxs<64>(v);
+        uint32_t m[4];
+        g_to_mem(v, m);
+        for (int q = 0; q < 4; q++) sc->basis[lane][q] = m[q];
+        g_to_mem(v64, m);
+        for (int q = 0; q < 4; q++) sc->basis[64 + lane][q] = m[q];
     }
+    KS_STAMP(7);
     // init = E_K(J0) ^ (len block) * H, len block = 0^64 || BE64(8*len)
     {
         const uint64_t bits = blks[b].len * 8;
         g128 L = {{0, 0, (uint32_t)(bits >> 32), (uint32_t)bits}};
 #if JFSX_KS_NIB
-        const g128 LH = g_mul_uy(L, H, gM, lane);  // every lane (barriers); lane 0 stores
+        const g128 LH = g_mul_uy_pre(L, H, gM, lane);  // every lane (barriers); lane 0 stores
 #else
         const g128 LH = lane == 0 ? g_mul(L, H) : L;
 #endif
@@ -1166,7 +1297,14 @@ __global__ __launch_bounds__(64) void gcm_keysetup_k(const KeyIn *__restrict__ k
             for (int q = 0; q < 4; q++) sc->init[q] = m[q] ^ EJ0[q];
         }
     }
+    KS_STAMP(8);
 }
+
+#ifdef JFSX_KS_PHASES
+extern "C" int jfsx_debug_ks_phases(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ks_ts), sizeof(g_ks_ts)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // finalize: one workgroup per block, one thread per partial slot
@@ -1249,8 +1387,14 @@ __global__ __launch_bounds__(1024) void gcm_finalize_k(const BlkDev *__restrict_
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-void launch_gcm_keysetup(hipStream_t s, int n, const KeyIn *keys, const BlkDev *blks, GcmSched *sched, DevTables t) {
-    if (n > 0) hipLaunchKernelGGL(gcm_keysetup_k, dim3(n), dim3(64), 0, s, keys, blks, sched, t.aes);
+// need_bs: the bitsliced main kernel runs (JFSX_CTX_BITSLICE, or the hybrid
+// shape selected by JFSX_GCM_HYBRID), so the schedule carries its S-box masks
+void launch_gcm_keysetup(hipStream_t s, int n, const KeyIn *keys, const BlkDev *blks, GcmSched *sched, DevTables t,
+                         bool bitslice) {
+    static const bool hybrid = getenv("JFSX_GCM_HYBRID") != nullptr;
+    if (n > 0)
+        hipLaunchKernelGGL(gcm_keysetup_k, dim3(n), dim3(64), 0, s, keys, blks, sched, t.aes,
+                           (int)(bitslice || hybrid));
 }
 
 void launch_gcm_main(hipStream_t s, int ntasks, int ncu, uint32_t *queue, bool open, int crc_mode, bool bitslice,

@@ -283,7 +283,7 @@ struct DevTables {
     const uint32_t *crcx;   // 64 lane shift constants, 32 x8pow, K_full
 };
 void launch_gcm_keysetup(hipStream_t s, int n, const KeyIn *keys, const BlkDev *blks, GcmSched *sched,
-                         DevTables t);
+                         DevTables t, bool bitslice);
 // persistent over min(ntasks, ncu) workgroups; queue: 4 device bytes the caller zeroed (enqueue_aead uploads it)
 void launch_gcm_main(hipStream_t s, int ntasks, int ncu, uint32_t *queue, bool open, int crc_mode, bool bitslice,
                      const Task *tasks, const BlkDev *blks, const GcmSched *sched, uint32_t *partial, uint32_t *pexp,

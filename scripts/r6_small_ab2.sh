@@ -1,0 +1,9 @@
+# JFSX_AGG_INFLIGHT 1 / 2 / 3 on per-object heap Encrypt at 64 KiB, 256 KiB, 1 MiB (no CPU leg)
+set -u
+t=${1:-r6v}
+S="bash scripts/suite.sh $t line"
+A="--mode agg --threads 20 --buffers heap --agg-op seal --agg-crc seg --no-cpu --warmup-seconds 3"
+for sz in 65536:400 262144:100 1048576:30; do
+  b=${sz%%:*}; n=${sz##*:}
+  for f in 1 2 3; do JFSX_AGG_INFLIGHT=$f $S if${f}_$b $A --block-bytes $b --steps $n || exit 1; done
+done
