@@ -457,6 +457,21 @@ struct GcmShape {
 __device__ __forceinline__ uint32_t hyb_nbs(uint32_t h) { return h & 15u; }
 __device__ __forceinline__ uint32_t hyb_rho(uint32_t h) { return (h >> 8) & 255u; }
 
+// JFSX_KS_PHASES probe build: the workgroup running block 0's first task
+// stamps the 100 MHz clock at the main kernel's phase boundaries (g_main_ts:
+// kernel start, tables staged, GHASH table built, rows done, epilogue done,
+// task done); jfsx_debug_main_phases reads them back
+#ifdef JFSX_KS_PHASES
+__device__ unsigned long long g_main_ts[8];
+#define MAIN_STAMP(cond, i)                                                                  \
+    do {                                                                                     \
+        __syncthreads();                                                                     \
+        if ((cond) && threadIdx.x == 0) g_main_ts[i] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define MAIN_STAMP(cond, i) ((void)0)
+#endif
+
 #ifdef JFSX_ABLATE_TRACE
 // diagnostic build only (make variant V=TRACE): per workgroup start / end
 // times (s_memrealtime, 100 MHz), HW_ID | XCC_ID << 32 and the task's bytes
@@ -510,6 +525,8 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
     }
     __syncthreads();
 
+    const bool first_task = task.blk == 0 && task.c0 == 0;
+    MAIN_STAMP(first_task, 2);
     const uint64_t c0 = task.c0, c1 = task.c1;
     const uint32_t nseg = (uint32_t)((c1 - c0 + kSeg - 1) / kSeg);
     constexpr uint32_t V = GcmShape<BS>::waves * NS;  // virtual waves (streams) per task
@@ -833,6 +850,7 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
         }
     }
 
+    MAIN_STAMP(first_task, 3);
     // ---- stream epilogues: lift lane accumulators to the stream end, reduce ----
     const uint64_t nblk = (blk.len + 15) >> 4;
 #pragma unroll
@@ -881,6 +899,7 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
         g_wgtrace[4 * task.trace + 3] = task.c1 - task.c0;
     }
 #endif
+    MAIN_STAMP(first_task, 4);
     // ---- segments shared by two or more waves: sum the raw shares, finish ----
     if (CRCMODE && kShares) {
         __syncthreads();
@@ -902,6 +921,7 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
             }
         }
     }
+    MAIN_STAMP(first_task, 5);
 }
 
 // gcm_main: persistent workgroups, one per CU (the LDS tables allow one),
@@ -922,6 +942,9 @@ __global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *
     __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
     __shared__ uint32_t s_task;
     const uint32_t tid = threadIdx.x;
+#ifdef JFSX_KS_PHASES
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     {
         const uint4 *ga = reinterpret_cast<const uint4 *>(tab.aes);
         uint4 *la = reinterpret_cast<uint4 *>(lds + kLdsAes);
@@ -932,6 +955,14 @@ __global__ __launch_bounds__(GcmShape<BS>::threads) void gcm_main_k(const Task *
             for (uint32_t i = tid; i < 1280; i += GcmShape<BS>::threads) lc[i] = gc[i];
         }
     }
+#ifdef JFSX_KS_PHASES
+    __syncthreads();
+    const unsigned long long t_staged = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0 && tasks[0].blk == 0 && blockIdx.x == 0) {  // the WG that is likely to pop task 0
+        g_main_ts[0] = t_start;
+        g_main_ts[1] = t_staged;
+    }
+#endif
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;  // wave index in an SGPR
     const uint32_t loff = ((lane & 31) << 2) | 0x00010000u;  // AES replica offset | table base
     const GhLane gl = gh_lane(lane);
@@ -1301,6 +1332,9 @@ __global__ __launch_bounds__(64) void gcm_keysetup_k(const KeyIn *__restrict__ k
 }
 
 #ifdef JFSX_KS_PHASES
+extern "C" int jfsx_debug_main_phases(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_main_ts), sizeof(g_main_ts)) == hipSuccess ? 0 : -1;
+}
 extern "C" int jfsx_debug_ks_phases(unsigned long long *out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ks_ts), sizeof(g_ks_ts)) == hipSuccess ? 0 : -1;
 }
