@@ -616,8 +616,15 @@ def resident_bench(args, world, rank, local, dist):
         if mode == "decrypt" and rsa:
             # each object also pays one RSA-OAEP private-key unwrap on the host
             # (encrypt.go:207-210): per thread, block time + unwrap time
-            per_block = cpu["cores"] * BLOCK / (cpu["value"] * 1e9)
-            cpu["value"] = round(cpu["cores"] * BLOCK / (per_block + rsa["host_us_per_unwrap_1thread"] * 1e-6) / 1e9, 3)
+            def with_unwrap(gbs, cores):
+                per_block = cores * BLOCK / (gbs * 1e9)
+                return round(cores * BLOCK / (per_block + rsa["host_us_per_unwrap_1thread"] * 1e-6) / 1e9, 3)
+            cpu["value"] = with_unwrap(cpu["value"], cpu["cores"])
+            if cpu.get("other_placement"):  # the same unwrap cost on the other placement
+                op_ = cpu["other_placement"]
+                op_["value"] = with_unwrap(op_["value"], op_["cores"])
+            if cpu.get("core_s_per_GB"):
+                cpu["core_s_per_GB"] = round(cpu["cores"] / cpu["value"], 4)
             cpu["sample"] += "; plus one libcrypto RSA-OAEP unwrap per block (%.1f us, measured on 1 thread)" % (
                 rsa["host_us_per_unwrap_1thread"])
     resident_plain = sum(shards[0].lens)
