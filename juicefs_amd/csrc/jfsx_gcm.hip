@@ -1350,8 +1350,11 @@ extern "C" int jfsx_debug_ks_phases(unsigned long long *out) {
 // 128-step product per set bit.  A small batch (the per-object path) has
 // blocks of many short tasks and so many slots: the workgroup grows to one
 // thread per slot (up to 1024) instead of one wave looping over them.
-template <bool OPEN, int CRCMODE>
-__global__ __launch_bounds__(1024) void gcm_finalize_k(const BlkDev *__restrict__ blks, const GcmSched *__restrict__ sched,
+// TH: the launch's thread cap.  TH = 64 (blocks of at most 64 slots: a group
+// of small per-object blocks) takes g_mul_uy_pre, whose table rows sit in
+// registers a 1024-thread workgroup does not have.
+template <bool OPEN, int CRCMODE, int TH>
+__global__ __launch_bounds__(TH) void gcm_finalize_k(const BlkDev *__restrict__ blks, const GcmSched *__restrict__ sched,
                                                       const uint32_t *__restrict__ partial,
                                                       const uint32_t *__restrict__ pexp, BlkOut *__restrict__ out) {
     const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nthr = blockDim.x;
@@ -1383,7 +1386,8 @@ __global__ __launch_bounds__(1024) void gcm_finalize_k(const BlkDev *__restrict_
         g128 z = g_from_mem(m);
         for (int k = 0; k < 32 && (eo >> k); k++) {
             if (!((eo >> k) & 1u)) continue;
-            const g128 zk = g_mul_uy(z, g_from_mem(h2k[k]), M, tid);
+            const g128 zk = TH == 64 ? g_mul_uy_pre(z, g_from_mem(h2k[k]), M, tid)
+                                     : g_mul_uy(z, g_from_mem(h2k[k]), M, tid);
             if ((e >> k) & 1u) z = zk;
         }
         g_to_mem(z, m);
@@ -1477,7 +1481,13 @@ void launch_gcm_finalize(hipStream_t s, int n, bool open, int crc_mode, const Bl
     if (n <= 0) return;
     // one thread per slot of the block with the most slots, 64..1024
     const uint32_t th = max_slots <= 64 ? 64u : max_slots >= 1024 ? 1024u : (max_slots + 63) / 64 * 64;
-#define L(O, C) hipLaunchKernelGGL((gcm_finalize_k<O, C>), dim3(n), dim3(th), 0, s, blks, sched, partial, pexp, out)
+#define L(O, C)                                                                                          \
+    do {                                                                                                 \
+        if (th == 64)                                                                                    \
+            hipLaunchKernelGGL((gcm_finalize_k<O, C, 64>), dim3(n), dim3(64), 0, s, blks, sched, partial, pexp, out); \
+        else                                                                                             \
+            hipLaunchKernelGGL((gcm_finalize_k<O, C, 1024>), dim3(n), dim3(th), 0, s, blks, sched, partial, pexp, out); \
+    } while (0)
     if (open) {
         if ((crc_mode & 3) == 2) L(true, 2); else L(true, 0);
     } else {

@@ -1,0 +1,1 @@
+bench.py --mode agg --threads 20 --buffers heap --agg-op open --agg-crc seg --algo chacha20poly1305 --steps 10
