@@ -206,13 +206,13 @@ struct AggArena {
 
 namespace {
 // pipelined batches that may run before small groups start to wait for more
-// bytes (JFSX_AGG_INFLIGHT, default 2), and the group size that goes at once
+// bytes (JFSX_AGG_INFLIGHT, default 3), and the group size that goes at once
 // whatever runs (JFSX_AGG_FILL_MB, default 4: one 4 MiB block)
 int pipe_inflight() {
     static const int v = [] {
         const char *e = getenv("JFSX_AGG_INFLIGHT");
-        const int t = e ? atoi(e) : 2;
-        return t >= 1 ? t : 2;
+        const int t = e ? atoi(e) : 3;  // 2 before the keysetup stream (profiles/r6/ab_small/)
+        return t >= 1 ? t : 3;
     }();
     return v;
 }
