@@ -52,6 +52,12 @@ namespace jfsx {
 // directly, the AES base as 0x10000 (bit 16 of the lane's v_perm operand loff)
 // plus the offset 20K.  So no lookup spends a VALU op on its base.
 // ---------------------------------------------------------------------------
+// JFSX_GF_CT_LIFT (default 1): the main kernel's per-lane GHASH lifts by
+// g_mul_ct instead of the bit-serial g_mul (A/B builds)
+#ifndef JFSX_GF_CT_LIFT
+#define JFSX_GF_CT_LIFT 1
+#endif
+
 constexpr uint32_t kLdsCrc = 0;
 constexpr uint32_t kLdsGh = 20480;              // GHASH T[b][j]: kLdsGh + (b << 8) | (j << 4)
 constexpr uint32_t kLdsAesOff = 20480;          // ds_read offset of the AES table
@@ -864,7 +870,8 @@ __device__ __forceinline__ void gcm_task(char *lds, const Task task, const BlkDe
 #ifdef JFSX_ABLATE_LIFT
             z = g_from_mem(a);  // timing experiment only: wrong tags
 #else
-            z = g_mul(g_from_mem(a), g_from_mem(sch->hpow[e]));
+            z = JFSX_GF_CT_LIFT ? g_mul_ct_call(g_from_mem(a), g_from_mem(sch->hpow[e]))
+                                : g_mul(g_from_mem(a), g_from_mem(sch->hpow[e]));
 #endif
         }
         uint32_t zm[4];
@@ -1027,6 +1034,11 @@ __device__ void aes_enc_global(const uint32_t *aes, const uint32_t *rk, const ui
 // x per step (Horner from the high coefficients: z = z x^4 + y N_t), the 16
 // multiples y (n3 + n2 x + n1 x^2 + n0 x^3) in LDS.  About 600 instructions
 // against g_mul's 2000; every lane of the wave must call it (barriers).
+// JFSX_GF_CT (default 1): keysetup's and finalize's GF products by
+// integer multiplies (g_mul_ct, jfsx_gf.h) instead of LDS nibble tables
+#ifndef JFSX_GF_CT
+#define JFSX_GF_CT 1
+#endif
 #ifndef JFSX_KS_NIB
 #define JFSX_KS_NIB 1  // 0: keysetup with the bit-serial g_mul (A/B)
 #endif
@@ -1277,10 +1289,10 @@ __global__ __launch_bounds__(64) void gcm_keysetup_k(const KeyIn *__restrict__ k
     {
         g128 z = {{0x80000000u, 0, 0, 0}};  // x^0 = 1
         for (int q = 0; q < 6; q++) {
-            const g128 m = g_mul_uy_pre(z, hs[q], gM, lane);
+            const g128 m = JFSX_GF_CT ? g_mul_ct_call(z, hs[q]) : g_mul_uy_pre(z, hs[q], gM, lane);
             if ((lane >> q) & 1) z = m;
         }
-        const g128 z64 = g_mul_uy_pre(z, hs[6], gM, lane);
+        const g128 z64 = JFSX_GF_CT ? g_mul_ct_call(z, hs[6]) : g_mul_uy_pre(z, hs[6], gM, lane);
         uint32_t m[4];
         g_to_mem(z, m);
         for (int q = 0; q < 4; q++) sc->hpow[lane][q] = m[q];
@@ -1318,7 +1330,7 @@ __global__ __launch_bounds__(64) void gcm_keysetup_k(const KeyIn *__restrict__ k
         const uint64_t bits = blks[b].len * 8;
         g128 L = {{0, 0, (uint32_t)(bits >> 32), (uint32_t)bits}};
 #if JFSX_KS_NIB
-        const g128 LH = g_mul_uy_pre(L, H, gM, lane);  // every lane (barriers); lane 0 stores
+        const g128 LH = JFSX_GF_CT ? g_mul_ct_call(L, H) : g_mul_uy_pre(L, H, gM, lane);  // lane 0 stores
 #else
         const g128 LH = lane == 0 ? g_mul(L, H) : L;
 #endif
@@ -1386,8 +1398,9 @@ __global__ __launch_bounds__(TH) void gcm_finalize_k(const BlkDev *__restrict__ 
         g128 z = g_from_mem(m);
         for (int k = 0; k < 32 && (eo >> k); k++) {
             if (!((eo >> k) & 1u)) continue;
-            const g128 zk = TH == 64 ? g_mul_uy_pre(z, g_from_mem(h2k[k]), M, tid)
-                                     : g_mul_uy(z, g_from_mem(h2k[k]), M, tid);
+            const g128 zk = JFSX_GF_CT ? g_mul_ct_call(z, g_from_mem(h2k[k]))
+                            : TH == 64 ? g_mul_uy_pre(z, g_from_mem(h2k[k]), M, tid)
+                                       : g_mul_uy(z, g_from_mem(h2k[k]), M, tid);
             if ((e >> k) & 1u) z = zk;
         }
         g_to_mem(z, m);

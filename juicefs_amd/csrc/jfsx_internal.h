@@ -14,6 +14,10 @@
 
 #include "../../include/jfsx.h"
 
+#define JFSX_GF_HD __device__ __forceinline__
+#define JFSX_GF_BREAK() __builtin_amdgcn_sched_barrier(0)
+#include "jfsx_gf.h"
+
 namespace jfsx {
 
 constexpr int kSeg = 32768;         // csBlock (disk_cache.go:1207)
@@ -177,6 +181,18 @@ __device__ __forceinline__ g128 g_mulx(g128 v) {
     v.w[0] = (v.w[0] >> 1) ^ (0xE1000000u & (0u - lsb));
     return v;
 }
+
+// per-lane x times per-lane y from integer multiplies (jfsx_gf.h): about 500
+// instructions against g_mul's 2000, no LDS, no barrier
+__device__ __forceinline__ g128 g_mul_ct(const g128 &x, const g128 &y) {
+    g128 z;
+    jfsx_gf::mul(x.w, y.w, z.w);
+    return z;
+}
+
+// the same as a call: the GCM kernels take it this way (inlined into them,
+// the iterative-ILP scheduler of the ROCm 7.2 compiler crashes)
+__device__ __noinline__ g128 g_mul_ct_call(g128 x, g128 y) { return g_mul_ct(x, y); }
 
 // generic bit-serial product (SP 800-38D Algorithm 1)
 __device__ __noinline__ g128 g_mul(g128 x, g128 y) {
