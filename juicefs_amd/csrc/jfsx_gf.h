@@ -35,6 +35,18 @@
 
 namespace jfsx_gf {
 
+// bit reversal of a word (v_bfrev_b32 on the GPU)
+JFSX_GF_HD uint32_t rev32(uint32_t v) {
+#if defined(__has_builtin) && __has_builtin(__builtin_bitreverse32)
+    return __builtin_bitreverse32(v);
+#else
+    v = ((v >> 1) & 0x55555555u) | ((v & 0x55555555u) << 1);
+    v = ((v >> 2) & 0x33333333u) | ((v & 0x33333333u) << 2);
+    v = ((v >> 4) & 0x0F0F0F0Fu) | ((v & 0x0F0F0F0Fu) << 4);
+    return __builtin_bswap32(v);
+#endif
+}
+
 // carry-less 32 x 32 -> 64
 JFSX_GF_HD uint64_t clmul32(uint32_t x, uint32_t y) {
     const uint32_t x0 = x & 0x11111111u, x1 = x & 0x22222222u, x2 = x & 0x44444444u, x3 = x & 0x88888888u;
@@ -64,10 +76,10 @@ JFSX_GF_HD void clmul64(uint64_t a, uint64_t b, uint64_t &lo, uint64_t &hi) {
 // z = x y in GCM's bit order; x, y, z as four words w[0..3] (reflected)
 JFSX_GF_HD void mul(const uint32_t x[4], const uint32_t y[4], uint32_t z[4]) {
     // plain order, 64-bit halves: A = a1 x^64 + a0
-    const uint64_t a0 = (uint64_t)__builtin_bitreverse32(x[0]) | (uint64_t)__builtin_bitreverse32(x[1]) << 32;
-    const uint64_t a1 = (uint64_t)__builtin_bitreverse32(x[2]) | (uint64_t)__builtin_bitreverse32(x[3]) << 32;
-    const uint64_t b0 = (uint64_t)__builtin_bitreverse32(y[0]) | (uint64_t)__builtin_bitreverse32(y[1]) << 32;
-    const uint64_t b1 = (uint64_t)__builtin_bitreverse32(y[2]) | (uint64_t)__builtin_bitreverse32(y[3]) << 32;
+    const uint64_t a0 = (uint64_t)rev32(x[0]) | (uint64_t)rev32(x[1]) << 32;
+    const uint64_t a1 = (uint64_t)rev32(x[2]) | (uint64_t)rev32(x[3]) << 32;
+    const uint64_t b0 = (uint64_t)rev32(y[0]) | (uint64_t)rev32(y[1]) << 32;
+    const uint64_t b1 = (uint64_t)rev32(y[2]) | (uint64_t)rev32(y[3]) << 32;
     uint64_t l0, h0, l1, h1, lm, hm;
     clmul64(a0, b0, l0, h0);
     clmul64(a1, b1, l1, h1);
@@ -83,10 +95,10 @@ JFSX_GF_HD void mul(const uint32_t x[4], const uint32_t y[4], uint32_t z[4]) {
     const uint64_t f3 = r3 ^ (r3 << 1) ^ (r3 << 2) ^ (r3 << 7) ^ (r2 >> 63) ^ (r2 >> 62) ^ (r2 >> 57);
     const uint64_t o = (r3 >> 63) ^ (r3 >> 62) ^ (r3 >> 57);  // coefficients 128.. of (r3 r2)(x^7 + x^2 + x)
     const uint64_t c0 = r0 ^ f2 ^ o ^ (o << 1) ^ (o << 2) ^ (o << 7), c1 = r1 ^ f3;
-    z[0] = __builtin_bitreverse32((uint32_t)c0);
-    z[1] = __builtin_bitreverse32((uint32_t)(c0 >> 32));
-    z[2] = __builtin_bitreverse32((uint32_t)c1);
-    z[3] = __builtin_bitreverse32((uint32_t)(c1 >> 32));
+    z[0] = rev32((uint32_t)c0);
+    z[1] = rev32((uint32_t)(c0 >> 32));
+    z[2] = rev32((uint32_t)c1);
+    z[3] = rev32((uint32_t)(c1 >> 32));
 }
 
 }  // namespace jfsx_gf
