@@ -1260,7 +1260,7 @@ def agg_bench(args, world, rank, local, dist, eng):
                 "note": "getrusage(RUSAGE_SELF) over the timed region: every thread of this process (the Python "
                         "callers and their ctypes calls, the aggregator's dispatchers); no bounce copies (pinned "
                         "blocks)"}
-    pcie = eng.pcie_probe()
+    pcie, probes = best_link_probe(eng)
     duplex = min(pcie["duplex_h2d"], pcie["duplex_d2h"])
     if rank == 0:
         print(json.dumps({
@@ -1285,7 +1285,8 @@ def agg_bench(args, world, rank, local, dist, eng):
                            "(host batches share the context's pipeline)",
             "roofline": {"bound": "pcie", "achieved": round(value, 2), "peak": duplex, "unit": "GB/s",
                          "frac": round(value / duplex, 4), "peak_basis": "min over directions of simultaneous H2D + "
-                         "D2H copies (jfsx_pcie_probe, after the run)", "pcie_measured": pcie,
+                         "D2H copies (jfsx_pcie_probe after the run, best of 3 per rate)", "pcie_measured": pcie,
+                         "pcie_probes": probes,
                          "frac_of_link": round(value / PCIE_GEN5_X16_GBS, 4)},
             "host_cpu": host_cpu, "cpu_baseline": cpu, "verified_blocks": verified, "full_check": full}), flush=True)
     for h in (hin, hout, hcrc, hdec, hcrc2):
@@ -1294,6 +1295,16 @@ def agg_bench(args, world, rank, local, dist, eng):
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def best_link_probe(eng, runs=3):
+    """the link's rates for the per-object lines: jfsx_pcie_probe after the
+    run, the best of `runs` probes per rate (one probe has read a duplex rate
+    15% under the others on a quiet box; the ceiling is what the link can
+    do), with every probe kept"""
+    probes = [eng.pcie_probe() for _ in range(runs)]
+    best = {k: max(p.get(k, 0.0) for p in probes) for k in probes[0]}
+    return best, probes
 
 
 def host_cpu_seconds():
@@ -1566,13 +1577,13 @@ def agg_heap_bench(args, world, rank, local, dist, eng):
         else:
             cpu = cpu_baseline(args, {"seal": "encrypt", "open": "objdecrypt", "checksum": "crc"}[op],
                                lens if (ragged or L != BLOCK) else None, node=node)
-    pcie = eng.pcie_probe()
+    pcie, probes = best_link_probe(eng)
     if op in ("seal", "open"):  # the block goes up and comes back down: both directions at once
         link_peak = min(pcie["duplex_h2d"], pcie["duplex_d2h"])
-        peak_basis = "min over directions of simultaneous H2D + D2H copies (jfsx_pcie_probe, after the run)"
+        peak_basis = "min over directions of simultaneous H2D + D2H copies (jfsx_pcie_probe after the run, best of 3)"
     else:  # checksum / ReadAt verify: only the data goes up (results land in the pinned mirror)
         link_peak = pcie["h2d"]
-        peak_basis = "H2D copies alone (jfsx_pcie_probe, after the run): the CRC calls move data one way"
+        peak_basis = "H2D copies alone (jfsx_pcie_probe after the run, best of 3): the CRC calls move data one way"
     gb = world * step_bytes * args.steps / 1e9
     host_cpu = {"cpu_seconds": round(cpu_used, 3), "cpu_s_per_GB": round(cpu_used / gb, 4),
                 "cores_busy": round(cpu_used / el, 2),
@@ -1610,7 +1621,7 @@ def agg_heap_bench(args, world, rank, local, dist, eng):
             "host_cpu": host_cpu,
             "roofline": {"bound": "pcie", "achieved": round(value, 2), "peak": link_peak, "unit": "GB/s",
                          "frac": round(value / link_peak, 4), "peak_basis": peak_basis,
-                         "pcie_measured": pcie, "h2d_one_way": pcie["h2d"],
+                         "pcie_measured": pcie, "pcie_probes": probes, "h2d_one_way": pcie["h2d"],
                          "frac_of_link": round(value / PCIE_GEN5_X16_GBS, 4)},
             "cpu_baseline": cpu, "verified_blocks": nb if full else 0, "full_check": full}), flush=True)
     eng.close()

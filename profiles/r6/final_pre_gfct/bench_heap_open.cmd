@@ -1,0 +1,1 @@
+bench.py --mode agg --threads 20 --steps 10 --buffers heap --agg-op open --agg-crc seg
