@@ -852,7 +852,7 @@ def full_check(args, E, blks, got, lens, base):
 PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
 # labelled PMC summaries (scripts/pmc_r3.py), newest first; the round-2 file
 # (FETCH / WRITE only, keyed by kernel) is the last resort for traffic
-PMC_FILES = ("r5/pmc_r5.json", "r4/pmc_r4.json", "r3/pmc_r3.json")
+PMC_FILES = ("r6/pmc_r6.json", "r5/pmc_r5.json", "r4/pmc_r4.json", "r3/pmc_r3.json")
 PMC_R2 = "r2/pmc_traffic.json"
 R2_KEYS = {"seal_gcm": "gcm_ttable", "open_gcm": "gcm_ttable", "seal_gcm_bitslice": "gcm_bitslice",
            "seal_chacha": "chacha", "open_chacha": "chacha", "crc_verify": "crc_verify",
