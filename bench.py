@@ -65,6 +65,8 @@ def parse():
                     help="agg --agg-op readat: the cache checksum level (disk_cache.go:1265-1307)")
     ap.add_argument("--reads-per-block", type=int, default=4, help="agg --agg-op readat: random reads per image")
     ap.add_argument("--agg-window-us", type=int, default=500, help="agg: aggregation window")
+    ap.add_argument("--log-clocks", action="store_true",
+                    help="agg --buffers heap: sample the GPUs' DPM clock levels (sysfs, read only) over the run")
     ap.add_argument("--agg-max-mb", type=int, default=12,
                     help="agg: byte cap of one aggregated batch (several batches pipeline at once)")
     ap.add_argument("--algo", choices=["aes256gcm", "chacha20poly1305"], default="aes256gcm")
@@ -1307,6 +1309,75 @@ def best_link_probe(eng, runs=3):
     return best, probes
 
 
+class ClockLog:
+    """--log-clocks: the GPUs' DPM levels (pp_dpm_sclk / mclk / fclk / socclk,
+    the level marked '*') and gpu_busy_percent, read from sysfs every 100 ms in
+    a thread over the warm-up and the timed region (read only; a diagnostic of
+    run-to-run spread).  summary(): per card that was busy, the share of
+    samples at each level, per phase."""
+
+    FILES = ("pp_dpm_sclk", "pp_dpm_mclk", "pp_dpm_fclk", "pp_dpm_socclk")
+
+    def __init__(self, period=0.1):
+        import glob
+        import threading
+        self.cards = sorted(glob.glob("/sys/class/drm/card[0-9]*/device"))
+        self.period, self.phase, self.samples = period, "warmup", []
+        self.ev = threading.Event()
+        self.th = threading.Thread(target=self._loop, daemon=True)
+
+    @staticmethod
+    def _read(path):
+        try:
+            with open(path) as f:
+                return f.read()
+        except OSError:
+            return None
+
+    def _loop(self):
+        while not self.ev.wait(self.period):
+            row = {}
+            for c in self.cards:
+                busy = self._read(c + "/gpu_busy_percent")
+                lv = {}
+                for n in self.FILES:
+                    t = self._read(c + "/" + n)
+                    cur = [ln.split(":", 1)[1].strip() for ln in (t or "").splitlines() if ln.rstrip().endswith("*")]
+                    lv[n[7:]] = cur[0].rstrip("*").strip() if cur else None
+                row[c.split("/")[-2]] = (int(busy) if busy and busy.strip().isdigit() else None, lv)
+            self.samples.append((self.phase, row))
+
+    def start(self):
+        self.th.start()
+
+    def mark(self, phase):
+        self.phase = phase
+
+    def stop(self):
+        self.ev.set()
+        self.th.join()
+
+    def summary(self):
+        import collections
+        out = {}
+        for card in {k for _, row in self.samples for k in row}:
+            busy = [row[card][0] for _, row in self.samples if row.get(card) and row[card][0] is not None]
+            if not busy or max(busy) == 0:
+                continue
+            per = {}
+            for phase in ("warmup", "timed"):
+                rows = [row[card] for ph, row in self.samples if ph == phase and card in row]
+                if not rows:
+                    continue
+                d = {"samples": len(rows), "busy_mean": round(sum(b or 0 for b, _ in rows) / len(rows), 1)}
+                for n in ("sclk", "mclk", "fclk", "socclk"):
+                    cnt = collections.Counter(lv.get(n) for _, lv in rows)
+                    d[n] = {str(k): round(v / len(rows), 3) for k, v in cnt.most_common()}
+                per[phase] = d
+            out[card] = per
+        return out or {"note": "no busy card readable under /sys/class/drm"}
+
+
 def host_cpu_seconds():
     """user + system CPU seconds of this process so far (every thread: the
     callers, the aggregator's dispatchers, the engine's bounce copies)"""
@@ -1497,13 +1568,20 @@ def agg_heap_bench(args, world, rank, local, dist, eng):
         d_steps = max(1, args.steps // 5)
         run(direct, 1)
         d_val = round(step_bytes * d_steps / run(direct, d_steps) / 1e9, 2)
+    clocks = ClockLog() if args.log_clocks else None
+    if clocks:
+        clocks.start()
     warm_up(args, lambda: run(through, 1), host=True)
+    if clocks:
+        clocks.mark("timed")
     c0, b0, k0 = agg.stats()
     m0 = eng.metrics(reset=False)
     barrier(dist)
     cpu0 = host_cpu_seconds()
     el = max_over_ranks(dist, run(through, args.steps), local)
     cpu_used = host_cpu_seconds() - cpu0
+    if clocks:
+        clocks.stop()
     c1, b1, k1 = agg.stats()
     agg.close()
     value = world * step_bytes * args.steps / el / 1e9
@@ -1619,6 +1697,7 @@ def agg_heap_bench(args, world, rank, local, dist, eng):
                                      ("seal_batches", "seal_bytes", "open_batches", "open_bytes", "crc_batches",
                                       "crc_bytes")},
             "host_cpu": host_cpu,
+            **({"clocks": clocks.summary()} if clocks else {}),
             "roofline": {"bound": "pcie", "achieved": round(value, 2), "peak": link_peak, "unit": "GB/s",
                          "frac": round(value / link_peak, 4), "peak_basis": peak_basis,
                          "pcie_measured": pcie, "pcie_probes": probes, "h2d_one_way": pcie["h2d"],
