@@ -36,6 +36,12 @@
 
 #include "jfsx_dev.h"
 
+// TabL::put as one masked LDS write (ds_mskor_b32) instead of an and / or
+// atomic pair; -DJFSX_LZ4_MSKOR=0 builds the pair (A/B)
+#ifndef JFSX_LZ4_MSKOR
+#define JFSX_LZ4_MSKOR 1
+#endif
+
 namespace jfsx {
 
 namespace {
@@ -325,8 +331,16 @@ struct TabL {
     __device__ __forceinline__ void put(uint32_t h, uint32_t v) const {
         lo[h] = (uint16_t)v;
         const uint32_t sh = 2 * (h & 15);
+#if JFSX_LZ4_MSKOR
+        // one LDS op: word = (word & ~mask) | bits (ds_mskor_b32, atomic in
+        // LDS like the and / or pair it replaces; a wave's LDS ops complete
+        // in order, so a later read of the word sees it)
+        const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t *)&hb[h >> 4];
+        asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"(a), "v"(3u << sh), "v"(((v >> 16) & 3u) << sh) : "memory");
+#else
         atomicAnd(&hb[h >> 4], ~(3u << sh));
         atomicOr(&hb[h >> 4], ((v >> 16) & 3u) << sh);
+#endif
     }
     __device__ void sweep(uint32_t s, uint32_t lane) {
         // lane owns words 4 lane .. 4 lane + 3 and their 64 entries
