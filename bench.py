@@ -1318,10 +1318,20 @@ class ClockLog:
 
     FILES = ("pp_dpm_sclk", "pp_dpm_mclk", "pp_dpm_fclk", "pp_dpm_socclk")
 
-    def __init__(self, period=0.1):
+    def __init__(self, period=0.1, device=0):
         import glob
         import threading
         self.cards = sorted(glob.glob("/sys/class/drm/card[0-9]*/device"))
+        self.ours = None  # the card of this process's GPU, by PCI address (torch's device properties)
+        try:
+            import torch
+            pr = torch.cuda.get_device_properties(device)
+            addr = "%04x:%02x:%02x." % (pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id)
+            for c in self.cards:
+                if os.path.basename(os.path.realpath(c)).startswith(addr):
+                    self.ours = c.split("/")[-2]
+        except Exception:  # noqa: BLE001 -- diagnostic only: fall back to every busy card
+            pass
         self.period, self.phase, self.samples = period, "warmup", []
         self.ev = threading.Event()
         self.th = threading.Thread(target=self._loop, daemon=True)
@@ -1362,7 +1372,7 @@ class ClockLog:
         out = {}
         for card in {k for _, row in self.samples for k in row}:
             busy = [row[card][0] for _, row in self.samples if row.get(card) and row[card][0] is not None]
-            if not busy or max(busy) == 0:
+            if card != self.ours and (not busy or max(busy) == 0):
                 continue
             per = {}
             for phase in ("warmup", "timed"):
@@ -1374,7 +1384,9 @@ class ClockLog:
                     cnt = collections.Counter(lv.get(n) for _, lv in rows)
                     d[n] = {str(k): round(v / len(rows), 3) for k, v in cnt.most_common()}
                 per[phase] = d
-            out[card] = per
+            out[card + (" (this GPU)" if card == self.ours else "")] = per
+        if out and self.ours is None:
+            out["note"] = "this GPU's card not identified: every busy card is listed"
         return out or {"note": "no busy card readable under /sys/class/drm"}
 
 
