@@ -1322,16 +1322,22 @@ class ClockLog:
         import glob
         import threading
         self.cards = sorted(glob.glob("/sys/class/drm/card[0-9]*/device"))
-        self.ours = None  # the card of this process's GPU, by PCI address (torch's device properties)
+        self.ours = None  # the card of this process's GPU, by PCI address (hipDeviceGetPCIBusId)
+        self.pci = None
         try:
-            import torch
-            pr = torch.cuda.get_device_properties(device)
-            addr = "%04x:%02x:%02x." % (pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id)
+            import ctypes
+            hip = ctypes.CDLL("libamdhip64.so")  # the runtime libjfsx already loaded into this process
+            buf = ctypes.create_string_buffer(64)
+            if hip.hipDeviceGetPCIBusId(buf, 64, device) != 0:
+                raise RuntimeError("hipDeviceGetPCIBusId failed")
+            self.pci = buf.value.decode().lower().rsplit(".", 1)[0] + "."
             for c in self.cards:
-                if os.path.basename(os.path.realpath(c)).startswith(addr):
+                if os.path.basename(os.path.realpath(c)).startswith(self.pci):
                     self.ours = c.split("/")[-2]
-        except Exception:  # noqa: BLE001 -- diagnostic only: fall back to every busy card
-            pass
+            if self.ours is None:
+                self.pci += " (cards at %s)" % ", ".join(os.path.basename(os.path.realpath(c)) for c in self.cards)
+        except Exception as e:  # noqa: BLE001 -- diagnostic only: fall back to every busy card
+            self.pci = "unknown: %s" % e
         self.period, self.phase, self.samples = period, "warmup", []
         self.ev = threading.Event()
         self.th = threading.Thread(target=self._loop, daemon=True)
@@ -1386,7 +1392,7 @@ class ClockLog:
                 per[phase] = d
             out[card + (" (this GPU)" if card == self.ours else "")] = per
         if out and self.ours is None:
-            out["note"] = "this GPU's card not identified: every busy card is listed"
+            out["note"] = "this GPU's card not identified (PCI %s): every busy card is listed" % self.pci
         return out or {"note": "no busy card readable under /sys/class/drm"}
 
 
