@@ -4,7 +4,7 @@ set -u
 t=${1:-r6ck}
 S="bash scripts/suite.sh $t line"
 A="--mode agg --threads 20 --buffers heap --agg-crc seg --no-cpu --warmup-seconds 3 --steps 10 --log-clocks"
-for i in 1 2 3 4 5 6 7; do
+for i in ${REPS:-1 2 3 4 5 6 7}; do
   $S seal_$i $A --agg-op seal || exit 1
   $S open_$i $A --agg-op open || exit 1
 done
